@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark: strain-vectors/sec of the v0 VAE training step on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], "C2"): v0 preset (hidden 1024, latent 64, linear KL anneal),
+bf16 MFMA GEMMs with fp32 master weights, batch 4096 strain rows per GPU per step, synthetic
+F4-shaped pan-genome matrix 10,000 strains x 55,039 genes resident in HBM (u8). One step = the
+whole hot path of trainer.py:109-120 on one batch: row gather, encoder/decoder forward with
+train-mode BatchNorm, reparameterisation, fused BCE/KL epilogues, full backward, gradient norm +
+clip, Adam. N>1 (torchrun): one process per GPU, each rank steps its own 4096 rows, gradients
+SUM-all-reduced over RCCL every step (weak scaling: value = all ranks' rows / max-rank time).
+
+Also reported (extra fields, not `value`): sampling throughput of `--mode sample` for the v1 preset
+(C3: genomes/s decoded in exact fp32 + thresholded to u8 masks, in HBM), the live-timed dominant
+kernel against the MFMA roofline, and the CPU baseline (the oracle = the reference's algorithm on
+torch-CPU, fp32, all host threads, a bounded sample of the same workload).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "genome-minimizer-2_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
+PEAK_F32_TFLOPS = 157.3     # MI355X fp32 matrix peak
+PEAK_HBM_GBS = 8000.0
+
+
+def train_flops_per_vector(G, H, L):
+    """2*(3*(2GH + 4H^2 + 3HL) - GH) (fwd + dX + dW; no dX for the input layer)."""
+    return 2 * (3 * (2 * G * H + 4 * H * H + 3 * H * L) - G * H)
+
+
+def decode_flops_per_genome(G, H, L):
+    return 2 * (L * H + 2 * H * H + H * G)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--genes", type=int, default=55039)
+    ap.add_argument("--strains", type=int, default=10000)
+    ap.add_argument("--hidden", type=int, default=1024)
+    ap.add_argument("--latent", type=int, default=64)
+    ap.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sample", action="store_true")
+    ap.add_argument("--sample-genomes", type=int, default=262144)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(G, H, L, budget_s):
+    """The oracle (reference algorithm, torch-CPU fp32, autograd) on a bounded sample: v0 preset,
+    one 512-row batch of the same G x H x L model per step, timed for ~budget_s seconds."""
+    sys.path.insert(0, ROOT)
+    from oracle import vae_oracle as O
+    threads = torch.get_num_threads()
+    B = 512
+    torch.manual_seed(0)
+    P = O.init_params(G, H, L)
+    S = O.init_bn_state(H)
+    rng = np.random.Generator(np.random.PCG64(1))
+    x = torch.tensor((rng.random((B, G), dtype=np.float32) < 0.3).astype(np.float32))
+    ls = O.LossState(O.PRESETS["v0"], 10)
+    opt = O.AdamState()
+    t0 = time.perf_counter()
+    O.train_step(P, S, ls, opt, x, torch.randn(B, L), 0)  # warm-up
+    first = time.perf_counter() - t0
+    n = max(1, min(20, int(budget_s / max(first, 1e-3))))
+    t0 = time.perf_counter()
+    for _ in range(n):
+        O.train_step(P, S, ls, opt, x, torch.randn(B, L), 0)
+    dt = time.perf_counter() - t0
+    return {"value": round(B * n / dt, 2), "unit": "strain-vectors/s", "cores": threads, "kind": "port",
+            "sample": f"oracle train_step (torch-CPU fp32 autograd, reference op order), v0 G={G} H={H} L={L}, "
+                      f"{n} steps of 512 rows after 1 warm-up, {dt:.1f}s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from gm2 import native
+    from gm2.data import ResidentMatrix, synthetic_pangenome
+    from gm2.model import VAE
+    from gm2.trainer import Adam
+
+    G, H, L, B = a.genes, a.hidden, a.latent, a.batch
+    prec = native.GM2_BF16 if a.precision == "bf16" else native.GM2_F32
+    x = synthetic_pangenome(a.strains, G, seed=12345 + rank)
+    mat = ResidentMatrix(x, device=dev)
+    del x
+    torch.manual_seed(0)  # identical init on every rank
+    model = VAE(G, H, L, device=dev, precision=prec)
+    opt = Adam(model, lr=1e-3)
+    ws = model.workspace(prec, B)
+    grads = torch.zeros_like(model.params)
+    nsteps = a.warmup + a.steps
+    # per-step scalar table (v0: linear beta over 10000 epochs at epoch 0 -> 0.1; no abundance/L1)
+    tab = np.zeros((nsteps, native.NUM_SCALARS), np.float64)
+    for i in range(nsteps):
+        t = i + 1
+        tab[i, native.S_BETA] = 0.1
+        tab[i, native.S_MAX_NORM] = 1.0
+        tab[i, native.S_NEG_STEP] = -(1e-3 / (1 - 0.9 ** t))
+        tab[i, native.S_BC2_SQRT] = math.sqrt(1 - 0.999 ** t)
+        tab[i, native.S_ONE_MINUS_B1], tab[i, native.S_BETA2] = 1 - 0.9, 0.999
+        tab[i, native.S_ONE_MINUS_B2], tab[i, native.S_ADAM_EPS] = 1 - 0.999, 1e-8
+    scal = torch.tensor(tab, dtype=torch.float32, device=dev)
+    g = torch.Generator().manual_seed(100 + rank)
+    rows = torch.cat([torch.randperm(a.strains, generator=g)[:B] for _ in range(nsteps)]).to(torch.int32).to(dev)
+    loss = torch.zeros(nsteps, native.LOSS_SLOTS, dtype=torch.float64, device=dev)
+    torch.cuda.manual_seed(1)
+
+    def step(i):
+        eps = torch.randn(B, L, device=dev)
+        batch = native.make_batch(mat.data, mat.ld, rows[i * B:(i + 1) * B], B, eps)
+        native.train_fwd_bwd(ws, batch, model.params, grads, model.bn, scal[i], loss[i])
+        if dist is not None:
+            dist.all_reduce(grads)
+        native.grad_norm(ws, model.params, grads, scal[i], loss[i])
+        native.adam_step(ws, model.params, grads, opt.exp_avg, opt.exp_avg_sq, scal[i])
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    native.timing_begin(native.KC_RECON_LOSS)
+    t0 = time.perf_counter()
+    for i in range(a.warmup, nsteps):
+        step(i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    k_ms, k_n = native.timing_end()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    losses = loss.cpu().numpy()
+    if not np.isfinite(losses[:, :3]).all():
+        raise RuntimeError("non-finite loss in the benchmark run")
+    value = world * B * a.steps / elapsed
+    # dominant kernel: decoder output layer GEMM [B,H]x[H,G] + fused BCE/abundance/dlogits epilogue
+    k_avg_ms = k_ms / max(k_n, 1)
+    k_flops = 2.0 * B * H * G
+    achieved = k_flops / (k_avg_ms * 1e-3) / 1e12
+    out = {
+        "metric": "strain-vectors/sec (train+sample), v0 preset, 1/2/4/8 MI355X vs host CPU",
+        "value": round(value, 1), "unit": "strain-vectors/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
+        "config": {"workload": "C2: v0 train step (fwd+bwd+clip+Adam), synthetic pan-genome "
+                               f"{a.strains}x{G} u8 resident, batch {B}/GPU",
+                   "preset": "v0", "genes": G, "hidden": H, "latent": L, "global_batch": B * world,
+                   "parallelism": f"dp{world}"},
+        "train_tflops": round(value * train_flops_per_vector(G, H, L) / 1e12, 2),
+        "roofline": {"bound": "mfma", "kernel": "k_gemm_recon_loss<bf16>" if prec == native.GM2_BF16
+                     else "k_gemm_recon_loss<f32>", "achieved": round(achieved, 1),
+                     "peak": PEAK_BF16_TFLOPS if prec == native.GM2_BF16 else PEAK_F32_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / (PEAK_BF16_TFLOPS if prec == native.GM2_BF16
+                                                                 else PEAK_F32_TFLOPS), 4),
+                     "traffic": None, "launch_ms": round(k_avg_ms, 4), "launches": k_n,
+                     "flops_per_launch": k_flops},
+    }
+    if rank == 0 and not a.no_sample:
+        out["sample"] = sample_bench(a, dev)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(G, H, L, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def sample_bench(a, dev):
+    """C3: v1 preset (hidden 512, latent 32) `--mode sample` decode, genomes/s, masks left in HBM."""
+    from gm2 import native
+    from gm2.model import VAE
+    G, H, L = a.genes, 512, 32
+    torch.manual_seed(0)
+    m = VAE(G, H, L, device=dev, precision=native.GM2_F32)
+    m.eval()
+    chunk = 65536
+    n = a.sample_genomes
+    z = torch.randn(n, L, device=dev)
+    mask = torch.empty(chunk, G, dtype=torch.uint8, device=dev)
+    ws = m.workspace(native.GM2_F32, chunk)
+    native.decode_mask(ws, m.params, m.bn, z[:chunk], chunk, mask, G)  # warm-up
+    torch.cuda.synchronize()
+    native.timing_begin(native.KC_MASK)
+    t0 = time.perf_counter()
+    for s in range(0, n, chunk):
+        k = min(chunk, n - s)
+        native.decode_mask(ws, m.params, m.bn, z[s:s + k], k, mask, G)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    k_ms, k_n = native.timing_end()
+    gps = n / dt
+    kflops = 2.0 * chunk * H * G
+    ach = kflops / (k_ms / max(k_n, 1) * 1e-3) / 1e12
+    return {"genomes_per_s": round(gps, 1), "preset": "v1", "genomes": n, "chunk": chunk, "dtype": "f32",
+            "decode_tflops": round(gps * decode_flops_per_genome(G, H, L) / 1e12, 2),
+            "roofline": {"bound": "mfma", "kernel": "k_gemm_mask<f32>", "achieved": round(ach, 2),
+                         "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_TFLOPS, 4),
+                         "launch_ms": round(k_ms / max(k_n, 1), 4)}}
+
+
+if __name__ == "__main__":
+    main()

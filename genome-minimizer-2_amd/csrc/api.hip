@@ -1,0 +1,533 @@
+// C-ABI of libgm2 (include/gm2.h): workspace layout + the per-step kernel schedule of the VAE
+// train / eval / sample hot path. Host-side only; kernels live in gemm.hip and kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gm2.h"
+#include "gm2_common.hpp"
+#include "gm2_kernels.hpp"
+
+using namespace gm2;
+
+namespace {
+
+thread_local std::string g_err;
+
+#define HIP_OK(x)                                                                                  \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess) throw Gm2Error("%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+  } while (0)
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  } catch (...) {
+    g_err = "unknown error";
+    return -2;
+  }
+}
+
+// reference parameter order (model.py:65-91)
+enum P {
+  E0W, E0B, E1G, E1BT, E3W, E3B, E4G, E4BT, E6W, E6B, E7G, E7BT, MUW, MUB, LVW, LVB,
+  D0W, D0B, D1G, D1BT, D3W, D3B, D4G, D4BT, D6W, D6B, D7G, D7BT, D9W, D9B, NP
+};
+static_assert(NP == GM2_NUM_PARAMS, "param count");
+
+struct Dims {
+  int64_t G, H, L, Bm;
+  int64_t Gp, Lp, K2L, L2r, Lr;
+  int64_t off[NP + 1];
+};
+
+Dims make_dims(const gm2_dims* d) {
+  if (!d) throw Gm2Error("null dims");
+  Dims x;
+  x.G = d->G, x.H = d->H, x.L = d->L;
+  if (x.G <= 0 || x.H <= 0 || x.L <= 0 || d->batch_max <= 0) throw Gm2Error("dims must be positive");
+  if (x.H % kTile) throw Gm2Error("hidden_dim %lld must be a multiple of 128", (long long)x.H);
+  if (256 % x.L) throw Gm2Error("latent_dim %lld must divide 256", (long long)x.L);
+  x.Bm = round_up(d->batch_max, kTile);
+  x.Gp = round_up(x.G, kTile);
+  x.Lp = round_up(x.L, kKPad);
+  x.K2L = round_up(2 * x.L, kKPad);
+  x.L2r = round_up(2 * x.L, kTile);
+  x.Lr = round_up(x.Lp, kTile);
+  const int64_t G = x.G, H = x.H, L = x.L;
+  const int64_t sz[NP] = {H * G, H, H, H, H * H, H, H, H, H * H, H, H, H, L * H, L, L * H, L,
+                          H * L, H, H, H, H * H, H, H, H, H * H, H, H, H, G * H, G};
+  x.off[0] = 0;
+  for (int i = 0; i < NP; ++i) x.off[i + 1] = x.off[i] + sz[i];
+  return x;
+}
+
+// ---------------------------------------------------------------------------------------------
+// workspace layout (bytes). Everything 256-B aligned. Element size es = 4 (F32) or 2 (BF16).
+// ---------------------------------------------------------------------------------------------
+struct Layout {
+  Dims d;
+  int prec;
+  int64_t es;
+  // GEMM shadows (T)
+  int64_t sE0, sE1, sE1T, sE2, sE2T, sHD, sHDT, sD0, sD0T, sD1, sD1T, sD2, sD2T, sD3, sD3T;
+  int64_t X, XT, Y[6], A[6], AT[6], save[6], HD, Z, ZT, dL, dLT, slabs, slab_cap, dY, dYT, dH, dHT;
+  int64_t bnpart, colpart, colpart_cap, losspart, losspart_cap, klpart, gradpart, clip, total;
+};
+
+Layout make_layout(const gm2_dims* gd, int prec) {
+  if (prec != GM2_F32 && prec != GM2_BF16) throw Gm2Error("bad precision %d", prec);
+  Layout o;
+  o.d = make_dims(gd);
+  o.prec = prec;
+  o.es = prec == GM2_F32 ? 4 : 2;
+  const Dims& d = o.d;
+  int64_t cur = 0;
+  auto take = [&](int64_t bytes) {
+    const int64_t at = cur;
+    cur += round_up(bytes, 256);
+    return at;
+  };
+  const int64_t es = o.es, H = d.H, Bm = d.Bm;
+  o.sE0 = take(H * d.Gp * es);
+  o.sE1 = take(H * H * es);
+  o.sE1T = take(H * H * es);
+  o.sE2 = take(H * H * es);
+  o.sE2T = take(H * H * es);
+  o.sHD = take(d.L2r * H * es);
+  o.sHDT = take(H * d.K2L * es);
+  o.sD0 = take(H * d.Lp * es);
+  o.sD0T = take(d.Lr * H * es);
+  o.sD1 = take(H * H * es);
+  o.sD1T = take(H * H * es);
+  o.sD2 = take(H * H * es);
+  o.sD2T = take(H * H * es);
+  o.sD3 = take(d.Gp * H * es);
+  o.sD3T = take(H * d.Gp * es);
+  o.X = take(Bm * d.Gp * es);
+  o.XT = take(d.Gp * Bm * es);
+  for (int i = 0; i < 6; ++i) {
+    o.Y[i] = take(Bm * H * 4);
+    o.A[i] = take(Bm * H * es);
+    o.AT[i] = take(H * Bm * es);
+    o.save[i] = take(2 * H * 4);
+  }
+  o.HD = take(Bm * 2 * d.L * 4);
+  o.Z = take(Bm * d.Lp * es);
+  o.ZT = take(d.Lr * Bm * es);
+  o.dL = take(Bm * d.Gp * es);
+  o.dLT = take(d.Gp * Bm * es);
+  const int64_t maxN = std::max<int64_t>({H, 2 * d.L, d.Lp, 128});
+  o.slab_cap = std::max<int64_t>(1024LL * kTile * kTile, Bm * maxN);
+  o.slabs = take(o.slab_cap * 4);
+  o.dY = take(Bm * H * es);
+  o.dYT = take(H * Bm * es);
+  o.dH = take(Bm * d.K2L * es);
+  o.dHT = take(d.L2r * Bm * es);
+  o.bnpart = take((Bm / kBnRowChunk) * H * 8);
+  o.colpart_cap = std::max<int64_t>({(Bm / kTile) * d.Gp, (Bm / 64) * H, (Bm / 64) * 2 * d.L});
+  o.colpart = take(o.colpart_cap * 4);
+  o.losspart_cap = std::max<int64_t>((d.Gp / kTile) * (Bm / kTile) * 2, Bm / 64);
+  o.losspart = take(o.losspart_cap * 4);
+  o.klpart = take((Bm / 64) * 4);
+  o.gradpart = take(2048 * 2 * 8);
+  o.clip = take(64);
+  o.total = cur;
+  return o;
+}
+
+template <typename T>
+struct Ctx {
+  const Layout& lo;
+  char* ws;
+  hipStream_t s;
+  const Dims& d;
+  Ctx(const Layout& l, void* w, void* st) : lo(l), ws((char*)w), s((hipStream_t)st), d(l.d) {}
+  T* t(int64_t off) const { return (T*)(ws + off); }
+  float* f(int64_t off) const { return (float*)(ws + off); }
+};
+
+int pick_splits(int tm, int tn, int nk) {
+  const int tiles = tm * tn;
+  int s = (512 + tiles - 1) / tiles;
+  s = std::min(s, 8);
+  s = std::min(s, std::max(1, nk / 4));
+  return std::max(1, s);
+}
+
+// GEMM into the fp32 slab scratch (split-K slices summed by the consumer). Returns #slabs.
+template <typename T>
+int gemm_to_slabs(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64_t ldq, int Np, int M, int N,
+                  int K, int64_t ldc) {
+  GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0};
+  const int S = pick_splits(Mp / kTile, Np / kTile, K / E<T>::KT);
+  const int64_t slab = (int64_t)Mp * ldc;
+  if ((int64_t)S * slab > c.lo.slab_cap) throw Gm2Error("slab capacity exceeded");
+  return launch_gemm_store<T>(g, S, c.f(c.lo.slabs), nullptr, 0, ldc, slab, nullptr, c.s);
+}
+
+template <typename T>
+void gemm_to(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64_t ldq, int Np, int M, int N, int K,
+             float* C0, float* C1, int msplit, int64_t ldc) {
+  GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0};
+  launch_gemm_store<T>(g, 1, C0, C1, msplit, ldc, 0, nullptr, c.s);
+}
+
+// the 6 BatchNorm blocks: (linear weight, linear bias, bn gamma, bn beta)
+const int kBlk[6][4] = {{E0W, E0B, E1G, E1BT}, {E3W, E3B, E4G, E4BT}, {E6W, E6B, E7G, E7BT},
+                        {D0W, D0B, D1G, D1BT}, {D3W, D3B, D4G, D4BT}, {D6W, D6B, D7G, D7BT}};
+
+template <typename T>
+TensorTable make_table(const Ctx<T>& c) {
+  const Dims& d = c.d;
+  const Layout& l = c.lo;
+  TensorTable tt{};
+  auto add = [&](int pi, int64_t rows, int64_t cols, int64_t sh, int64_t sld, int64_t srow0, int64_t shT,
+                 int64_t tld) {
+    TensorDesc& e = tt.t[tt.n];
+    e.off = d.off[pi];
+    e.rows = rows;
+    e.cols = cols;
+    e.shadow = sh >= 0 ? (void*)(c.ws + sh) : nullptr;
+    e.sld = sld;
+    e.srow0 = srow0;
+    e.shadowT = shT >= 0 ? (void*)(c.ws + shT) : nullptr;
+    e.tld = tld;
+    e.tile0 = tt.n == 0 ? 0
+                        : tt.t[tt.n - 1].tile0 + ((tt.t[tt.n - 1].rows + 63) / 64) * ((tt.t[tt.n - 1].cols + 63) / 64);
+    tt.n++;
+  };
+  const int64_t H = d.H, G = d.G, L = d.L;
+  add(E0W, H, G, l.sE0, d.Gp, 0, -1, 0);
+  add(E3W, H, H, l.sE1, H, 0, l.sE1T, H);
+  add(E6W, H, H, l.sE2, H, 0, l.sE2T, H);
+  add(MUW, L, H, l.sHD, H, 0, l.sHDT, d.K2L);
+  add(LVW, L, H, l.sHD, H, L, l.sHDT, d.K2L);
+  add(D0W, H, L, l.sD0, d.Lp, 0, l.sD0T, H);
+  add(D3W, H, H, l.sD1, H, 0, l.sD1T, H);
+  add(D6W, H, H, l.sD2, H, 0, l.sD2T, H);
+  add(D9W, G, H, l.sD3, H, 0, l.sD3T, d.Gp);
+  return tt;
+}
+
+// ---------------------------------------------------------------------------------------------
+// forward (train or eval). Fills A_l (+A_l^T when train), Y_l, save_l, HD, Z, ZT and runs the
+// fused reconstruction-loss epilogue (dL, dL^T when with_grad).
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, int train, int with_grad,
+             const float* scal, double* loss, float* grads) {
+  const Dims& d = c.d;
+  const Layout& l = c.lo;
+  const int B = (int)b->n;
+  if (B <= 0 || B > d.Bm) throw Gm2Error("batch rows %d outside (0, batch_max=%lld]", B, (long long)d.Bm);
+  if (train && B < 2) throw Gm2Error("Expected more than 1 value per channel when training (batch of 1)");
+  if (!b->data) throw Gm2Error("null data");
+  const int Bp = (int)round_up(B, kTile);
+  const int H = (int)d.H, L = (int)d.L;
+  // 1) strain rows -> X, X^T
+  launch_gather_rows<T>(b->data, b->ld_data, b->rows, B, (int)d.G, c.t(l.X), d.Gp, (int)d.Gp, c.t(l.XT), d.Bm, Bp,
+                        c.s);
+  // 2) encoder blocks
+  const T* in = c.t(l.X);
+  int64_t ldin = d.Gp;
+  int Kin = (int)d.Gp;
+  const int64_t shadow_in[6] = {l.sE0, l.sE1, l.sE2, l.sD0, l.sD1, l.sD2};
+  for (int i = 0; i < 6; ++i) {
+    if (i == 3) {  // heads + reparameterization between encoder and decoder
+      const int S = gemm_to_slabs<T>(c, c.t(l.A[2]), H, Bp, c.t(l.sHD), H, (int)d.L2r, B, 2 * L, H, 2 * L);
+      launch_reparam<T>(c.f(l.slabs), S, (int64_t)Bp * 2 * L, L, prm + d.off[MUB], prm + d.off[LVB], b->eps, B, Bp,
+                        c.f(l.HD), c.t(l.Z), d.Lp, c.t(l.ZT), d.Bm, (int)d.Lr, c.f(l.klpart), c.s);
+      in = c.t(l.Z);
+      ldin = d.Lp;
+      Kin = (int)d.Lp;
+    }
+    const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(shadow_in[i]), Kin, H, B, H, Kin, H);
+    launch_bn_fwd_partial(c.f(l.slabs), S, (int64_t)Bp * H, H, prm + d.off[kBlk[i][1]], B, H, c.f(l.Y[i]),
+                          c.f(l.bnpart), c.s);
+    launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train, prm + d.off[kBlk[i][2]],
+                           prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
+                           c.f(l.save[i]), c.t(l.A[i]), train ? c.t(l.AT[i]) : nullptr, d.Bm, c.s);
+    in = c.t(l.A[i]);
+    ldin = H;
+    Kin = H;
+  }
+  // 3) output layer + reconstruction loss (+ dlogits)
+  GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, B, (int)d.G, H, Bp, (int)d.Gp, 0};
+  launch_gemm_recon_loss<T>(g, prm + d.off[D9B], c.t(l.X), d.Gp, with_grad, scal, c.t(l.dL), d.Gp, c.t(l.dLT), d.Bm,
+                            c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
+  const int nblk = gemm_recon_grid_blocks<T>(g);
+  launch_reduce_to(c.f(l.losspart), nblk, 2, 2, loss + 0, c.s);
+  launch_reduce_to(c.f(l.klpart), Bp / 64, 1, 1, loss + 2, c.s);
+  if (with_grad) launch_colsum(c.f(l.colpart), Bp / kTile, d.Gp, (int)d.G, grads + d.off[D9B], nullptr, 0, c.s);
+}
+
+template <typename T>
+void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, const float* scal) {
+  const Dims& d = c.d;
+  const Layout& l = c.lo;
+  const int B = (int)b->n, Bp = (int)round_up(B, kTile);
+  const int H = (int)d.H, L = (int)d.L, G = (int)d.G;
+  const int64_t Bm = d.Bm;
+  // output layer: dW9 = dL^T . A5 ; dA5 = dL . W9
+  gemm_to<T>(c, c.t(l.dLT), Bm, (int)d.Gp, c.t(l.AT[5]), Bm, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H);
+  int S = gemm_to_slabs<T>(c, c.t(l.dL), d.Gp, Bp, c.t(l.sD3T), d.Gp, H, B, H, (int)d.Gp, H);
+  const int64_t shadowT[6] = {-1, l.sE1T, l.sE2T, l.sD0T, l.sD1T, l.sD2T};
+  for (int i = 5; i >= 0; --i) {
+    const int64_t slab = (int64_t)Bp * (i == 2 ? H : H);
+    launch_bn_bwd_partial(c.f(l.slabs), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
+                          prm + d.off[kBlk[i][3]], B, H, c.f(l.bnpart), c.s);
+    launch_bn_bwd_apply<T>(c.f(l.slabs), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
+                           prm + d.off[kBlk[i][3]], c.f(l.bnpart), B, Bp, H, gr + d.off[kBlk[i][2]],
+                           gr + d.off[kBlk[i][3]], c.t(l.dY), c.t(l.dYT), Bm, c.f(l.colpart), c.s);
+    launch_colsum(c.f(l.colpart), Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, c.s);
+    // weight gradient of this block's Linear: dW = dY^T . in^T
+    if (i == 0) {
+      gemm_to<T>(c, c.t(l.dYT), Bm, H, c.t(l.XT), Bm, (int)d.Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G);
+      break;
+    }
+    if (i == 3) {
+      gemm_to<T>(c, c.t(l.dYT), Bm, H, c.t(l.ZT), Bm, (int)d.Lr, H, L, Bp, gr + d.off[D0W], nullptr, 0, L);
+      // dz = dY3 . W_d0  -> reparam backward -> dH (mu | logvar)
+      S = gemm_to_slabs<T>(c, c.t(l.dY), H, Bp, c.t(l.sD0T), H, (int)d.Lr, B, L, H, L);
+      launch_reparam_bwd<T>(c.f(l.slabs), S, (int64_t)Bp * L, L, c.f(l.HD), b->eps, scal, B, Bp, L, c.t(l.dH), d.K2L,
+                            c.t(l.dHT), Bm, (int)d.L2r, c.f(l.colpart), c.s);
+      launch_colsum(c.f(l.colpart), Bp / 64, 2 * L, 2 * L, gr + d.off[MUB], gr + d.off[LVB], L, c.s);
+      gemm_to<T>(c, c.t(l.dHT), Bm, (int)d.L2r, c.t(l.AT[2]), Bm, H, 2 * L, H, Bp, gr + d.off[MUW],
+                 gr + d.off[LVW], L, H);
+      S = gemm_to_slabs<T>(c, c.t(l.dH), d.K2L, Bp, c.t(l.sHDT), d.K2L, H, B, H, (int)d.K2L, H);
+      continue;
+    }
+    gemm_to<T>(c, c.t(l.dYT), Bm, H, c.t(l.AT[i - 1]), Bm, H, H, H, Bp, gr + d.off[kBlk[i][0]], nullptr, 0, H);
+    S = gemm_to_slabs<T>(c, c.t(l.dY), H, Bp, c.t(shadowT[i]), H, H, B, H, H, H);
+  }
+}
+
+template <typename T>
+void decode_chain(const Ctx<T>& c, const float* prm, float* bn, int n, uint8_t* mask, int64_t ldm, float* probs,
+                  int64_t ldpr) {
+  const Dims& d = c.d;
+  const Layout& l = c.lo;
+  const int Bp = (int)round_up(n, kTile), H = (int)d.H;
+  const T* in = c.t(l.Z);
+  int64_t ldin = d.Lp;
+  int Kin = (int)d.Lp;
+  const int64_t shadow_in[3] = {l.sD0, l.sD1, l.sD2};
+  for (int j = 0; j < 3; ++j) {
+    const int i = 3 + j;
+    const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(shadow_in[j]), Kin, H, n, H, Kin, H);
+    launch_bn_fwd_partial(c.f(l.slabs), S, (int64_t)Bp * H, H, prm + d.off[kBlk[i][1]], n, H, c.f(l.Y[i]),
+                          c.f(l.bnpart), c.s);
+    launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), n, Bp, H, 0, prm + d.off[kBlk[i][2]],
+                           prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, nullptr,
+                           c.t(l.A[i]), nullptr, d.Bm, c.s);
+    in = c.t(l.A[i]);
+    ldin = H;
+    Kin = H;
+  }
+  GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, n, (int)d.G, H, Bp, (int)d.Gp, 0};
+  launch_gemm_mask<T>(g, prm + d.off[D9B], mask, ldm, probs, ldpr, c.s);
+}
+
+template <typename T>
+void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr, float* bn, const float* scal,
+               double* loss, void* ws, void* st) {
+  Ctx<T> c(lo, ws, st);
+  forward<T>(c, b, prm, bn, 1, 1, scal, loss, gr);
+  backward<T>(c, b, prm, gr, scal);
+}
+
+}  // namespace
+
+// =================================================================================================
+extern "C" {
+
+const char* gm2_last_error(void) { return g_err.c_str(); }
+int gm2_abi_version(void) { return GM2_ABI_VERSION; }
+
+int gm2_param_count(const gm2_dims* d, int64_t* n) {
+  return guarded([&] { *n = make_dims(d).off[NP]; });
+}
+
+int gm2_param_offsets(const gm2_dims* d, int64_t* off) {
+  return guarded([&] {
+    const Dims x = make_dims(d);
+    for (int i = 0; i <= NP; ++i) off[i] = x.off[i];
+  });
+}
+
+int gm2_workspace_size(const gm2_dims* d, int prec, size_t* bytes) {
+  return guarded([&] { *bytes = (size_t)make_layout(d, prec).total; });
+}
+
+int gm2_workspace_init(const gm2_dims* d, int prec, void* ws, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    const Layout lo = make_layout(d, prec);
+    if ((size_t)lo.total > ws_bytes) throw Gm2Error("workspace too small: %zu < %lld", ws_bytes, (long long)lo.total);
+    if ((uintptr_t)ws & 255) throw Gm2Error("workspace must be 256-B aligned");
+    HIP_OK(hipMemsetAsync(ws, 0, (size_t)lo.total, (hipStream_t)stream));
+  });
+}
+
+int gm2_sync_shadows(const gm2_dims* d, int prec, const float* params, void* ws, void* stream) {
+  return guarded([&] {
+    const Layout lo = make_layout(d, prec);
+    if (prec == GM2_F32) {
+      Ctx<float> c(lo, ws, stream);
+      launch_shadow_sync<float>(make_table(c), params, c.s);
+    } else {
+      Ctx<bf16_t> c(lo, ws, stream);
+      launch_shadow_sync<bf16_t>(make_table(c), params, c.s);
+    }
+  });
+}
+
+int gm2_train_fwd_bwd(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, float* grads,
+                      float* bn_running, const float* scalars, double* loss, void* ws, void* stream) {
+  return guarded([&] {
+    const Layout lo = make_layout(d, prec);
+    if (prec == GM2_F32) run_train<float>(lo, batch, params, grads, bn_running, scalars, loss, ws, stream);
+    else run_train<bf16_t>(lo, batch, params, grads, bn_running, scalars, loss, ws, stream);
+  });
+}
+
+int gm2_grad_norm(const gm2_dims* d, int prec, const float* params, const float* grads, const float* scalars,
+                  double* loss, void* ws, void* stream) {
+  return guarded([&] {
+    const Layout lo = make_layout(d, prec);
+    const int64_t n = lo.d.off[NP];
+    const int nb = grad_stats_blocks(n);
+    double* part = (double*)((char*)ws + lo.gradpart);
+    float* clip = (float*)((char*)ws + lo.clip);
+    launch_grad_stats(params, grads, n, scalars, part, nb, (hipStream_t)stream);
+    launch_grad_finalize(part, nb, scalars, clip, loss + 3, (hipStream_t)stream);
+    // loss[4] = norm (fp32 -> fp64) via a tiny copy kernel-free path: reuse reduce_to on clip[1]
+    launch_reduce_to(clip + 1, 1, 1, 1, loss + 4, (hipStream_t)stream);
+  });
+}
+
+int gm2_adam_step(const gm2_dims* d, int prec, float* params, const float* grads, float* m, float* v,
+                  const float* scalars, void* ws, void* stream) {
+  return guarded([&] {
+    const Layout lo = make_layout(d, prec);
+    const int64_t n = lo.d.off[NP];
+    const float* clip = (const float*)((char*)ws + lo.clip);
+    launch_adam(grads, params, m, v, n, scalars, clip, (hipStream_t)stream);
+    if (prec == GM2_F32) {
+      Ctx<float> c(lo, ws, stream);
+      launch_shadow_sync<float>(make_table(c), params, c.s);
+    } else {
+      Ctx<bf16_t> c(lo, ws, stream);
+      launch_shadow_sync<bf16_t>(make_table(c), params, c.s);
+    }
+  });
+}
+
+int gm2_eval_forward(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params,
+                     const float* bn_running, const float* scalars, double* loss, void* ws, void* stream) {
+  return guarded([&] {
+    const Layout lo = make_layout(d, prec);
+    float* bn = const_cast<float*>(bn_running);  // eval mode never writes running stats
+    if (prec == GM2_F32) {
+      Ctx<float> c(lo, ws, stream);
+      forward<float>(c, batch, params, bn, 0, 0, scalars, loss, nullptr);
+    } else {
+      Ctx<bf16_t> c(lo, ws, stream);
+      forward<bf16_t>(c, batch, params, bn, 0, 0, scalars, loss, nullptr);
+    }
+  });
+}
+
+int gm2_decode_mask(const gm2_dims* d, const float* params, const float* bn_running, const float* z, int64_t n,
+                    uint8_t* mask, int64_t ld_mask, float* probs, int64_t ld_probs, void* ws, void* stream) {
+  return guarded([&] {
+    const Layout lo = make_layout(d, GM2_F32);
+    if (n <= 0 || n > lo.d.Bm) throw Gm2Error("decode rows %lld outside (0, batch_max]", (long long)n);
+    if (ld_mask < lo.d.G || (probs && ld_probs < lo.d.G)) throw Gm2Error("decode: ld < G");
+    Ctx<float> c(lo, ws, stream);
+    // z [n][L] -> Z [Bm][Lp] (pad columns stay zero from workspace init)
+    HIP_OK(hipMemcpy2DAsync(c.f(lo.Z), lo.d.Lp * 4, z, lo.d.L * 4, lo.d.L * 4, n, hipMemcpyDeviceToDevice, c.s));
+    decode_chain<float>(c, params, const_cast<float*>(bn_running), (int)n, mask, ld_mask, probs, ld_probs);
+  });
+}
+
+int gm2_encode(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, const float* bn_running,
+               float* mu, float* logvar, void* ws, void* stream) {
+  return guarded([&] {
+    const Layout lo = make_layout(d, prec);
+    gm2_batch b = *batch;
+    auto run = [&](auto tag) {
+      using T = decltype(tag);
+      Ctx<T> c(lo, ws, stream);
+      const Dims& dd = c.d;
+      const int B = (int)b.n, Bp = (int)round_up(B, kTile), H = (int)dd.H, L = (int)dd.L;
+      if (B <= 0 || B > dd.Bm) throw Gm2Error("encode rows outside (0, batch_max]");
+      float* bn = const_cast<float*>(bn_running);
+      launch_gather_rows<T>(b.data, b.ld_data, b.rows, B, (int)dd.G, c.t(lo.X), dd.Gp, (int)dd.Gp, c.t(lo.XT), dd.Bm,
+                            Bp, c.s);
+      const T* in = c.t(lo.X);
+      int64_t ldin = dd.Gp;
+      int Kin = (int)dd.Gp;
+      const int64_t sh[3] = {lo.sE0, lo.sE1, lo.sE2};
+      for (int i = 0; i < 3; ++i) {
+        const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(sh[i]), Kin, H, B, H, Kin, H);
+        launch_bn_fwd_partial(c.f(lo.slabs), S, (int64_t)Bp * H, H, params + dd.off[kBlk[i][1]], B, H, c.f(lo.Y[i]),
+                              c.f(lo.bnpart), c.s);
+        launch_bn_fwd_apply<T>(c.f(lo.Y[i]), H, c.f(lo.bnpart), B, Bp, H, 0, params + dd.off[kBlk[i][2]],
+                               params + dd.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
+                               nullptr, c.t(lo.A[i]), nullptr, dd.Bm, c.s);
+        in = c.t(lo.A[i]);
+        ldin = H;
+        Kin = H;
+      }
+      const int S = gemm_to_slabs<T>(c, c.t(lo.A[2]), H, Bp, c.t(lo.sHD), H, (int)dd.L2r, B, 2 * L, H, 2 * L);
+      launch_reparam<T>(c.f(lo.slabs), S, (int64_t)Bp * 2 * L, L, params + dd.off[MUB], params + dd.off[LVB], nullptr,
+                        B, Bp, c.f(lo.HD), c.t(lo.Z), dd.Lp, c.t(lo.ZT), dd.Bm, (int)dd.Lr, c.f(lo.klpart), c.s);
+      if (mu) HIP_OK(hipMemcpy2DAsync(mu, L * 4, c.f(lo.HD), 2 * L * 4, L * 4, B, hipMemcpyDeviceToDevice, c.s));
+      if (logvar)
+        HIP_OK(hipMemcpy2DAsync(logvar, L * 4, c.f(lo.HD) + L, 2 * L * 4, L * 4, B, hipMemcpyDeviceToDevice, c.s));
+    };
+    if (prec == GM2_F32) run(float{});
+    else run(bf16_t{});
+  });
+}
+
+int gm2_gemm_nt(int prec, const void* P, int64_t ldp, const void* Q, int64_t ldq, float* C, int64_t ldc, int64_t M,
+                int64_t N, int64_t K, int splits, float* slab_ws, void* stream) {
+  return guarded([&] {
+    auto run = [&](auto tag) {
+      using T = decltype(tag);
+      GemmArgs<T> g{(const T*)P, ldp, (const T*)Q, ldq, (int)M, (int)N, (int)K, (int)round_up(M, kTile),
+                    (int)round_up(N, kTile), 0};
+      if (splits <= 1) {
+        launch_gemm_store<T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, (hipStream_t)stream);
+      } else {
+        const int S = launch_gemm_store<T>(g, splits, slab_ws, nullptr, 0, ldc, (int64_t)M * ldc, nullptr,
+                                           (hipStream_t)stream);
+        // sum the slabs column-block-wise: treat [S][M*ldc] as rows
+        launch_colsum(slab_ws, S, M * ldc, (int)(M * ldc), C, nullptr, 0, (hipStream_t)stream);
+      }
+    };
+    if (prec == GM2_F32) run(float{});
+    else if (prec == GM2_BF16) run(bf16_t{});
+    else throw Gm2Error("bad precision");
+  });
+}
+
+int gm2_timing_begin(int kernel_classes) {
+  return guarded([&] { timing_begin(kernel_classes); });
+}
+
+int gm2_timing_end(double* total_ms, int64_t* launches) {
+  return guarded([&] { timing_end(total_ms, launches); });
+}
+
+}  // extern "C"

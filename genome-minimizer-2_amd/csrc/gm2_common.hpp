@@ -1,0 +1,51 @@
+// Shared device helpers for libgm2 (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gm2 {
+
+typedef uint16_t bf16_t;  // bf16 storage type (bit pattern)
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int kWave = 64;
+constexpr int kTile = 128;   // GEMM block tile (M and N); every operand's row count is padded to it
+constexpr int kKPad = 64;    // K padding of every operand (covers bf16 BK=64 and f32 BK=32)
+
+__host__ __device__ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 (RNE, NaN preserved) on gfx950
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+// element-type adaptors: T is float (exact fp32 path) or bf16_t (bf16 MFMA path)
+template <typename T> struct E;
+template <> struct E<float> {
+  static constexpr int KT = 32;  // K elements per 128-byte LDS row chunk
+  __device__ static __forceinline__ float ld(const float* p) { return *p; }
+  __device__ static __forceinline__ float cvt(float v) { return v; }
+};
+template <> struct E<bf16_t> {
+  static constexpr int KT = 64;
+  __device__ static __forceinline__ float ld(const bf16_t* p) { return bf2f(*p); }
+  __device__ static __forceinline__ bf16_t cvt(float v) { return f2bf(v); }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// sigmoid_fp32(l) > 0.5  <=>  l > 0x33C00000 (pinned against the reference in tests/golden)
+constexpr float kMaskLogitThreshold = 8.940696716308594e-08f;
+
+}  // namespace gm2

@@ -1,0 +1,158 @@
+// Internal kernel launchers of libgm2 (host side). Public C-ABI: include/gm2.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+
+#include "gm2_common.hpp"
+
+namespace gm2 {
+
+struct Gm2Error : std::runtime_error {
+  explicit Gm2Error(const std::string& s) : std::runtime_error(s) {}
+  template <typename... A>
+  Gm2Error(const char* fmt, A... a) : std::runtime_error(fmt_str(fmt, a...)) {}
+  template <typename... A>
+  static std::string fmt_str(const char* fmt, A... a) {
+    char buf[512];
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wformat-security"
+    snprintf(buf, sizeof buf, fmt, a...);
+#pragma clang diagnostic pop
+    return buf;
+  }
+};
+
+#define GM2_CHECK_LAUNCH()                                                                     \
+  do {                                                                                         \
+    hipError_t e_ = hipGetLastError();                                                         \
+    if (e_ != hipSuccess) throw ::gm2::Gm2Error("%s:%d launch: %s", __FILE__, __LINE__,       \
+                                                hipGetErrorString(e_));                        \
+  } while (0)
+
+// indices into the per-step device scalar block (float[kNumScal]); written by the host
+enum Scal {
+  kScalBeta = 0,       // KL weight beta (loss_components.py:76-88)
+  kScalWGamma = 1,     // weight * gamma of the gene-abundance term (0: component absent)
+  kScalLambda = 2,     // lambda_l1 (0: component absent)
+  kScalNegStep = 3,    // -lr / (1 - beta1^t)             (Adam step_size, negated)
+  kScalBc2Sqrt = 4,    // sqrt(1 - beta2^t)
+  kScalMaxNorm = 5,    // clip_grad_norm_ max_norm (<= 0: no clipping)
+  kScalOneMinusB1 = 6, // 1 - beta1  (Adam: exp_avg.lerp_(grad, 1 - beta1))
+  kScalBeta2 = 7,       // beta2       (exp_avg_sq.mul_(beta2).addcmul_(g, g, value=1 - beta2))
+  kScalOneMinusB2 = 8,
+  kScalAdamEps = 9,
+  kNumScal = 16
+};
+
+template <typename T>
+struct GemmArgs {
+  const T* P;
+  int64_t ldp;
+  const T* Q;
+  int64_t ldq;
+  int M, N, K;   // logical sizes (K already padded to 64, pads zero)
+  int Mp, Np;    // allocated row counts of P / Q (multiples of 128)
+  int k_per_split;
+};
+
+// ---- live per-kernel timing (bench.py): hipEvent pairs around every launch of one class ----
+enum KernelClass { kKcReconLoss = 1, kKcGemmStore = 2, kKcMask = 4 };
+void timing_begin(int classes);
+void timing_end(double* total_ms, int64_t* launches);
+struct TimedLaunch {  // records an event pair around a launch when its class is being timed
+  TimedLaunch(int cls, hipStream_t s);
+  ~TimedLaunch();
+  int idx;
+  hipStream_t s;
+};
+
+// ---- gemm.hip ----
+template <typename T>
+int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc,
+                      int64_t slab, const float* bias, hipStream_t s);
+template <typename T>
+int gemm_recon_grid_blocks(const GemmArgs<T>& g);
+template <typename T>
+void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const T* X, int64_t ldx, int with_grad,
+                            const float* scal, T* dL, int64_t ldd, T* dLT, int64_t lddt, float* loss_part,
+                            float* colpart, int64_t ldcol, hipStream_t s);
+template <typename T>
+void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs,
+                      int64_t ldpr, hipStream_t s);
+
+// ---- kernels.hip ----
+constexpr int kBnRowChunk = 128;  // rows per BatchNorm partial-statistics chunk
+
+// gather strain rows of the resident u8 matrix into X [Bp][ldx] and X^T [ldxt rows][Bp] (T);
+// zero-fills columns >= G and rows >= B up to the padded extents
+template <typename T>
+void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* rows, int B, int G, T* X, int64_t ldx,
+                        int Gp, T* XT, int64_t ldxt, int Bp, hipStream_t s);
+
+// BN forward: y = sum of S slabs + bias -> Y; per-chunk (mean, M2) partials
+void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, const float* bias, int B, int H,
+                           float* Y, float* part, hipStream_t s);
+// BN forward apply (train: batch stats from partials + running-stat update; eval: running stats)
+template <typename T>
+void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
+                         const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,
+                         T* AT, int64_t ldat, hipStream_t s);
+// BN backward: partials of sum(do), sum((y-mean)*do) with do = dA * [bn_out > 0]
+void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
+                           const float* gamma, const float* beta, int B, int H, float* part, hipStream_t s);
+template <typename T>
+void launch_bn_bwd_apply(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
+                         const float* gamma, const float* beta, const float* part, int B, int Bp, int H,
+                         float* dgamma, float* dbeta, T* dY, T* dYT, int64_t ldyt, float* colpart,
+                         hipStream_t s);
+// reparameterization + KL (model.py:100-104, loss_components.py:77)
+template <typename T>
+void launch_reparam(const float* slabs, int S, int64_t slab, int L, const float* bmu, const float* blv,
+                    const float* eps, int B, int Bp, float* HD, T* Z, int64_t ldz, T* ZT, int64_t ldzt, int Lrows,
+                    float* kl_part, hipStream_t s);
+template <typename T>
+void launch_reparam_bwd(const float* dzslabs, int S, int64_t slab, int64_t ldslab, const float* HD,
+                        const float* eps, const float* scal, int B, int Bp, int L, T* dH, int64_t ldh, T* dHT,
+                        int64_t ldht, int Hrows, float* colpart, hipStream_t s);
+// out[n] = sum_r part[r*ld + n]  (deterministic order)
+void launch_colsum(const float* part, int rows, int64_t ld, int n, float* out0, float* out1, int nsplit,
+                   hipStream_t s);
+// out[i] = sum of partial buffers in double, fixed order (loss record slots)
+void launch_reduce_to(const float* part, int n, int stride, int count, double* out, hipStream_t s);
+
+// parameter tensor table for the multi-tensor optimizer / shadow kernels
+struct TensorDesc {
+  int64_t off;        // offset in the flat fp32 param/grad/m/v buffers
+  int64_t rows, cols;
+  void* shadow;       // padded GEMM copy (T) [.. rows ..][sld] or nullptr
+  int64_t sld;
+  int64_t srow0;      // first shadow row of this tensor (mean/logvar share one shadow)
+  void* shadowT;      // transposed padded copy [cols][tld] or nullptr
+  int64_t tld;
+  int64_t tile0;      // first 64x64 tile of this tensor in the shadow-sync grid
+};
+constexpr int kMaxTensors = 32;
+struct TensorTable {
+  int n;
+  TensorDesc t[kMaxTensors];
+};
+
+template <typename T>
+void launch_shadow_sync(const TensorTable& tt, const float* params, hipStream_t s);
+// sum((g + lambda*sign(p))^2) and sum(|p|) over all params -> partials; then finalize
+void launch_grad_stats(const float* params, const float* grads, int64_t n, const float* scal, double* part,
+                       int nblocks, hipStream_t s);
+void launch_grad_finalize(const double* part, int nblocks, const float* scal, float* clip_out,
+                          double* loss_l1abs, hipStream_t s);
+void launch_adam(const float* grads, float* params, float* m, float* v, int64_t n, const float* scal,
+                 const float* clip, hipStream_t s);
+
+int grad_stats_blocks(int64_t n);
+
+}  // namespace gm2

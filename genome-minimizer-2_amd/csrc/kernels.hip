@@ -1,0 +1,623 @@
+// Non-GEMM kernels of the VAE hot path: strain-row gather, BatchNorm (train/eval, fwd/bwd),
+// reparameterization + KL, deterministic reductions, clip-norm statistics, Adam, GEMM shadows.
+// All are HBM/latency-bound streaming kernels over [B,H]-sized (or P-sized) data; they keep
+// every padded element of their outputs at zero (the GEMM operand contract, gemm.hip).
+#include "gm2_common.hpp"
+#include "gm2_kernels.hpp"
+
+namespace gm2 {
+
+namespace {
+
+constexpr double kBnEps = 1e-5;       // nn.BatchNorm1d default eps
+constexpr double kBnMomentum = 0.1;   // nn.BatchNorm1d default momentum
+
+// ---------------------------------------------------------------------------------------------
+// gather: X[r][c] = data[rows[r]][c] (u8 0/1 -> T), X^T via an LDS transpose. Tile 64 x 128.
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data, int64_t ld_data,
+                                              const int32_t* __restrict__ rows, int B, int G, T* __restrict__ X,
+                                              int64_t ldx, T* __restrict__ XT, int64_t ldxt) {
+  __shared__ float tile[128][65];
+  const int c0 = blockIdx.x * 128, r0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+  const int ch = t & 7;          // 16-column chunk
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int rl = pass * 32 + (t >> 3);
+    const int r = r0 + rl;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < B) {
+      const int64_t src = rows ? (int64_t)rows[r] : (int64_t)r;
+      v = *(const uint4*)(data + src * ld_data + c0 + ch * 16);
+    }
+    const uint8_t* b = (const uint8_t*)&v;
+    float f[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = c0 + ch * 16 + i;
+      f[i] = (c < G) ? (float)b[i] : 0.f;
+      tile[ch * 16 + i][rl] = f[i];
+    }
+    T* dst = X + (int64_t)r * ldx + c0 + ch * 16;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dst[i] = E<T>::cvt(f[i]);
+  }
+  __syncthreads();
+  // X^T: 128 rows (columns of X) x 64 (batch rows)
+  for (int i = t; i < 128 * 64; i += 256) {
+    const int c = i >> 6, rl = i & 63;
+    XT[(int64_t)(c0 + c) * ldxt + r0 + rl] = E<T>::cvt(tile[c][rl]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// BN forward partial statistics. Block: 64 columns x 128 rows (4 row groups x 32 rows).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bn_fwd_partial(const float* __restrict__ slabs, int S, int64_t slab,
+                                                      int64_t ld, const float* __restrict__ bias, int B, int H,
+                                                      float* __restrict__ Y, float2* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * kBnRowChunk;
+  const int nrows = min(kBnRowChunk, B - r0);
+  const float b = bias ? bias[col] : 0.f;
+  float v[32];
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int rl = rg + 4 * i;
+    float y = 0.f;
+    if (rl < nrows) {
+      const int64_t o = (int64_t)(r0 + rl) * ld + col;
+      y = slabs[o];
+      for (int s = 1; s < S; ++s) y += slabs[(int64_t)s * slab + o];
+      y += b;
+      Y[o] = y;
+      sum += y;
+    }
+    v[i] = y;
+  }
+  red[rg][threadIdx.x & 63] = sum;
+  __syncthreads();
+  const int c = threadIdx.x & 63;
+  const float mean = (red[0][c] + red[1][c] + red[2][c] + red[3][c]) / (float)nrows;
+  __syncthreads();
+  float m2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int rl = rg + 4 * i;
+    if (rl < nrows) { const float d = v[i] - mean; m2 += d * d; }
+  }
+  red[rg][c] = m2;
+  __syncthreads();
+  if (rg == 0) part[(int64_t)blockIdx.y * H + col] = make_float2(mean, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+}
+
+// Chan merge of per-chunk (mean, M2) -> batch mean and biased variance (double)
+__device__ inline void bn_merge(const float2* __restrict__ part, int B, int H, int col, double& mean, double& var) {
+  double n = 0.0, mu = 0.0, M2 = 0.0;
+  const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
+  for (int ch = 0; ch < nch; ++ch) {
+    const double nb = (double)min(kBnRowChunk, B - ch * kBnRowChunk);
+    const float2 p = part[(int64_t)ch * H + col];
+    const double delta = (double)p.x - mu;
+    const double nt = n + nb;
+    mu += delta * nb / nt;
+    M2 += (double)p.y + delta * delta * n * nb / nt;
+    n = nt;
+  }
+  mean = mu;
+  var = M2 / n;
+}
+
+// ---------------------------------------------------------------------------------------------
+// BN forward apply + ReLU: A = relu(y*alpha + beta'), alpha = invstd*gamma, beta' = beta - mean*alpha
+// (the reference's batch_norm transform), A^T via LDS. Tile 64 rows x 64 cols.
+// save[0][c] = mean, save[1][c] = invstd (train) — reused by the backward.
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_bn_fwd_apply(const float* __restrict__ Y, int64_t ld,
+                                                    const float2* __restrict__ part, int B, int H, int train,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    float* __restrict__ rmean, float* __restrict__ rvar,
+                                                    float* __restrict__ save, T* __restrict__ A,
+                                                    T* __restrict__ AT, int64_t ldat) {
+  __shared__ float coef[2][64];
+  __shared__ float tile[64][65];
+  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+  if (t < 64) {
+    const int col = c0 + t;
+    float invstd, meanf;
+    if (train) {
+      double mean, var;
+      bn_merge(part, B, H, col, mean, var);
+      invstd = (float)(1.0 / sqrt(var + kBnEps));
+      meanf = (float)mean;
+      if (blockIdx.y == 0) {
+        save[col] = meanf;
+        save[H + col] = invstd;
+        const double unb = B > 1 ? var * (double)B / (double)(B - 1) : var;
+        rmean[col] = (float)(kBnMomentum * mean + (1.0 - kBnMomentum) * (double)rmean[col]);
+        rvar[col] = (float)(kBnMomentum * unb + (1.0 - kBnMomentum) * (double)rvar[col]);
+      }
+    } else {
+      // eval transform bit-identical to the reference CPU path (pinned in tests): float
+      // invstd = 1/sqrt(rv + eps), alpha = gamma*invstd, beta' = fma(-mean, alpha, beta)
+      meanf = rmean[col];
+      invstd = 1.0f / sqrtf(rvar[col] + (float)kBnEps);
+      if (blockIdx.y == 0 && save) { save[col] = meanf; save[H + col] = invstd; }
+    }
+    const float alpha = invstd * gamma[col];
+    coef[0][t] = alpha;
+    coef[1][t] = fmaf(-meanf, alpha, beta[col]);
+  }
+  __syncthreads();
+  const int c = t & 63;
+  for (int rl = t >> 6; rl < 64; rl += 4) {
+    const int r = r0 + rl;
+    float a = 0.f;
+    if (r < B) a = fmaxf(fmaf(Y[(int64_t)r * ld + c0 + c], coef[0][c], coef[1][c]), 0.f);
+    A[(int64_t)r * ld + c0 + c] = E<T>::cvt(a);
+    tile[c][rl] = a;
+  }
+  __syncthreads();
+  if (AT) {
+    for (int i = t; i < 64 * 64; i += 256) {
+      const int cc = i >> 6, rl = i & 63;
+      AT[(int64_t)(c0 + cc) * ldat + r0 + rl] = E<T>::cvt(tile[cc][rl]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// BN backward partials: do = dA * [y*alpha+beta' > 0]; sums of do and (y-mean)*do per chunk
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict__ dslabs, int S, int64_t slab,
+                                                      const float* __restrict__ Y, int64_t ld,
+                                                      const float* __restrict__ save, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, int B, int H,
+                                                      float2* __restrict__ part) {
+  __shared__ float red[2][4][64];
+  const int c = threadIdx.x & 63;
+  const int col = blockIdx.x * 64 + c;
+  const int rg = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * kBnRowChunk;
+  const int nrows = min(kBnRowChunk, B - r0);
+  const float mean = save[col], invstd = save[H + col];
+  const float alpha = invstd * gamma[col];
+  const float bprime = fmaf(-mean, alpha, beta[col]);
+  float s1 = 0.f, s2 = 0.f;
+  for (int rl = rg; rl < nrows; rl += 4) {
+    const int64_t o = (int64_t)(r0 + rl) * ld + col;
+    float da = dslabs[o];
+    for (int s = 1; s < S; ++s) da += dslabs[(int64_t)s * slab + o];
+    const float y = Y[o];
+    const float d = fmaf(y, alpha, bprime) > 0.f ? da : 0.f;
+    s1 += d;
+    s2 += (y - mean) * d;
+  }
+  red[0][rg][c] = s1;
+  red[1][rg][c] = s2;
+  __syncthreads();
+  if (rg == 0)
+    part[(int64_t)blockIdx.y * H + col] = make_float2(red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c],
+                                                      red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
+}
+
+// BN backward apply (training-mode formula of the reference's native batch_norm backward):
+//   dx = (do - sum(do)/B - (y-mean) * sum((y-mean)*do) * invstd^2 / B) * invstd * gamma
+//   dgamma = sum((y-mean)*do) * invstd ; dbeta = sum(do)
+// Writes dY, dY^T (T) and per-64-row column sums of dx (the preceding Linear's bias gradient).
+template <typename T>
+__global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ dslabs, int S, int64_t slab,
+                                                    const float* __restrict__ Y, int64_t ld,
+                                                    const float* __restrict__ save, const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta, const float2* __restrict__ part,
+                                                    int B, int H, float* __restrict__ dgamma,
+                                                    float* __restrict__ dbeta, T* __restrict__ dY,
+                                                    T* __restrict__ dYT, int64_t ldyt, float* __restrict__ colpart) {
+  __shared__ float cf[5][64];
+  __shared__ float tile[64][65];
+  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+  if (t < 64) {
+    const int col = c0 + t;
+    double s1 = 0.0, s2 = 0.0;
+    const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
+    for (int ch = 0; ch < nch; ++ch) {
+      const float2 p = part[(int64_t)ch * H + col];
+      s1 += p.x;
+      s2 += p.y;
+    }
+    const float mean = save[col], invstd = save[H + col];
+    const float alpha = invstd * gamma[col];
+    if (blockIdx.y == 0) {
+      dgamma[col] = (float)(s2 * invstd);
+      dbeta[col] = (float)s1;
+    }
+    cf[0][t] = mean;
+    cf[1][t] = alpha;
+    cf[2][t] = fmaf(-mean, alpha, beta[col]);
+    cf[3][t] = (float)(s1 / B);                                 // grad_mean
+    cf[4][t] = (float)(s2 * (double)invstd * invstd / B);      // proj_scale
+  }
+  __syncthreads();
+  const int c = t & 63;
+  const float gs = cf[1][c];  // grad_scale = invstd * gamma
+  float csum = 0.f;
+  for (int rl = t >> 6; rl < 64; rl += 4) {
+    const int r = r0 + rl;
+    float dx = 0.f;
+    if (r < B) {
+      const int64_t o = (int64_t)r * ld + c0 + c;
+      float da = dslabs[o];
+      for (int s = 1; s < S; ++s) da += dslabs[(int64_t)s * slab + o];
+      const float y = Y[o];
+      const float d = fmaf(y, cf[1][c], cf[2][c]) > 0.f ? da : 0.f;
+      dx = (d - cf[3][c] - (y - cf[0][c]) * cf[4][c]) * gs;
+    }
+    csum += dx;
+    dY[(int64_t)r * ld + c0 + c] = E<T>::cvt(dx);
+    tile[c][rl] = dx;
+  }
+  __syncthreads();
+  for (int i = t; i < 64 * 64; i += 256) {
+    const int cc = i >> 6, rl = i & 63;
+    dYT[(int64_t)(c0 + cc) * ldyt + r0 + rl] = E<T>::cvt(tile[cc][rl]);
+  }
+  __syncthreads();
+  float* red = &tile[0][0];
+  red[t] = csum;
+  __syncthreads();
+  if (t < 64) colpart[(int64_t)blockIdx.y * H + c0 + t] = red[t] + red[t + 64] + red[t + 128] + red[t + 192];
+}
+
+// ---------------------------------------------------------------------------------------------
+// reparameterization: mu|lv = heads (+bias); z = mu + exp(0.5*lv)*eps; KL partial sums.
+// Block: 64 rows; thread loops over (row, l) pairs.
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_reparam(const float* __restrict__ slabs, int S, int64_t slab, int L,
+                                               const float* __restrict__ bmu, const float* __restrict__ blv,
+                                               const float* __restrict__ eps, int B, float* __restrict__ HD,
+                                               T* __restrict__ Z, int64_t ldz, T* __restrict__ ZT, int64_t ldzt,
+                                               float* __restrict__ kl_part) {
+  __shared__ float red[4];
+  const int r0 = blockIdx.x * 64;
+  const int ldh = 2 * L;
+  float kl = 0.f;
+  for (int i = threadIdx.x; i < 64 * L; i += 256) {
+    const int rl = i / L, l = i % L, r = r0 + rl;
+    float z = 0.f;
+    if (r < B) {
+      const int64_t o = (int64_t)r * ldh;
+      float mu = slabs[o + l], lv = slabs[o + L + l];
+      for (int s = 1; s < S; ++s) { mu += slabs[s * slab + o + l]; lv += slabs[s * slab + o + L + l]; }
+      mu += bmu[l];
+      lv += blv[l];
+      HD[o + l] = mu;
+      HD[o + L + l] = lv;
+      const float sd = expf(0.5f * lv);
+      z = mu + sd * (eps ? eps[(int64_t)r * L + l] : 0.f);
+      kl += ((1.0f + lv) - mu * mu) - expf(lv);
+    }
+    Z[(int64_t)r * ldz + l] = E<T>::cvt(z);
+    ZT[(int64_t)l * ldzt + r] = E<T>::cvt(z);
+  }
+  kl = wave_sum(kl);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = kl;
+  __syncthreads();
+  if (threadIdx.x == 0) kl_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// backward through reparameterization + beta*KL (autograd of model.py:101-103 and
+// loss_components.py:77): dmu = dz + beta*mu ; dlv = 0.5*dz*eps*std - 0.5*beta*(1 - exp(lv))
+template <typename T>
+__global__ __launch_bounds__(256) void k_reparam_bwd(const float* __restrict__ dz, int S, int64_t slab,
+                                                   int64_t ldslab, const float* __restrict__ HD,
+                                                   const float* __restrict__ eps, const float* __restrict__ scal,
+                                                   int B, int L, T* __restrict__ dH, int64_t ldh, T* __restrict__ dHT,
+                                                   int64_t ldht, float* __restrict__ colpart) {
+  __shared__ float acc[2][256];
+  const float beta = scal[kScalBeta];
+  const int r0 = blockIdx.x * 64;
+  const int L2 = 2 * L;
+  // 256 % L == 0 (host-checked): thread t always sees column t % L, so its column sums live in
+  // registers and are combined in a fixed order (deterministic bias gradients)
+  float smu = 0.f, slv = 0.f;
+  for (int i = threadIdx.x; i < 64 * L; i += 256) {
+    const int rl = i / L, l = i % L, r = r0 + rl;
+    float gmu = 0.f, glv = 0.f;
+    if (r < B) {
+      const int64_t o = (int64_t)r * ldslab + l;
+      float d = dz[o];
+      for (int s = 1; s < S; ++s) d += dz[s * slab + o];
+      const float mu = HD[(int64_t)r * L2 + l], lv = HD[(int64_t)r * L2 + L + l];
+      const float sd = expf(0.5f * lv);
+      const float e = eps[(int64_t)r * L + l];
+      gmu = d + (0.5f * beta) * (2.0f * mu);
+      glv = 0.5f * ((d * e) * sd) + (-0.5f * beta + (0.5f * beta) * expf(lv));
+    }
+    dH[(int64_t)r * ldh + l] = E<T>::cvt(gmu);
+    dH[(int64_t)r * ldh + L + l] = E<T>::cvt(glv);
+    dHT[(int64_t)l * ldht + r] = E<T>::cvt(gmu);
+    dHT[(int64_t)(L + l) * ldht + r] = E<T>::cvt(glv);
+    smu += gmu;
+    slv += glv;
+  }
+  acc[0][threadIdx.x] = smu;
+  acc[1][threadIdx.x] = slv;
+  __syncthreads();
+  if (threadIdx.x < L) {
+    float a = 0.f, b = 0.f;
+    for (int k = threadIdx.x; k < 256; k += L) { a += acc[0][k]; b += acc[1][k]; }
+    colpart[(int64_t)blockIdx.x * L2 + threadIdx.x] = a;
+    colpart[(int64_t)blockIdx.x * L2 + L + threadIdx.x] = b;
+  }
+}
+
+__global__ void k_colsum(const float* __restrict__ part, int rows, int64_t ld, int n, float* __restrict__ out0,
+                         float* __restrict__ out1, int nsplit) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) s += part[(int64_t)r * ld + c];
+  if (c < nsplit) out0[c] = s;
+  else out1[c - nsplit] = s;
+}
+
+__global__ __launch_bounds__(256) void k_reduce_to(const float* __restrict__ part, int n, int stride, int count,
+                                                 double* __restrict__ out) {
+  __shared__ double red[4];
+  for (int k = 0; k < count; ++k) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) s += (double)part[(int64_t)i * stride + k];
+    s = wave_sum_d(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) out[k] = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// GEMM shadows: padded (and transposed) T copies of the Linear weights. Tile 64x64.
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_shadow_sync(TensorTable tt, const float* __restrict__ params) {
+  __shared__ float tile[64][65];
+  int ti = 0;
+  while (ti + 1 < tt.n && (int64_t)blockIdx.x >= tt.t[ti + 1].tile0) ++ti;
+  const TensorDesc& d = tt.t[ti];
+  const int64_t local = blockIdx.x - d.tile0;
+  const int64_t tcols = (d.cols + 63) / 64;
+  const int64_t r0 = (local / tcols) * 64, c0 = (local % tcols) * 64;
+  const float* src = params + d.off;
+  T* sh = (T*)d.shadow;
+  T* shT = (T*)d.shadowT;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int rl = i >> 6, cl = i & 63;
+    const int64_t r = r0 + rl, c = c0 + cl;
+    float v = 0.f;
+    if (r < d.rows && c < d.cols) {
+      v = src[r * d.cols + c];
+      if (sh) sh[(d.srow0 + r) * d.sld + c] = E<T>::cvt(v);
+    }
+    tile[cl][rl] = v;
+  }
+  __syncthreads();
+  if (shT) {
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+      const int cl = i >> 6, rl = i & 63;
+      const int64_t r = r0 + rl, c = c0 + cl;
+      if (r < d.rows && c < d.cols) shT[c * d.tld + d.srow0 + r] = E<T>::cvt(tile[cl][rl]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// clip_grad_norm_ statistics (+ L1 term) and the fused L1 + clip + Adam update
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float sgnf(float x) { return (float)((x > 0.f) - (x < 0.f)); }
+
+__global__ __launch_bounds__(256) void k_grad_stats(const float* __restrict__ p, const float* __restrict__ g,
+                                                  int64_t n, const float* __restrict__ scal,
+                                                  double* __restrict__ part) {
+  __shared__ double red[2][4];
+  const float lam = scal[kScalLambda];
+  double ss = 0.0, ab = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float pv = p[i];
+    const float gv = g[i] + lam * sgnf(pv);
+    ss += (double)gv * gv;
+    ab += fabs((double)pv);
+  }
+  ss = wave_sum_d(ss);
+  ab = wave_sum_d(ab);
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = ss; red[1][threadIdx.x >> 6] = ab; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[blockIdx.x * 2 + 0] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    part[blockIdx.x * 2 + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_grad_finalize(const double* __restrict__ part, int nb,
+                                                     const float* __restrict__ scal, float* __restrict__ clip,
+                                                     double* __restrict__ l1abs) {
+  __shared__ double red[2][4];
+  double ss = 0.0, ab = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) { ss += part[2 * i]; ab += part[2 * i + 1]; }
+  ss = wave_sum_d(ss);
+  ab = wave_sum_d(ab);
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = ss; red[1][threadIdx.x >> 6] = ab; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double s = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    const float norm = (float)sqrt(s);
+    const float mx = scal[kScalMaxNorm];
+    float c = 1.0f;
+    if (mx > 0.f) c = fminf(mx / (norm + 1e-6f), 1.0f);
+    clip[0] = c;
+    clip[1] = norm;
+    if (l1abs) *l1abs = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_adam(const float* __restrict__ g, float* __restrict__ p,
+                                            float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                            const float* __restrict__ scal, const float* __restrict__ clip) {
+  const float lam = scal[kScalLambda], negstep = scal[kScalNegStep], bc2s = scal[kScalBc2Sqrt];
+  const float w1 = scal[kScalOneMinusB1], b2 = scal[kScalBeta2], w2 = scal[kScalOneMinusB2];
+  const float aeps = scal[kScalAdamEps];
+  const float cc = clip[0];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float pv = p[i];
+    const float gv = (g[i] + lam * sgnf(pv)) * cc;
+    float mv = m[i];
+    mv = mv + w1 * (gv - mv);                    // lerp_(grad, w1), w1 < 0.5 branch
+    float vv = v[i] * b2;
+    vv = vv + w2 * gv * gv;                      // addcmul_(g, g, value=w2)
+    const float denom = sqrtf(vv) / bc2s + aeps;
+    p[i] = pv + negstep * (mv / denom);          // addcdiv_(m, denom, value=-step_size)
+    m[i] = mv;
+    v[i] = vv;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* rows, int B, int G, T* X, int64_t ldx,
+                        int Gp, T* XT, int64_t ldxt, int Bp, hipStream_t s) {
+  if (Gp % 128 || Bp % 64 || ld_data % 16 || ld_data < Gp || ((uintptr_t)data & 15))
+    throw Gm2Error("gather: bad layout (Gp=%d Bp=%d ld=%lld)", Gp, Bp, (long long)ld_data);
+  hipLaunchKernelGGL(k_gather<T>, dim3(Gp / 128, Bp / 64), dim3(256), 0, s, data, ld_data, rows, B, G, X, ldx, XT,
+                     ldxt);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, const float* bias, int B, int H,
+                           float* Y, float* part, hipStream_t s) {
+  if (H % 64) throw Gm2Error("bn: H %% 64");
+  const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
+  hipLaunchKernelGGL(k_bn_fwd_partial, dim3(H / 64, nch), dim3(256), 0, s, slabs, S, slab, ld, bias, B, H, Y,
+                     (float2*)part);
+  GM2_CHECK_LAUNCH();
+}
+
+template <typename T>
+void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
+                         const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A, T* AT,
+                         int64_t ldat, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_fwd_apply<T>, dim3(H / 64, Bp / 64), dim3(256), 0, s, Y, ld, (const float2*)part, B, H,
+                     train, gamma, beta, rmean, rvar, save, A, AT, ldat);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
+                           const float* gamma, const float* beta, int B, int H, float* part, hipStream_t s) {
+  const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
+  hipLaunchKernelGGL(k_bn_bwd_partial, dim3(H / 64, nch), dim3(256), 0, s, dslabs, S, slab, Y, ld, save, gamma,
+                     beta, B, H, (float2*)part);
+  GM2_CHECK_LAUNCH();
+}
+
+template <typename T>
+void launch_bn_bwd_apply(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
+                         const float* gamma, const float* beta, const float* part, int B, int Bp, int H,
+                         float* dgamma, float* dbeta, T* dY, T* dYT, int64_t ldyt, float* colpart, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3(H / 64, Bp / 64), dim3(256), 0, s, dslabs, S, slab, Y, ld, save, gamma,
+                     beta, (const float2*)part, B, H, dgamma, dbeta, dY, dYT, ldyt, colpart);
+  GM2_CHECK_LAUNCH();
+}
+
+template <typename T>
+void launch_reparam(const float* slabs, int S, int64_t slab, int L, const float* bmu, const float* blv,
+                    const float* eps, int B, int Bp, float* HD, T* Z, int64_t ldz, T* ZT, int64_t ldzt, int Lrows,
+                    float* kl_part, hipStream_t s) {
+  (void)Lrows;
+  hipLaunchKernelGGL(k_reparam<T>, dim3(Bp / 64), dim3(256), 0, s, slabs, S, slab, L, bmu, blv, eps, B, HD, Z, ldz,
+                     ZT, ldzt, kl_part);
+  GM2_CHECK_LAUNCH();
+}
+
+template <typename T>
+void launch_reparam_bwd(const float* dzslabs, int S, int64_t slab, int64_t ldslab, const float* HD, const float* eps,
+                        const float* scal, int B, int Bp, int L, T* dH, int64_t ldh, T* dHT, int64_t ldht, int Hrows,
+                        float* colpart, hipStream_t s) {
+  (void)Hrows;
+  if (L > 256 || 256 % L) throw Gm2Error("reparam_bwd: latent_dim must divide 256");
+  hipLaunchKernelGGL(k_reparam_bwd<T>, dim3(Bp / 64), dim3(256), 0, s, dzslabs, S, slab, ldslab, HD, eps, scal, B, L,
+                     dH, ldh, dHT, ldht, colpart);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_colsum(const float* part, int rows, int64_t ld, int n, float* out0, float* out1, int nsplit,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(k_colsum, dim3((n + 255) / 256), dim3(256), 0, s, part, rows, ld, n, out0, out1 ? out1 : out0,
+                     out1 ? nsplit : n);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_reduce_to(const float* part, int n, int stride, int count, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_to, dim3(1), dim3(256), 0, s, part, n, stride, count, out);
+  GM2_CHECK_LAUNCH();
+}
+
+template <typename T>
+void launch_shadow_sync(const TensorTable& tt, const float* params, hipStream_t s) {
+  if (tt.n <= 0) return;
+  const TensorDesc& last = tt.t[tt.n - 1];
+  const int64_t tiles = last.tile0 + ((last.rows + 63) / 64) * ((last.cols + 63) / 64);
+  hipLaunchKernelGGL(k_shadow_sync<T>, dim3((unsigned)tiles), dim3(256), 0, s, tt, params);
+  GM2_CHECK_LAUNCH();
+}
+
+int grad_stats_blocks(int64_t n) { return (int)std::min<int64_t>(2048, std::max<int64_t>(1, (n + 255) / 256)); }
+
+void launch_grad_stats(const float* params, const float* grads, int64_t n, const float* scal, double* part,
+                       int nblocks, hipStream_t s) {
+  hipLaunchKernelGGL(k_grad_stats, dim3(nblocks), dim3(256), 0, s, params, grads, n, scal, part);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_grad_finalize(const double* part, int nblocks, const float* scal, float* clip_out, double* l1abs,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(k_grad_finalize, dim3(1), dim3(256), 0, s, part, nblocks, scal, clip_out, l1abs);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_adam(const float* grads, float* params, float* m, float* v, int64_t n, const float* scal,
+                 const float* clip, hipStream_t s) {
+  const int nb = (int)std::min<int64_t>(8192, (n + 255) / 256);
+  hipLaunchKernelGGL(k_adam, dim3(nb), dim3(256), 0, s, grads, params, m, v, n, scal, clip);
+  GM2_CHECK_LAUNCH();
+}
+
+#define GM2_INST(T)                                                                                             \
+  template void launch_gather_rows<T>(const uint8_t*, int64_t, const int32_t*, int, int, T*, int64_t, int, T*,  \
+                                      int64_t, int, hipStream_t);                                               \
+  template void launch_bn_fwd_apply<T>(const float*, int64_t, const float*, int, int, int, int, const float*,   \
+                                       const float*, float*, float*, float*, T*, T*, int64_t, hipStream_t);     \
+  template void launch_bn_bwd_apply<T>(const float*, int, int64_t, const float*, int64_t, const float*,         \
+                                       const float*, const float*, const float*, int, int, int, float*, float*, \
+                                       T*, T*, int64_t, float*, hipStream_t);                                   \
+  template void launch_reparam<T>(const float*, int, int64_t, int, const float*, const float*, const float*,   \
+                                  int, int, float*, T*, int64_t, T*, int64_t, int, float*, hipStream_t);        \
+  template void launch_reparam_bwd<T>(const float*, int, int64_t, int64_t, const float*, const float*,         \
+                                      const float*, int, int, int, T*, int64_t, T*, int64_t, int, float*,       \
+                                      hipStream_t);                                                             \
+  template void launch_shadow_sync<T>(const TensorTable&, const float*, hipStream_t);
+GM2_INST(float)
+GM2_INST(bf16_t)
+#undef GM2_INST
+
+}  // namespace gm2

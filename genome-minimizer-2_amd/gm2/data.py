@@ -1,0 +1,166 @@
+"""Data side of the hot path: the presence/absence matrix resident in HBM, and a DataLoader mirror
+that yields strain-row index batches with the reference's RNG consumption.
+
+Reference: data ingest `load_and_validate_data` (explore_data/data_exploration.py:54-107), the split
++ loaders of `create_dataloaders` (utils/experiments.py:225-252), DataLoader/RandomSampler semantics
+of torch (one int64 base-seed draw per iterator, one seed draw + randperm per shuffled epoch).
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import torch
+
+
+def _pad_cols(G):
+    return int(math.ceil(G / 128) * 128)
+
+
+class ResidentMatrix:
+    """0/1 matrix [n, G] stored once in HBM as u8 rows of ld = roundup(G, 128) bytes (zero pad).
+    1 byte per gene: the F4 matrix (10k x 55k) is 0.55 GB; batches are gathered by row index."""
+
+    def __init__(self, x, device=None):
+        if isinstance(x, ResidentMatrix):
+            self.__dict__.update(x.__dict__)
+            return
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        t = torch.as_tensor(np.asarray(x) if not torch.is_tensor(x) else x)
+        if t.dim() != 2:
+            raise ValueError("presence/absence matrix must be 2-D [strains, genes]")
+        self.n, self.G = int(t.shape[0]), int(t.shape[1])
+        self.ld = _pad_cols(self.G)
+        if t.dtype != torch.uint8:
+            tf = t.to(torch.float32)
+            bad = ((tf != 0) & (tf != 1)).any().item() if tf.numel() else False
+            if bad:
+                raise ValueError("the fused BCE path needs a binary 0/1 matrix (reference data is 0/1)")
+            t = tf.to(torch.uint8)
+        buf = torch.zeros(max(self.n, 1), self.ld, dtype=torch.uint8)
+        buf[: self.n, : self.G] = t.cpu()
+        self.data = buf.to(device)
+
+    def __len__(self):
+        return self.n
+
+
+class _Subset:
+    """`len(loader.dataset)` for the epoch averages (trainer.py:127, :152)."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+
+class StrainLoader:
+    """DataLoader(TensorDataset(X[idx]), batch_size, shuffle) mirror: iterates device int32 row
+    indices into a ResidentMatrix. RNG use is the torch DataLoader's: each iterator draws an int64
+    base seed from the global CPU generator; a shuffled one then draws its sampler seed and runs
+    randperm on a private generator (so the global stream advances exactly as in the reference)."""
+
+    def __init__(self, matrix: ResidentMatrix, rows=None, batch_size=32, shuffle=False, drop_last=False):
+        self.matrix = matrix
+        rows = np.arange(matrix.n) if rows is None else np.asarray(rows)
+        self.rows_host = torch.as_tensor(rows, dtype=torch.int64)
+        self.rows = self.rows_host.to(torch.int32).to(matrix.data.device)
+        self.batch_size = int(batch_size)
+        self.shuffle = bool(shuffle)
+        self.drop_last = bool(drop_last)
+        self.dataset = _Subset(len(rows))
+
+    def __len__(self):
+        n = len(self.dataset)
+        return n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
+
+    def __iter__(self):
+        n = len(self.dataset)
+        torch.empty((), dtype=torch.int64).random_()  # _BaseDataLoaderIter._base_seed
+        if self.shuffle:
+            seed = int(torch.empty((), dtype=torch.int64).random_().item())
+            g = torch.Generator()
+            g.manual_seed(seed)
+            perm = torch.randperm(n, generator=g).to(torch.int32).to(self.rows.device)
+            order = self.rows[perm.long()]
+        else:
+            order = self.rows
+        for s in range(0, n, self.batch_size):
+            e = min(n, s + self.batch_size)
+            if self.drop_last and e - s < self.batch_size:
+                break
+            yield order[s:e]
+
+
+def as_strain_loader(loader, device=None):
+    """Accept a reference-style torch DataLoader(TensorDataset(X), batch_size, shuffle) too."""
+    if isinstance(loader, StrainLoader):
+        return loader
+    ds = loader.dataset
+    x = ds.tensors[0] if hasattr(ds, "tensors") else torch.stack([ds[i][0] for i in range(len(ds))])
+    from torch.utils.data import RandomSampler
+    shuffle = isinstance(loader.sampler, RandomSampler)
+    return StrainLoader(ResidentMatrix(x, device=device), None, loader.batch_size, shuffle, loader.drop_last)
+
+
+def split_indices(n, test_size=0.3, val_ratio=0.3333, random_state=12345):
+    """create_dataloaders' two train_test_split calls (experiments.py:232-237) on row indices."""
+    from sklearn.model_selection import train_test_split
+    idx = np.arange(n)
+    tr, tmp = train_test_split(idx, test_size=test_size, random_state=random_state)
+    va, te = train_test_split(tmp, test_size=val_ratio, random_state=random_state)
+    return tr, va, te
+
+
+def load_and_validate_data(dataset_csv, phylogroups_csv):
+    """(large_data, merged_df, data_without_lineage) as data_exploration.py:54-107: genes x strains
+    CSV (index_col=0), strain IDs upper-cased, 'Lineage' row dropped, transposed and inner-merged
+    with the phylogroup table on ID."""
+    import pandas as pd
+    large = pd.read_csv(dataset_csv, index_col=0, header=0)
+    large.columns = large.columns.str.upper()
+    phylo = pd.read_csv(phylogroups_csv, index_col=0, header=0)
+    without = large.drop(index=["Lineage"], errors="ignore")
+    merged = pd.merge(without.transpose(), phylo, how="inner", left_index=True, right_on="ID")
+    if merged.empty:
+        raise ValueError("Merged dataset is empty - check ID matching between datasets")
+    if "Phylogroup" not in merged.columns:
+        raise ValueError("Phylogroup column not found in merged data")
+    return large, merged, without
+
+
+def synthetic_pangenome(n, g, seed=12345, core_frac=0.15, core_freq=0.98):
+    """Synthetic binary pan-genome: 15% core genes at f=0.98, accessory genes
+    f ~ Beta(0.1, 1); X[s, g] ~ Bernoulli(f_g). numpy PCG64(seed). Returns u8 [n, g]."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    f = rng.beta(0.1, 1.0, size=g)
+    core = rng.random(g) < core_frac
+    f[core] = core_freq
+    out = np.empty((n, g), dtype=np.uint8)
+    step = max(1, (1 << 26) // max(g, 1))
+    for s in range(0, n, step):
+        e = min(n, s + step)
+        out[s:e] = rng.random((e - s, g), dtype=np.float32) < f[None, :]
+    return out
+
+
+def write_synthetic_csvs(root, n, g, seed=12345):
+    """Write a synthetic data/ tree in the reference's on-disk layout (genes x strains CSV with a
+    'Lineage' row, ID,Phylogroup CSV, essential genes CSV) for CLI runs without the private data."""
+    import pandas as pd
+    x = synthetic_pangenome(n, g, seed)
+    genes = [f"gene{i:05d}" for i in range(g)]
+    strains = [f"S{i:06d}" for i in range(n)]
+    df = pd.DataFrame(x.T, index=genes, columns=strains)
+    lineage = pd.DataFrame([[1] * n], index=["Lineage"], columns=strains)
+    os.makedirs(os.path.join(root, "data"), exist_ok=True)
+    pd.concat([lineage, df]).to_csv(os.path.join(root, "data", "F4_complete_presence_absence.csv"))
+    groups = np.array(list("ABCDEFG"))[np.arange(n) % 7]
+    pd.DataFrame({"ID": strains, "Phylogroup": groups}).to_csv(
+        os.path.join(root, "data", "accessionID_phylogroup_BD.csv"), index=False)
+    pd.DataFrame({"gene": genes[: max(1, g // 20)]}).to_csv(os.path.join(root, "data", "essential_genes.csv"),
+                                                           index=False)
+    return x

@@ -1,0 +1,79 @@
+"""Sampling / checkpoint utilities — mirror of src/genome_minimizer_2/utils/extras.py:
+load_model (:166-189), sample_from_model (:192-203), get_latent_variables (:205-228),
+count_essential_genes (:49-87), write_samples_to_dataframe (:31-39). Plots are out of scope."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import native
+from .data import ResidentMatrix, as_strain_loader
+from .model import VAE
+
+
+def load_model(input_dim, hidden_dim, latent_dim, path_to_model, precision=native.GM2_BF16):
+    """VAE(...) + load_state_dict(torch.load(path, weights_only=True)) + eval() (extras.py:185-187)."""
+    model = VAE(input_dim, hidden_dim, latent_dim, precision=precision, init=False)
+    model.load_state_dict(torch.load(path_to_model, weights_only=True, map_location="cpu"))
+    model.eval()
+    return model
+
+
+def sample_from_model(model, latent_dim, num_samples, device, binary_dtype=np.float64, return_probs=True,
+                      chunk=65536):
+    """z ~ N(0, I) drawn with torch.randn(num_samples, latent_dim, device=device) exactly as the
+    reference, decoded in exact fp32 with eval-mode BatchNorm, thresholded at sigmoid > 0.5.
+    Returns (binary [N,G] as `binary_dtype` (reference: float64), probs fp32 [N,G] or None, z)."""
+    with torch.no_grad():
+        z = torch.randn(num_samples, latent_dim, device=device)
+    mask, probs = model.decode_mask(z, want_probs=return_probs, chunk=chunk)
+    binary = mask.cpu().numpy()
+    if binary_dtype is not None and binary_dtype != np.uint8:
+        binary = binary.astype(binary_dtype)
+    return binary, (probs.cpu().numpy() if probs is not None else None), z
+
+
+def get_latent_variables(model, data_loader, device=None):
+    """Encoder means of every row of `data_loader`, in loader order (extras.py:205-228)."""
+    model.eval()
+    loader = as_strain_loader(data_loader, model.device)
+    mat = loader.matrix
+    out = []
+    ws = model.workspace(model.precision, loader.batch_size)
+    for rows in loader:
+        n = rows.shape[0]
+        mu = torch.empty(n, model.latent_dim, device=model.device)
+        native.encode(ws, native.make_batch(mat.data, mat.ld, rows, n, None), model.params, model.bn, mu, None)
+        out.append(mu)
+    if not out:
+        return np.zeros((0, model.latent_dim), np.float32)
+    return torch.cat(out).cpu().numpy()
+
+
+def count_essential_genes(binary_generated_samples, essential_gene_positions):
+    """Per sample, how many essential genes are present: a gene counts when ANY of its column
+    positions (< G) is non-zero (extras.py:65-85), vectorised over samples."""
+    b = np.asarray(binary_generated_samples)
+    G = b.shape[1]
+    present = b.astype(bool) if b.dtype != bool else b
+    counts = np.zeros(b.shape[0], dtype=int)
+    for _, positions in essential_gene_positions.items():
+        cols = [p for p in positions if p < G]
+        if cols:
+            counts += present[:, cols].any(axis=1)
+    return counts
+
+
+def write_samples_to_dataframe(binary_generated_samples, all_genes, output_file):
+    """Genes x samples CSV with a leading 'Gene' column (extras.py:31-39)."""
+    import pandas as pd
+    df = pd.DataFrame(binary_generated_samples, columns=all_genes)
+    df.index = [f"Sample_{i+1}" for i in range(df.shape[0])]
+    df = df.transpose()
+    df.columns = [f"Sample_{i+1}" for i in range(df.shape[1])]
+    df = df.reset_index().rename(columns={"index": "Gene"})
+    df.to_csv(output_file, index=False)
+
+
+def as_matrix(x, device=None):
+    return x if isinstance(x, ResidentMatrix) else ResidentMatrix(x, device=device)

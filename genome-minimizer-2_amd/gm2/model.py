@@ -1,0 +1,226 @@
+"""VAE — MI355X mirror of the reference model (src/genome_minimizer_2/training/model.py:13-120).
+
+Same constructor, same state_dict keys / shapes / dtypes, same init RNG replay, same
+encode / reparameterization / decode / forward contract. The difference is the storage: all 30
+parameter tensors live in ONE flat fp32 device buffer (reference order, model.py:65-91) and all
+6 BatchNorm running statistics in one [6][2][H] buffer, which is what libgm2's kernels consume.
+Every compute method runs through libgm2.so; there is no PyTorch-op fallback.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import torch
+
+from . import native
+
+LINEARS = ["encoder.0", "encoder.3", "encoder.6", "mean_layer", "logvar_layer",
+           "decoder.0", "decoder.3", "decoder.6", "decoder.9"]
+BNS = ["encoder.1", "encoder.4", "encoder.7", "decoder.1", "decoder.4", "decoder.7"]
+
+
+def param_specs(G, H, L):
+    """(name, shape) in `model.parameters()` order (model.py:65-91)."""
+    s = []
+    for i, fan_in in enumerate([G, H, H]):
+        s += [(f"encoder.{3*i}.weight", (H, fan_in)), (f"encoder.{3*i}.bias", (H,)),
+              (f"encoder.{3*i+1}.weight", (H,)), (f"encoder.{3*i+1}.bias", (H,))]
+    s += [("mean_layer.weight", (L, H)), ("mean_layer.bias", (L,)),
+          ("logvar_layer.weight", (L, H)), ("logvar_layer.bias", (L,))]
+    for i, fan_in in enumerate([L, H, H]):
+        s += [(f"decoder.{3*i}.weight", (H, fan_in)), (f"decoder.{3*i}.bias", (H,)),
+              (f"decoder.{3*i+1}.weight", (H,)), (f"decoder.{3*i+1}.bias", (H,))]
+    s += [("decoder.9.weight", (G, H)), ("decoder.9.bias", (G,))]
+    return s
+
+
+def reference_init(G, H, L):
+    """Host-side replay of the reference init on the global CPU generator: nn.Linear ctor
+    (kaiming_uniform a=sqrt(5) weight, uniform(+-1/sqrt(fan_in)) bias, construction order), then
+    xavier_uniform_ on every Linear weight and zero biases (model.py:115-120). BN: ones / zeros.
+    Host work, once per model: not on the hot path."""
+    shapes = dict(param_specs(G, H, L))
+    P = {}
+    for lin in LINEARS:
+        w = torch.empty(shapes[lin + ".weight"])
+        b = torch.empty(shapes[lin + ".bias"])
+        torch.nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+        bound = 1.0 / math.sqrt(w.shape[1]) if w.shape[1] > 0 else 0.0
+        torch.nn.init.uniform_(b, -bound, bound)
+        P[lin + ".weight"], P[lin + ".bias"] = w, b
+    for bn in BNS:
+        P[bn + ".weight"] = torch.ones(H)
+        P[bn + ".bias"] = torch.zeros(H)
+    for lin in LINEARS:
+        torch.nn.init.xavier_uniform_(P[lin + ".weight"])
+        P[lin + ".bias"].zero_()
+    return [P[n] for n, _ in param_specs(G, H, L)]
+
+
+def _default_device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("genome-minimizer-2 MI355X build: no HIP device visible (torch.cuda.is_available() "
+                           "is False); the hot path has no CPU implementation")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class VAE:
+    """Drop-in for the reference VAE (model.py:13). `precision` selects the GEMM arithmetic of
+    training/eval/encode (native.GM2_F32 exact fp32, native.GM2_BF16); sampling always decodes in
+    exact fp32 so its thresholded masks match the fp32 reference."""
+
+    def __init__(self, input_dim, hidden_dim, latent_dim, device=None, precision=native.GM2_BF16,
+                 init=True):
+        self.input_dim, self.hidden_dim, self.latent_dim = int(input_dim), int(hidden_dim), int(latent_dim)
+        self.device = torch.device(device) if device is not None else None
+        self.precision = precision
+        self.training = True
+        G, H, L = self.input_dim, self.hidden_dim, self.latent_dim
+        self.specs = param_specs(G, H, L)
+        self.offsets = native.param_offsets(G, H, L)
+        self.n_params = self.offsets[-1]
+        host = reference_init(G, H, L) if init else [torch.zeros(s) for _, s in self.specs]
+        self._host_init = torch.cat([t.reshape(-1) for t in host])
+        self.num_batches_tracked = [0] * 6
+        self.params = None
+        self.bn = None
+        self._workspaces = {}
+        self._shadow_stamp = {}
+        self._version = 0
+        if self.device is None or self.device.type == "cuda":
+            self.to(self.device or _default_device())
+
+    # ---------------------------------------------------------------- storage / torch-like API
+    def to(self, device):
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError("the MI355X VAE lives on a HIP device; CPU execution is not provided")
+        if self.params is None:
+            self.params = self._host_init.to(device).contiguous()
+            bn = torch.zeros(6, 2, self.hidden_dim)
+            bn[:, 1] = 1.0
+            self.bn = bn.to(device).contiguous()
+            self._host_init = None
+        else:
+            self.params = self.params.to(device)
+            self.bn = self.bn.to(device)
+        self.device = device
+        self._workspaces.clear()
+        self.touch()
+        return self
+
+    def touch(self):
+        """Mark the fp32 master parameters as edited (GEMM shadows are re-derived lazily)."""
+        self._version += 1
+
+    def train(self, mode=True):
+        self.training = bool(mode)
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def param_views(self):
+        out = OrderedDict()
+        for i, (n, shp) in enumerate(self.specs):
+            out[n] = self.params[self.offsets[i]:self.offsets[i + 1]].view(shp)
+        return out
+
+    def named_parameters(self):
+        return list(self.param_views().items())
+
+    def parameters(self):
+        return list(self.param_views().values())
+
+    def state_dict(self):
+        """Same keys, order, shapes and dtypes as the reference module's state_dict."""
+        views = self.param_views()
+        sd = OrderedDict()
+        for lin in ["encoder.0", "encoder.1", "encoder.3", "encoder.4", "encoder.6", "encoder.7",
+                    "mean_layer", "logvar_layer", "decoder.0", "decoder.1", "decoder.3", "decoder.4",
+                    "decoder.6", "decoder.7", "decoder.9"]:
+            sd[lin + ".weight"] = views[lin + ".weight"].detach().clone()
+            sd[lin + ".bias"] = views[lin + ".bias"].detach().clone()
+            if lin in BNS:
+                i = BNS.index(lin)
+                sd[lin + ".running_mean"] = self.bn[i, 0].detach().clone()
+                sd[lin + ".running_var"] = self.bn[i, 1].detach().clone()
+                sd[lin + ".num_batches_tracked"] = torch.tensor(self.num_batches_tracked[i], dtype=torch.long)
+        return sd
+
+    def load_state_dict(self, sd, strict=True):
+        views = self.param_views()
+        expected = set(self.state_dict().keys()) if strict else set()
+        missing = [k for k in expected if k not in sd]
+        unexpected = [k for k in sd if strict and k not in expected]
+        if missing or unexpected:
+            raise RuntimeError(f"Error(s) in loading state_dict for VAE: missing {missing}, unexpected {unexpected}")
+        with torch.no_grad():
+            for k, v in sd.items():
+                if k in views:
+                    if tuple(v.shape) != tuple(views[k].shape):
+                        raise RuntimeError(f"size mismatch for {k}: {tuple(v.shape)} vs {tuple(views[k].shape)}")
+                    views[k].copy_(v.to(self.device, torch.float32))
+                elif k.endswith("running_mean") or k.endswith("running_var"):
+                    i = BNS.index(k.rsplit(".", 1)[0])
+                    self.bn[i, 0 if k.endswith("mean") else 1].copy_(v.to(self.device, torch.float32))
+                elif k.endswith("num_batches_tracked"):
+                    self.num_batches_tracked[BNS.index(k.rsplit(".", 1)[0])] = int(v)
+        self.touch()
+        return self
+
+    # ------------------------------------------------------------------ native workspaces
+    def workspace(self, prec, batch_max):
+        """Workspace for (precision, capacity); reused while large enough."""
+        key = prec
+        ws = self._workspaces.get(key)
+        if ws is None or ws.d.batch_max < batch_max:
+            cap = max(int(batch_max), ws.d.batch_max if ws else 0)
+            ws = native.Workspace(native.dims(self.input_dim, self.hidden_dim, self.latent_dim, cap), prec,
+                                  self.device)
+            self._workspaces[key] = ws
+            self._shadow_stamp[key] = -1
+        if self._shadow_stamp[key] != self._version:
+            native.sync_shadows(ws, self.params)
+            self._shadow_stamp[key] = self._version
+        return ws
+
+    def shadows_current(self, prec):
+        """Called after an in-kernel optimizer step that refreshed the shadows itself."""
+        self._shadow_stamp[prec] = self._version
+
+    # ---------------------------------------------------------------------- compute API
+    def decode(self, z):
+        """p = sigmoid(decoder(z)) in eval mode, exact fp32 (model.py:106-107)."""
+        _, p = self.decode_mask(z, want_probs=True)
+        return p
+
+    def decode_mask(self, z, want_probs=False, chunk=65536):
+        """(mask u8 [N,G], probs fp32 [N,G] or None) = (sigmoid(decode(z)) > 0.5, p).
+        Eval-mode BatchNorm (running statistics), exactly as model.decode after model.eval()."""
+        z = z.to(self.device, torch.float32).contiguous()
+        N, G = z.shape[0], self.input_dim
+        mask = torch.empty(N, G, dtype=torch.uint8, device=self.device)
+        probs = torch.empty(N, G, dtype=torch.float32, device=self.device) if want_probs else None
+        for s in range(0, N, chunk):
+            n = min(chunk, N - s)
+            ws = self.workspace(native.GM2_F32, min(chunk, N))
+            native.decode_mask(ws, self.params, self.bn, z[s:s + n], n, mask[s:], G,
+                               None if probs is None else probs[s:], G)
+        return mask, probs
+
+    def encode(self, x):
+        """(mean, logvar) of the eval-mode encoder (model.py:95-98) for a 0/1 matrix x [B, G]."""
+        from .data import ResidentMatrix
+        m = x if isinstance(x, ResidentMatrix) else ResidentMatrix(x, device=self.device)
+        B = m.n
+        mu = torch.empty(B, self.latent_dim, device=self.device)
+        lv = torch.empty(B, self.latent_dim, device=self.device)
+        ws = self.workspace(self.precision, B)
+        native.encode(ws, native.make_batch(m.data, m.ld, None, B, None), self.params, self.bn, mu, lv)
+        return mu, lv
+
+    def __repr__(self):
+        return (f"VAE(input_dim={self.input_dim}, hidden_dim={self.hidden_dim}, latent_dim={self.latent_dim}, "
+                f"device={self.device}, precision={'fp32' if self.precision == native.GM2_F32 else 'bf16'})")

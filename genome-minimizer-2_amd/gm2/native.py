@@ -1,0 +1,180 @@
+"""ctypes binding of libgm2.so (include/gm2.h) — the only route from the Python host to the GPU.
+
+There is no fallback: if the library is missing or fails to load, every entry point raises.
+Device pointers are passed as integers (`tensor.data_ptr()`), the stream as torch's current
+HIP stream handle, so launches are ordered with the surrounding torch work.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgm2.so")
+
+GM2_F32 = 0
+GM2_BF16 = 1
+NUM_PARAMS = 30
+NUM_SCALARS = 16
+LOSS_SLOTS = 8
+
+# scalar block indices (gm2.h GM2_S_*)
+S_BETA, S_WGAMMA, S_LAMBDA, S_NEG_STEP, S_BC2_SQRT, S_MAX_NORM = 0, 1, 2, 3, 4, 5
+S_ONE_MINUS_B1, S_BETA2, S_ONE_MINUS_B2, S_ADAM_EPS = 6, 7, 8, 9
+
+EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_offsets",
+           "gm2_workspace_size", "gm2_workspace_init", "gm2_sync_shadows", "gm2_train_fwd_bwd",
+           "gm2_grad_norm", "gm2_adam_step", "gm2_eval_forward", "gm2_decode_mask", "gm2_encode",
+           "gm2_gemm_nt", "gm2_timing_begin", "gm2_timing_end"]
+KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
+
+
+class Dims(C.Structure):
+    _fields_ = [("G", C.c_int64), ("H", C.c_int64), ("L", C.c_int64), ("batch_max", C.c_int64)]
+
+
+class Batch(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("ld_data", C.c_int64), ("rows", C.c_void_p), ("n", C.c_int64),
+                ("eps", C.c_void_p)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libgm2.so once; raises (never falls back) when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libgm2.so not built ({LIB_PATH}); run __graft_entry__.build() or "
+                           "python genome-minimizer-2_amd/build_native.py")
+    L = C.CDLL(LIB_PATH)
+    vp, i64, i32, dp = C.c_void_p, C.c_int64, C.c_int, C.POINTER(Dims)
+    sig = {
+        "gm2_last_error": (C.c_char_p, []),
+        "gm2_abi_version": (C.c_int, []),
+        "gm2_param_count": (C.c_int, [dp, C.POINTER(C.c_int64)]),
+        "gm2_param_offsets": (C.c_int, [dp, C.POINTER(C.c_int64)]),
+        "gm2_workspace_size": (C.c_int, [dp, i32, C.POINTER(C.c_size_t)]),
+        "gm2_workspace_init": (C.c_int, [dp, i32, vp, C.c_size_t, vp]),
+        "gm2_sync_shadows": (C.c_int, [dp, i32, vp, vp, vp]),
+        "gm2_train_fwd_bwd": (C.c_int, [dp, i32, C.POINTER(Batch), vp, vp, vp, vp, vp, vp, vp]),
+        "gm2_grad_norm": (C.c_int, [dp, i32, vp, vp, vp, vp, vp, vp]),
+        "gm2_adam_step": (C.c_int, [dp, i32, vp, vp, vp, vp, vp, vp, vp]),
+        "gm2_eval_forward": (C.c_int, [dp, i32, C.POINTER(Batch), vp, vp, vp, vp, vp, vp]),
+        "gm2_decode_mask": (C.c_int, [dp, vp, vp, vp, i64, vp, i64, vp, i64, vp, vp]),
+        "gm2_encode": (C.c_int, [dp, i32, C.POINTER(Batch), vp, vp, vp, vp, vp, vp]),
+        "gm2_gemm_nt": (C.c_int, [i32, vp, i64, vp, i64, vp, i64, i64, i64, i64, i32, vp, vp]),
+        "gm2_timing_begin": (C.c_int, [i32]),
+        "gm2_timing_end": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    if L.gm2_abi_version() != 1:
+        raise RuntimeError("libgm2 ABI mismatch")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().gm2_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dims(G, H, L, batch_max) -> Dims:
+    return Dims(int(G), int(H), int(L), int(batch_max))
+
+
+def param_offsets(G, H, L):
+    d = dims(G, H, L, 1)
+    off = (C.c_int64 * (NUM_PARAMS + 1))()
+    check(lib().gm2_param_offsets(C.byref(d), off), "gm2_param_offsets")
+    return list(off)
+
+
+def workspace_size(d: Dims, prec: int) -> int:
+    n = C.c_size_t()
+    check(lib().gm2_workspace_size(C.byref(d), prec, C.byref(n)), "gm2_workspace_size")
+    return n.value
+
+
+class Workspace:
+    """Caller-owned device scratch of one (dims, precision) geometry."""
+
+    def __init__(self, d: Dims, prec: int, device):
+        self.d, self.prec = d, prec
+        self.nbytes = workspace_size(d, prec)
+        self.buf = torch.empty(self.nbytes + 256, dtype=torch.uint8, device=device)
+        base = self.buf.data_ptr()
+        self.off = (-base) % 256
+        self.ptr = C.c_void_p(base + self.off)
+        check(lib().gm2_workspace_init(C.byref(d), prec, self.ptr, self.nbytes, stream()),
+              "gm2_workspace_init")
+
+
+def make_batch(data, ld, rows, n, eps) -> Batch:
+    return Batch(data.data_ptr(), int(ld), None if rows is None else rows.data_ptr(), int(n),
+                 None if eps is None else eps.data_ptr())
+
+
+def sync_shadows(ws: Workspace, params):
+    check(lib().gm2_sync_shadows(C.byref(ws.d), ws.prec, ptr(params), ws.ptr, stream()), "gm2_sync_shadows")
+
+
+def train_fwd_bwd(ws: Workspace, batch: Batch, params, grads, bn, scal, loss):
+    check(lib().gm2_train_fwd_bwd(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), ptr(grads), ptr(bn),
+                                  ptr(scal), ptr(loss), ws.ptr, stream()), "gm2_train_fwd_bwd")
+
+
+def grad_norm(ws: Workspace, params, grads, scal, loss):
+    check(lib().gm2_grad_norm(C.byref(ws.d), ws.prec, ptr(params), ptr(grads), ptr(scal), ptr(loss), ws.ptr,
+                              stream()), "gm2_grad_norm")
+
+
+def adam_step(ws: Workspace, params, grads, m, v, scal):
+    check(lib().gm2_adam_step(C.byref(ws.d), ws.prec, ptr(params), ptr(grads), ptr(m), ptr(v), ptr(scal), ws.ptr,
+                              stream()), "gm2_adam_step")
+
+
+def eval_forward(ws: Workspace, batch: Batch, params, bn, scal, loss):
+    check(lib().gm2_eval_forward(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), ptr(bn), ptr(scal),
+                                 ptr(loss), ws.ptr, stream()), "gm2_eval_forward")
+
+
+def decode_mask(ws: Workspace, params, bn, z, n, mask, ld_mask, probs=None, ld_probs=0):
+    check(lib().gm2_decode_mask(C.byref(ws.d), ptr(params), ptr(bn), ptr(z), int(n), ptr(mask), int(ld_mask),
+                                ptr(probs), int(ld_probs), ws.ptr, stream()), "gm2_decode_mask")
+
+
+def encode(ws: Workspace, batch: Batch, params, bn, mu, logvar):
+    check(lib().gm2_encode(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), ptr(bn), ptr(mu), ptr(logvar),
+                           ws.ptr, stream()), "gm2_encode")
+
+
+def gemm_nt(prec, P, ldp, Q, ldq, Cout, ldc, M, N, K, splits=1, slab=None):
+    check(lib().gm2_gemm_nt(prec, ptr(P), ldp, ptr(Q), ldq, ptr(Cout), ldc, M, N, K, splits, ptr(slab), stream()),
+          "gm2_gemm_nt")
+
+
+def timing_begin(classes: int):
+    check(lib().gm2_timing_begin(int(classes)), "gm2_timing_begin")
+
+
+def timing_end():
+    """(total_ms, launches) of the timed kernel class since timing_begin."""
+    ms, n = C.c_double(), C.c_int64()
+    check(lib().gm2_timing_end(C.byref(ms), C.byref(n)), "gm2_timing_end")
+    return ms.value, n.value

@@ -1,0 +1,151 @@
+/*
+ * libgm2 — MI355X (gfx950) native VAE train + sample hot path of genome-minimizer-2.
+ *
+ * C ABI: plain pointers and sizes only. Every pointer argument is a DEVICE pointer owned by the
+ * caller (PyTorch's caching allocator in the Python host), except the `const gm2_dims*` /
+ * `gm2_batch*` descriptors, which live in host memory. No call allocates device memory; the
+ * scratch comes from a caller-allocated workspace whose size `gm2_workspace_size` reports. Every
+ * compute call is asynchronous and stream-ordered on the `stream` it is given (a hipStream_t
+ * passed as void*). Return value: 0 on success, <0 on error; `gm2_last_error()` then returns a
+ * thread-local message. The Python host (gm2/native.py) turns a non-zero return into a
+ * RuntimeError, which main.py maps to exit code 1 as the reference does (main.py:686-692).
+ *
+ * The reference is pure Python (PyTorch eager), so it has no FFI of its own; each entry point
+ * below names the reference call site whose work it replaces (paths relative to
+ * /root/reference/src/genome_minimizer_2 unless they start with main.py).
+ *
+ * Parameter layout: ONE flat fp32 buffer holding the 30 tensors of `model.parameters()` in
+ * reference order (model.py:65-91: encoder.0.weight, encoder.0.bias, encoder.1.weight, ...,
+ * decoder.9.bias), each row-major exactly as in the state_dict. `gm2_param_offsets` gives the
+ * offsets. Gradients, Adam exp_avg / exp_avg_sq use the same layout. BatchNorm running
+ * statistics: ONE flat fp32 buffer [6][2][H] = (running_mean, running_var) for encoder.1,
+ * encoder.4, encoder.7, decoder.1, decoder.4, decoder.7; num_batches_tracked stays on the host.
+ */
+#ifndef GM2_H
+#define GM2_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GM2_ABI_VERSION 1
+#define GM2_NUM_PARAMS 30 /* tensors in model.parameters() */
+#define GM2_NUM_SCALARS 16
+
+/* arithmetic of the GEMMs: GM2_F32 = exact fp32 MFMA (parity / sampling), GM2_BF16 = bf16 MFMA
+ * with fp32 accumulation, fp32 master weights and fp32 BatchNorm / loss / optimizer math */
+enum { GM2_F32 = 0, GM2_BF16 = 1 };
+
+/* model + call geometry. G = genes (input_dim), H = hidden_dim (multiple of 128),
+ * L = latent_dim (divides 256), batch_max = the largest row count any call will pass. */
+typedef struct gm2_dims {
+  int64_t G, H, L;
+  int64_t batch_max;
+} gm2_dims;
+
+/* one batch of strain rows. `data` is the resident u8 presence/absence matrix [n_rows][ld_data]
+ * (ld_data a multiple of 16 and >= roundup(G,128), zero padded), `rows` the int32 row indices of
+ * this batch (NULL = rows 0..n-1), `eps` the N(0,1) draws of model.py:102 as fp32 [n][L]. */
+typedef struct gm2_batch {
+  const uint8_t* data;
+  int64_t ld_data;
+  const int32_t* rows;
+  int64_t n;
+  const float* eps;
+} gm2_batch;
+
+/* device scalar block (fp32[GM2_NUM_SCALARS]) read by the kernels, written by the host per step
+ * so a captured graph can replay: */
+enum {
+  GM2_S_BETA = 0,          /* KL weight (loss_components.py:76-88)                         */
+  GM2_S_WGAMMA = 1,        /* weight * gamma of GeneAbundanceLoss (0 = absent)              */
+  GM2_S_LAMBDA = 2,        /* lambda_l1 (0 = absent)                                        */
+  GM2_S_NEG_STEP = 3,      /* -lr / (1 - beta1^t)                                           */
+  GM2_S_BC2_SQRT = 4,      /* sqrt(1 - beta2^t)                                             */
+  GM2_S_MAX_NORM = 5,      /* clip_grad_norm_ max_norm (<= 0: no clipping)                  */
+  GM2_S_ONE_MINUS_B1 = 6,
+  GM2_S_BETA2 = 7,
+  GM2_S_ONE_MINUS_B2 = 8,
+  GM2_S_ADAM_EPS = 9
+};
+
+/* loss record (fp64[GM2_LOSS_SLOTS], device) filled per call:
+ *   [0] sum of BCE elements           (ReconstructionLoss, loss_components.py:49-50)
+ *   [1] sum of reconstructed p        (GeneAbundanceLoss before w*gamma; p >= 0 so |.| = id)
+ *   [2] sum(1 + lv - mu^2 - exp(lv))  (KLDivergenceLoss before -0.5*beta)
+ *   [3] sum |theta| over all params   (l1_regularization before lambda; gm2_grad_norm)
+ *   [4] total gradient L2 norm after L1 (clip_grad_norm_ total_norm; gm2_grad_norm)       */
+#define GM2_LOSS_SLOTS 8
+
+const char* gm2_last_error(void);
+int gm2_abi_version(void);
+
+/* sizes / layout queries (host only) */
+int gm2_param_count(const gm2_dims* d, int64_t* n_params);
+int gm2_param_offsets(const gm2_dims* d, int64_t* offsets /* [GM2_NUM_PARAMS + 1] */);
+int gm2_workspace_size(const gm2_dims* d, int precision, size_t* bytes);
+
+/* Initialise a workspace (zero it, lay out GEMM shadows and pads). Call once after allocation. */
+int gm2_workspace_init(const gm2_dims* d, int precision, void* ws, size_t ws_bytes, void* stream);
+
+/* Re-derive the padded GEMM copies of the Linear weights from `params` (after init,
+ * load_state_dict, or any host-side edit). gm2_adam_step keeps them current itself. */
+int gm2_sync_shadows(const gm2_dims* d, int precision, const float* params, void* ws, void* stream);
+
+/* Training forward + backward of one batch (replaces trainer.py:110-118: model(data),
+ * compute_total_loss, total_loss.backward()). Overwrites `grads` with the data-term gradient
+ * (reconstruction + beta*KL + abundance; the L1 term is added by gm2_grad_norm/gm2_adam_step),
+ * updates BN running stats (train-mode BatchNorm, model.py:67-86), writes loss slots [0..2]. */
+int gm2_train_fwd_bwd(const gm2_dims* d, int precision, const gm2_batch* batch, const float* params,
+                      float* grads, float* bn_running, const float* scalars, double* loss, void* ws,
+                      void* stream);
+
+/* L1 term + clip_grad_norm_ statistics (trainer.py:119; loss_components.py:167-184): computes
+ * ||g + lambda*sign(theta)||_2 (loss slot [4]), sum|theta| (slot [3]) and the clip coefficient
+ * min(1, max_norm/(norm+1e-6)) kept in the workspace for gm2_adam_step. */
+int gm2_grad_norm(const gm2_dims* d, int precision, const float* params, const float* grads,
+                  const float* scalars, double* loss, void* ws, void* stream);
+
+/* torch.optim.Adam step (trainer.py:120; lr from StepLR, experiments.py:260-265) on
+ * (grads + lambda*sign(theta)) * clip, then refreshes the GEMM shadows. */
+int gm2_adam_step(const gm2_dims* d, int precision, float* params, const float* grads, float* exp_avg,
+                  float* exp_avg_sq, const float* scalars, void* ws, void* stream);
+
+/* Validation forward (trainer.py:139-149): eval-mode BatchNorm (running stats), reparam with the
+ * given eps, loss slots [0..2]; nothing else is written. */
+int gm2_eval_forward(const gm2_dims* d, int precision, const gm2_batch* batch, const float* params,
+                     const float* bn_running, const float* scalars, double* loss, void* ws, void* stream);
+
+/* Sampling decode (extras.py:192-203, main.py:351-370): z fp32 [n][L] -> eval-mode decoder in exact
+ * fp32 -> mask u8 [n][ld_mask] = (sigmoid(logit) > 0.5), optionally probs fp32 [n][ld_probs]
+ * (NULL to skip). n <= batch_max. */
+int gm2_decode_mask(const gm2_dims* d, const float* params, const float* bn_running, const float* z,
+                    int64_t n, uint8_t* mask, int64_t ld_mask, float* probs, int64_t ld_probs, void* ws,
+                    void* stream);
+
+/* Encoder of VAE.encode (model.py:95-98), eval-mode BatchNorm, on `batch` (eps unused):
+ * mu and logvar fp32 [n][L] (either may be NULL). Used by get_latent_variables (extras.py:205-228). */
+int gm2_encode(const gm2_dims* d, int precision, const gm2_batch* batch, const float* params,
+               const float* bn_running, float* mu, float* logvar, void* ws, void* stream);
+
+/* Raw NT GEMM primitive, exposed for kernel-level tests: C[M][ldc] (fp32) = P[M][K] * Q[N][K]^T,
+ * P/Q of `precision` element type with >= roundup(M|N,128) allocated rows, K % 64 == 0. */
+int gm2_gemm_nt(int precision, const void* P, int64_t ldp, const void* Q, int64_t ldq, float* C,
+                int64_t ldc, int64_t M, int64_t N, int64_t K, int splits, float* slab_ws, void* stream);
+
+/* Live kernel timing for the benchmark's roofline figure: between gm2_timing_begin(classes) and
+ * gm2_timing_end, every launch of a selected kernel class is bracketed by a hipEvent pair on its
+ * own stream; gm2_timing_end synchronises those events and returns their summed duration and the
+ * launch count. Classes: GM2_KC_RECON_LOSS (decoder output layer GEMM + fused BCE / dlogits
+ * epilogue), GM2_KC_GEMM_STORE (every other GEMM), GM2_KC_MASK (sampling output layer GEMM). */
+enum { GM2_KC_RECON_LOSS = 1, GM2_KC_GEMM_STORE = 2, GM2_KC_MASK = 4 };
+int gm2_timing_begin(int kernel_classes);
+int gm2_timing_end(double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GM2_H */
