@@ -79,7 +79,7 @@ struct Layout {
   int64_t es;
   // GEMM shadows (T)
   int64_t sE0, sE1, sE1T, sE2, sE2T, sHD, sHDT, sD0, sD0T, sD1, sD1T, sD2, sD2T, sD3, sD3T;
-  int64_t X, XT, Y[6], A[6], AT[6], save[6], HD, Z, ZT, dL, dLT, slabs, slab_cap, dY, dYT, dH, dHT;
+  int64_t X, XT, XB, Y[6], A[6], AT[6], save[6], HD, Z, ZT, dL, dLT, slabs, slab_cap, dY, dYT, dH, dHT;
   int64_t bnpart, colpart, colpart_cap, losspart, losspart_cap, klpart, gradpart, clip, total;
 };
 
@@ -114,6 +114,7 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.sD3T = take(H * d.Gp * es);
   o.X = take(Bm * d.Gp * es);
   o.XT = take(d.Gp * Bm * es);
+  o.XB = take(d.Gp * (Bm / 32) * 4);
   for (int i = 0; i < 6; ++i) {
     o.Y[i] = take(Bm * H * 4);
     o.A[i] = take(Bm * H * es);
@@ -155,11 +156,12 @@ struct Ctx {
   float* f(int64_t off) const { return (float*)(ws + off); }
 };
 
-int pick_splits(int tm, int tn, int nk) {
-  const int tiles = tm * tn;
-  int s = (512 + tiles - 1) / tiles;
+// split-K so that a launch has ~1 block per CU (256-tile, 1 block/CU resident) or ~2 (128-tile)
+int pick_splits(int tiles, int nk, int tile) {
+  const int target = tile == 256 ? 256 : 512;
+  int s = (target + tiles - 1) / tiles;
   s = std::min(s, 8);
-  s = std::min(s, std::max(1, nk / 4));
+  s = std::min(s, std::max(1, nk / 8));
   return std::max(1, s);
 }
 
@@ -168,30 +170,50 @@ template <typename T>
 int gemm_to_slabs(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64_t ldq, int Np, int M, int N,
                   int K, int64_t ldc) {
   GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0};
-  const int S = pick_splits(Mp / kTile, Np / kTile, K / E<T>::KT);
+  const int tile = gemm_tile_for<T>(g);
+  const int S = pick_splits((Mp / tile) * (Np / tile), K / E<T>::KT, tile);
   const int64_t slab = (int64_t)Mp * ldc;
   if ((int64_t)S * slab > c.lo.slab_cap) throw Gm2Error("slab capacity exceeded");
   return launch_gemm_store<T>(g, S, c.f(c.lo.slabs), nullptr, 0, ldc, slab, nullptr, c.s);
 }
 
+// GEMM into C0/C1 (fp32, row split at msplit). Launches with too few tiles to fill the chip are
+// split over K into slabs and summed by k_slab_sum (deterministic order).
 template <typename T>
 void gemm_to(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64_t ldq, int Np, int M, int N, int K,
              float* C0, float* C1, int msplit, int64_t ldc) {
   GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0};
-  launch_gemm_store<T>(g, 1, C0, C1, msplit, ldc, 0, nullptr, c.s);
+  const int tile = gemm_tile_for<T>(g);
+  int S = pick_splits((Mp / tile) * (Np / tile), K / E<T>::KT, tile);
+  const int64_t slab = round_up((int64_t)M * N, 4);
+  if ((int64_t)S * slab > c.lo.slab_cap) S = 1;
+  if (S <= 1) {
+    launch_gemm_store<T>(g, 1, C0, C1, msplit, ldc, 0, nullptr, c.s);
+    return;
+  }
+  S = launch_gemm_store<T>(g, S, c.f(c.lo.slabs), nullptr, 0, N, slab, nullptr, c.s);
+  launch_slab_sum(c.f(c.lo.slabs), S, slab, M, N, C0, C1, C1 ? msplit : M, ldc, c.s);
 }
 
 // the 6 BatchNorm blocks: (linear weight, linear bias, bn gamma, bn beta)
 const int kBlk[6][4] = {{E0W, E0B, E1G, E1BT}, {E3W, E3B, E4G, E4BT}, {E6W, E6B, E7G, E7BT},
                         {D0W, D0B, D1G, D1BT}, {D3W, D3B, D4G, D4BT}, {D6W, D6B, D7G, D7BT}};
 
+// Tensor tables. kind 0: the 9 Linear weights with natural + transposed shadows (tile0 counts
+// 64x64 tiles; used by the fp32 -> shadow sync). kind 1: all 30 parameters in reference order, the
+// weights with their natural shadow (tile0 counts 4096-element blocks; fused Adam). kind 2: the
+// weights that have a transposed shadow (tile0 counts 64x64 tiles; shadow transpose).
 template <typename T>
-TensorTable make_table(const Ctx<T>& c) {
+TensorTable make_table(const Ctx<T>& c, int kind = 0) {
   const Dims& d = c.d;
   const Layout& l = c.lo;
   TensorTable tt{};
+  auto tiles_of = [&](const TensorDesc& e) {
+    return kind == 1 ? (e.rows * e.cols + 4095) / 4096 : ((e.rows + 63) / 64) * ((e.cols + 63) / 64);
+  };
   auto add = [&](int pi, int64_t rows, int64_t cols, int64_t sh, int64_t sld, int64_t srow0, int64_t shT,
                  int64_t tld) {
+    if (kind == 2 && shT < 0) return;
     TensorDesc& e = tt.t[tt.n];
     e.off = d.off[pi];
     e.rows = rows;
@@ -199,22 +221,33 @@ TensorTable make_table(const Ctx<T>& c) {
     e.shadow = sh >= 0 ? (void*)(c.ws + sh) : nullptr;
     e.sld = sld;
     e.srow0 = srow0;
-    e.shadowT = shT >= 0 ? (void*)(c.ws + shT) : nullptr;
+    e.shadowT = (shT >= 0 && kind != 1) ? (void*)(c.ws + shT) : nullptr;
     e.tld = tld;
-    e.tile0 = tt.n == 0 ? 0
-                        : tt.t[tt.n - 1].tile0 + ((tt.t[tt.n - 1].rows + 63) / 64) * ((tt.t[tt.n - 1].cols + 63) / 64);
+    e.tile0 = tt.n == 0 ? 0 : tt.t[tt.n - 1].tile0 + tiles_of(tt.t[tt.n - 1]);
     tt.n++;
   };
   const int64_t H = d.H, G = d.G, L = d.L;
+  auto vec = [&](int pi, int64_t n) {
+    if (kind == 1) add(pi, 1, n, -1, 0, 0, -1, 0);
+  };
   add(E0W, H, G, l.sE0, d.Gp, 0, -1, 0);
+  vec(E0B, H); vec(E1G, H); vec(E1BT, H);
   add(E3W, H, H, l.sE1, H, 0, l.sE1T, H);
+  vec(E3B, H); vec(E4G, H); vec(E4BT, H);
   add(E6W, H, H, l.sE2, H, 0, l.sE2T, H);
+  vec(E6B, H); vec(E7G, H); vec(E7BT, H);
   add(MUW, L, H, l.sHD, H, 0, l.sHDT, d.K2L);
+  vec(MUB, L);
   add(LVW, L, H, l.sHD, H, L, l.sHDT, d.K2L);
+  vec(LVB, L);
   add(D0W, H, L, l.sD0, d.Lp, 0, l.sD0T, H);
+  vec(D0B, H); vec(D1G, H); vec(D1BT, H);
   add(D3W, H, H, l.sD1, H, 0, l.sD1T, H);
+  vec(D3B, H); vec(D4G, H); vec(D4BT, H);
   add(D6W, H, H, l.sD2, H, 0, l.sD2T, H);
+  vec(D6B, H); vec(D7G, H); vec(D7BT, H);
   add(D9W, G, H, l.sD3, H, 0, l.sD3T, d.Gp);
+  vec(D9B, G);
   return tt;
 }
 
@@ -234,8 +267,8 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   const int Bp = (int)round_up(B, kTile);
   const int H = (int)d.H, L = (int)d.L;
   // 1) strain rows -> X, X^T
-  launch_gather_rows<T>(b->data, b->ld_data, b->rows, B, (int)d.G, c.t(l.X), d.Gp, (int)d.Gp, c.t(l.XT), d.Bm, Bp,
-                        c.s);
+  launch_gather_rows<T>(b->data, b->ld_data, b->rows, B, (int)d.G, c.t(l.X), d.Gp, (int)d.Gp,
+                        train ? c.t(l.XT) : nullptr, d.Bm, Bp, (uint32_t*)(c.ws + l.XB), d.Bm / 32, c.s);
   // 2) encoder blocks
   const T* in = c.t(l.X);
   int64_t ldin = d.Gp;
@@ -262,12 +295,14 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   }
   // 3) output layer + reconstruction loss (+ dlogits)
   GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, B, (int)d.G, H, Bp, (int)d.Gp, 0};
-  launch_gemm_recon_loss<T>(g, prm + d.off[D9B], c.t(l.X), d.Gp, with_grad, scal, c.t(l.dL), d.Gp, c.t(l.dLT), d.Bm,
+  launch_gemm_recon_loss<T>(g, prm + d.off[D9B], (const uint32_t*)(c.ws + l.XB), d.Bm / 32, with_grad, scal, c.t(l.dL),
+                            d.Gp, c.t(l.dLT), d.Bm,
                             c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
   const int nblk = gemm_recon_grid_blocks<T>(g);
   launch_reduce_to(c.f(l.losspart), nblk, 2, 2, loss + 0, c.s);
   launch_reduce_to(c.f(l.klpart), Bp / 64, 1, 1, loss + 2, c.s);
-  if (with_grad) launch_colsum(c.f(l.colpart), Bp / kTile, d.Gp, (int)d.G, grads + d.off[D9B], nullptr, 0, c.s);
+  if (with_grad)
+    launch_colsum(c.f(l.colpart), gemm_recon_row_tiles<T>(g), d.Gp, (int)d.G, grads + d.off[D9B], nullptr, 0, c.s);
 }
 
 template <typename T>
@@ -420,13 +455,15 @@ int gm2_adam_step(const gm2_dims* d, int prec, float* params, const float* grads
     const Layout lo = make_layout(d, prec);
     const int64_t n = lo.d.off[NP];
     const float* clip = (const float*)((char*)ws + lo.clip);
-    launch_adam(grads, params, m, v, n, scalars, clip, (hipStream_t)stream);
+    (void)n;
     if (prec == GM2_F32) {
       Ctx<float> c(lo, ws, stream);
-      launch_shadow_sync<float>(make_table(c), params, c.s);
+      launch_adam_fused<float>(make_table(c, 1), grads, params, m, v, scalars, clip, c.s);
+      launch_shadow_transpose<float>(make_table(c, 2), c.s);
     } else {
       Ctx<bf16_t> c(lo, ws, stream);
-      launch_shadow_sync<bf16_t>(make_table(c), params, c.s);
+      launch_adam_fused<bf16_t>(make_table(c, 1), grads, params, m, v, scalars, clip, c.s);
+      launch_shadow_transpose<bf16_t>(make_table(c, 2), c.s);
     }
   });
 }
@@ -471,8 +508,8 @@ int gm2_encode(const gm2_dims* d, int prec, const gm2_batch* batch, const float*
       const int B = (int)b.n, Bp = (int)round_up(B, kTile), H = (int)dd.H, L = (int)dd.L;
       if (B <= 0 || B > dd.Bm) throw Gm2Error("encode rows outside (0, batch_max]");
       float* bn = const_cast<float*>(bn_running);
-      launch_gather_rows<T>(b.data, b.ld_data, b.rows, B, (int)dd.G, c.t(lo.X), dd.Gp, (int)dd.Gp, c.t(lo.XT), dd.Bm,
-                            Bp, c.s);
+      launch_gather_rows<T>(b.data, b.ld_data, b.rows, B, (int)dd.G, c.t(lo.X), dd.Gp, (int)dd.Gp, nullptr, dd.Bm,
+                            Bp, nullptr, 0, c.s);
       const T* in = c.t(lo.X);
       int64_t ldin = dd.Gp;
       int Kin = (int)dd.Gp;

@@ -4,14 +4,20 @@
 //  * T = bf16_t : v_mfma_f32_16x16x32_bf16 (training fast path, fp32 accumulate)
 //  * T = float  : v_mfma_f32_16x16x4_f32   (exact-f32 path: sampling decode + parity training)
 //
-// Block tile 128x128, 4 waves (2x2), each wave 64x64 = 4x4 MFMA tiles; one K-step = one
-// 128-byte row chunk per operand row (64 bf16 / 32 f32). Operands are staged HBM->LDS with
-// global_load_lds_dwordx4 (no VGPR round trip) into a 2-stage ring; the LDS image is
-// XOR-swizzled (chunk ^= (row>>1)&7) by permuting the per-lane SOURCE address, which makes the
-// 16-lane ds_read_b128 groups conflict-free (see DESIGN.md §GEMM).
+// Tile configurations (Cfg<BM, BN, WGM, WGN>): a block of WGM x WGN waves owns a BM x BN output
+// tile, each wave a (BM/WGM) x (BN/WGN) sub-tile of 16x16 MFMA fragments.
+//   Big   256x256, 8 waves (2x4, 128x64 per wave): the G x H GEMMs (half the L2->LDS bytes per
+//         FLOP of a 128x128 tile, which at full MFMA rate would need ~36 TB/s of L2 bandwidth).
+//   Small 128x128, 4 waves (2x2, 64x64 per wave): the H x H / latent GEMMs.
+// One K-step = one 128-byte row chunk per operand row (64 bf16 / 32 f32). Operands are staged
+// HBM->LDS with global_load_lds_dwordx4 (no VGPR round trip) into a 2-stage ring; the LDS image
+// is XOR-swizzled (chunk ^= (row>>1)&7) through the per-lane SOURCE address, which makes the
+// 16-lane ds_read_b128 groups conflict-free (DESIGN.md §GEMM).
+// Block -> tile: 1-D grid, bijective XCD remap (consecutive logical tiles share an XCD's L2),
+// then split-K slice outermost and GROUP_M=8 grouped (m fastest) tile order.
 //
-// Contract (checked on the host in api.cpp): every operand buffer has >= roundup(M|N,128)
-// rows, K is a multiple of 64, pads are zero. Split-K over blockIdx.z.
+// Contract (checked on the host): every operand buffer has >= roundup(M|N, tile) rows, K is a
+// multiple of 64, pads are zero.
 #include "gm2_common.hpp"
 #include "gm2_kernels.hpp"
 
@@ -22,92 +28,122 @@ namespace gm2 {
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kStageBytes = 2 * kTile * 128;  // A + B, 16 KiB each
-constexpr int kLdsBytes = 2 * kStageBytes;    // double buffered: 64 KiB
-
 typedef __attribute__((address_space(3))) void lds_void;
 
-template <typename T>
-__device__ __forceinline__ void stage_tile(const T* __restrict__ P, int64_t ldp, int row0, int k0,
-                                           char* lds, int wid, int lane) {
-  // 128 rows x 128 B = 1024 16-byte chunks; 256 threads -> 4 glds per thread.
-  // wave instruction j covers chunks [j*256 + wid*64, +64): LDS dest is lane-linear.
-  constexpr int EPC = 16 / sizeof(T);  // elements per 16-byte chunk
+template <int BM_, int BN_, int WGM_, int WGN_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_;
+  static constexpr int NT = 64 * WGM * WGN;          // threads
+  static constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  static constexpr int FM = WTM / 16, FN = WTN / 16;  // 16x16 fragments per wave
+  static constexpr int STAGE = (BM + BN) * 128;      // bytes per pipeline stage
+  static constexpr int LDS = 2 * STAGE;
+};
+using Big = Cfg<256, 256, 2, 4>;
+using Small = Cfg<128, 128, 2, 2>;
+
+struct TileXY {
+  int m0, n0, split, t;
+};
+
+// XCD-aware, grouped tile order (see header)
+template <class C>
+__device__ __forceinline__ TileXY tile_of(int tm, int tn) {
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int ntile = tm * tn;
+  const int split = wg / ntile;
+  const int t = wg - split * ntile;
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tn;
+  const int grp = t / per_group;
+  const int first_m = grp * GROUP;
+  const int gsize = min(tm - first_m, GROUP);
+  const int in = t - grp * per_group;
+  const int pm = first_m + in % gsize;
+  const int pn = in / gsize;
+  return {pm * C::BM, pn * C::BN, split, pm * tn + pn};
+}
+
+template <class C, typename T, int ROWS>
+__device__ __forceinline__ void stage_rows(const T* __restrict__ P, int64_t ldp, int row0, int k0, char* lds,
+                                           int wid, int lane) {
+  // ROWS rows x 128 B = ROWS*8 16-byte chunks; wave instruction j covers chunks
+  // [j*NT + wid*64, +64): the LDS destination is lane-linear (glds semantics).
+  constexpr int EPC = 16 / sizeof(T);
+  constexpr int PER = ROWS * 8 / C::NT;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int i = j * 256 + wid * 64 + lane;
+  for (int j = 0; j < PER; ++j) {
+    const int i = j * C::NT + wid * 64 + lane;
     const int row = i >> 3;
-    const int cs = i & 7;
-    const int c = cs ^ ((row >> 1) & 7);
+    const int c = (i & 7) ^ ((row >> 1) & 7);
     const T* src = P + (int64_t)(row0 + row) * ldp + k0 + c * EPC;
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (j * 256 + wid * 64) * 16),
-                                     16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (j * C::NT + wid * 64) * 16), 16, 0, 0);
   }
 }
 
 __device__ __forceinline__ int frag_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
-// Main loop. acc[mi][ni] holds rows wm*64+mi*16+4*(lane>>4)+j, cols wn*64+ni*16+(lane&15).
-template <typename T>
-__device__ __forceinline__ void gemm_mainloop(const T* __restrict__ P, int64_t ldp,
-                                              const T* __restrict__ Q, int64_t ldq, int m0, int n0,
-                                              int kbeg, int nk, char* smem, f32x4 (&acc)[4][4]) {
+// Main loop. acc[mi][ni][j] = C[m0 + wm*WTM + mi*16 + 4*(lane>>4) + j][n0 + wn*WTN + ni*16 + (lane&15)]
+template <class C, typename T>
+__device__ __forceinline__ void mainloop(const T* __restrict__ P, int64_t ldp, const T* __restrict__ Q, int64_t ldq,
+                                         int m0, int n0, int kbeg, int nk, char* smem,
+                                         f32x4 (&acc)[C::FM][C::FN]) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / C::WGN, wn = wid % C::WGN;
   constexpr int KT = E<T>::KT;
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < C::FM; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < C::FN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (nk <= 0) return;
 
-  stage_tile<T>(P, ldp, m0, kbeg, smem, wid, lane);
-  stage_tile<T>(Q, ldq, n0, kbeg, smem + kTile * 128, wid, lane);
+  stage_rows<C, T, C::BM>(P, ldp, m0, kbeg, smem, wid, lane);
+  stage_rows<C, T, C::BN>(Q, ldq, n0, kbeg, smem + C::BM * 128, wid, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * kStageBytes;
+    char* cur = smem + (kt & 1) * C::STAGE;
     if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
+      char* nxt = smem + ((kt + 1) & 1) * C::STAGE;
       const int kn = kbeg + (kt + 1) * KT;
-      stage_tile<T>(P, ldp, m0, kn, nxt, wid, lane);
-      stage_tile<T>(Q, ldq, n0, kn, nxt + kTile * 128, wid, lane);
+      stage_rows<C, T, C::BM>(P, ldp, m0, kn, nxt, wid, lane);
+      stage_rows<C, T, C::BN>(Q, ldq, n0, kn, nxt + C::BM * 128, wid, lane);
     }
     const char* sA = cur;
-    const char* sB = cur + kTile * 128;
+    const char* sB = cur + C::BM * 128;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int c = s * 4 + (lane >> 4);
       if constexpr (sizeof(T) == 2) {
-        bf16x8 a[4], b[4];
+        bf16x8 b[C::FN];
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-          a[mi] = *(const bf16x8*)(sA + frag_off(wm * 64 + mi * 16 + (lane & 15), c));
+        for (int ni = 0; ni < C::FN; ++ni)
+          b[ni] = *(const bf16x8*)(sB + frag_off(wn * C::WTN + ni * 16 + (lane & 15), c));
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          b[ni] = *(const bf16x8*)(sB + frag_off(wn * 64 + ni * 16 + (lane & 15), c));
+        for (int mi = 0; mi < C::FM; ++mi) {
+          const bf16x8 a = *(const bf16x8*)(sA + frag_off(wm * C::WTM + mi * 16 + (lane & 15), c));
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+          for (int ni = 0; ni < C::FN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[ni], acc[mi][ni], 0, 0, 0);
+        }
       } else {
-        f32x4 a[4], b[4];
+        f32x4 b[C::FN];
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-          a[mi] = *(const f32x4*)(sA + frag_off(wm * 64 + mi * 16 + (lane & 15), c));
+        for (int ni = 0; ni < C::FN; ++ni)
+          b[ni] = *(const f32x4*)(sB + frag_off(wn * C::WTN + ni * 16 + (lane & 15), c));
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          b[ni] = *(const f32x4*)(sB + frag_off(wn * 64 + ni * 16 + (lane & 15), c));
+        for (int mi = 0; mi < C::FM; ++mi) {
+          const f32x4 a = *(const f32x4*)(sA + frag_off(wm * C::WTM + mi * 16 + (lane & 15), c));
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
-              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mi][j], b[ni][j], acc[mi][ni], 0, 0, 0);
+            for (int ni = 0; ni < C::FN; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[ni][j], acc[mi][ni], 0, 0, 0);
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -119,30 +155,29 @@ __device__ __forceinline__ void gemm_mainloop(const T* __restrict__ P, int64_t l
 // Epilogue 1: fp32 store. Rows m < msplit go to C0, rows >= msplit to C1 (row m - msplit); the
 // split-K slice z writes slab z (C0 + z*slab). Optional per-column bias.
 // ---------------------------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(kThreads, 2) void k_gemm_store(GemmArgs<T> g, float* __restrict__ C0,
-                                                          float* __restrict__ C1, int msplit,
-                                                          int64_t ldc, int64_t slab,
-                                                          const float* __restrict__ bias) {
+template <class C, typename T>
+__global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __restrict__ C0, float* __restrict__ C1,
+                                                    int msplit, int64_t ldc, int64_t slab,
+                                                    const float* __restrict__ bias) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int n0 = blockIdx.x * kTile, m0 = blockIdx.y * kTile;
-  const int kbeg = blockIdx.z * g.k_per_split;
+  const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
+  const int kbeg = tl.split * g.k_per_split;
   const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = (kend - kbeg) / E<T>::KT;
-  f32x4 acc[4][4];
-  gemm_mainloop<T>(g.P, g.ldp, g.Q, g.ldq, m0, n0, kbeg, nk, smem, acc);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
-  float* Cz = C0 + (int64_t)blockIdx.z * slab;
+  f32x4 acc[C::FM][C::FN];
+  mainloop<C, T>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
+  float* Cz = C0 + (int64_t)tl.split * slab;
 #pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int n = n0 + wn * 64 + ni * 16 + (lane & 15);
+  for (int ni = 0; ni < C::FN; ++ni) {
+    const int n = tl.n0 + wn * C::WTN + ni * 16 + (lane & 15);
     if (n >= g.N) continue;
     const float bn = bias ? bias[n] : 0.f;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < C::FM; ++mi)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int m = m0 + wm * 64 + mi * 16 + 4 * (lane >> 4) + j;
+        const int m = tl.m0 + wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
         if (m >= g.M) continue;
         const float v = acc[mi][ni][j] + bn;
         if (m < msplit) Cz[(int64_t)m * ldc + n] = v;
@@ -156,93 +191,164 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_store(GemmArgs<T> g, float
 // :111-115 gene abundance) and, in training, dL/dlogit exactly as autograd composes
 // Sigmoid->BCE: dp = (p-x)/max((1-p)p, 1e-12) + w*gamma ; dl = dp*(1-p)*p.
 // (sign(colsum p) == 1 wherever p > 0, and dl == 0 wherever p == 0: no batch-wide pass needed.)
-// Writes dL [m][ldd] and dL^T [n][lddt] (both T, zero outside the valid MxN box), the per-block
-// sums of BCE and p (loss_part[blk*2 + {0,1}]) and the per-(m-tile, n) column sums of dl.
+// FAST (bf16 training path): v_exp / v_rcp / v_log hardware approximations (~1 ulp) and
+// log(1-p) for log1p(-p); exact libm forms on the fp32 parity path.
+// Writes dL [m][ldd] (row-major, staged through LDS for full-line stores) and dL^T [n][lddt]
+// (4 consecutive m per lane), zero outside the valid M x N box; per-tile BCE and sum(p) into
+// loss_part[tile*2 + {0,1}]; per-(m-tile, n) column sums of dl into colpart.
 // ---------------------------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(kThreads, 2) void k_gemm_recon_loss(
-    GemmArgs<T> g, const float* __restrict__ bias, const T* __restrict__ X, int64_t ldx,
-    int with_grad, const float* __restrict__ scal, T* __restrict__ dL, int64_t ldd,
-    T* __restrict__ dLT, int64_t lddt, float* __restrict__ loss_part, float* __restrict__ colpart,
-    int64_t ldcol) {
+template <bool FAST>
+__device__ __forceinline__ void recon_elem(float l, float x, float wgam, float& e, float& p, float& dl) {
+  if constexpr (FAST) {
+    const float ex = __builtin_amdgcn_exp2f(-l * 1.4426950408889634f);
+    p = __builtin_amdgcn_rcpf(1.0f + ex);
+    const float omp = 1.0f - p;
+    const float t = x != 0.f ? p : omp;
+    e = -fmaxf(__builtin_amdgcn_logf(t) * 0.6931471805599453f, -100.f);
+    const float dp = (p - x) * __builtin_amdgcn_rcpf(fmaxf(omp * p, 1e-12f)) + wgam;
+    dl = dp * omp * p;
+  } else {
+    p = 1.0f / (1.0f + expf(-l));
+    e = x != 0.f ? -fmaxf(logf(p), -100.f) : -fmaxf(log1pf(-p), -100.f);
+    const float omp = 1.0f - p;
+    const float dp = (p - x) / fmaxf(omp * p, 1e-12f) + wgam;
+    dl = dp * omp * p;
+  }
+}
+
+template <class C, typename T>
+__global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const float* __restrict__ bias,
+                                                         const uint32_t* __restrict__ xbits, int64_t ldxb,
+                                                         int with_grad, const float* __restrict__ scal,
+                                                         T* __restrict__ dL, int64_t ldd, T* __restrict__ dLT,
+                                                         int64_t lddt, float* __restrict__ loss_part,
+                                                         float* __restrict__ colpart, int64_t ldcol) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int n0 = blockIdx.x * kTile, m0 = blockIdx.y * kTile;
-  f32x4 acc[4][4];
-  gemm_mainloop<T>(g.P, g.ldp, g.Q, g.ldq, m0, n0, 0, g.K / E<T>::KT, smem, acc);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
+  constexpr bool FAST = sizeof(T) == 2;
+  constexpr int XW = C::WTM / 32;  // target words per lane per column (bit-packed X^T)
+  const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
+  const TileXY tl = tile_of<C>(tm, tn);
+  f32x4 acc[C::FM][C::FN];
+  mainloop<C, T>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
+  const int q = lane >> 4;
   const float wgam = scal[kScalWGamma];
   float bce = 0.f, psum = 0.f;
-  float csum[4] = {0.f, 0.f, 0.f, 0.f};
+  float csum[C::FN];
+  // phase 1: loss terms and dl in registers (dl overwrites the accumulator)
 #pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int n = n0 + wn * 64 + ni * 16 + (lane & 15);
+  for (int ni = 0; ni < C::FN; ++ni) {
+    csum[ni] = 0.f;
+    const int n = tl.n0 + wn * C::WTN + ni * 16 + (lane & 15);
     const bool nok = n < g.N;
     const float bn = nok ? bias[n] : 0.f;
+    uint32_t xw[XW];
+    const uint32_t* xp = xbits + (int64_t)n * ldxb + (tl.m0 + wm * C::WTM) / 32;
+    if constexpr (XW == 4) {
+      const uint4 v = *(const uint4*)xp;
+      xw[0] = v.x; xw[1] = v.y; xw[2] = v.z; xw[3] = v.w;
+    } else {
+      const uint2 v = *(const uint2*)xp;
+      xw[0] = v.x; xw[1] = v.y;
+    }
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int mb = m0 + wm * 64 + mi * 16 + 4 * (lane >> 4);
-      float dl4[4];
+    for (int mi = 0; mi < C::FM; ++mi) {
+      const int mb = tl.m0 + wm * C::WTM + mi * 16 + 4 * q;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int m = mb + j;
         float dl = 0.f;
-        if (nok && m < g.M) {
-          const float l = acc[mi][ni][j] + bn;
-          const float p = 1.0f / (1.0f + expf(-l));
-          const float x = E<T>::ld(X + (int64_t)m * ldx + n);
-          // BCE element (x in {0,1}): (x-1)*max(log1p(-p),-100) - x*max(log(p),-100)
-          const float e = x != 0.f ? -fmaxf(logf(p), -100.f) : -fmaxf(log1pf(-p), -100.f);
+        if (nok && mb + j < g.M) {
+          const float x = (float)((xw[mi >> 1] >> ((mi & 1) * 16 + 4 * q + j)) & 1u);
+          float e, p;
+          recon_elem<FAST>(acc[mi][ni][j] + bn, x, wgam, e, p, dl);
           bce += e;
           psum += p;
-          const float omp = 1.0f - p;
-          const float dp = (p - x) / fmaxf(omp * p, 1e-12f) + wgam;
-          dl = dp * omp * p;
           csum[ni] += dl;
         }
-        dl4[j] = dl;
-      }
-      if (with_grad) {
-        if (mb < g.Mp) {  // padded rows are written (as zeros) so K-pads stay zero downstream
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (n < g.Np) dL[(int64_t)(mb + j) * ldd + n] = E<T>::cvt(dl4[j]);
-          if (n < g.Np) {
-            if constexpr (sizeof(T) == 2) {
-              uint2 pk;
-              pk.x = (uint32_t)f2bf(dl4[0]) | ((uint32_t)f2bf(dl4[1]) << 16);
-              pk.y = (uint32_t)f2bf(dl4[2]) | ((uint32_t)f2bf(dl4[3]) << 16);
-              *(uint2*)(dLT + (int64_t)n * lddt + mb) = pk;
-            } else {
-              *(f32x4*)(dLT + (int64_t)n * lddt + mb) = f32x4{dl4[0], dl4[1], dl4[2], dl4[3]};
-            }
-          }
-        }
+        acc[mi][ni][j] = dl;
       }
     }
   }
-  // block reductions: BCE, sum(p) -> loss_part; column sums of dl over this block's 128 rows
-  // the main loop ended on a barrier: reuse the staging LDS for the reductions (one LDS object)
-  float(*red)[4] = (float(*)[4])smem;
-  float(*colred)[128] = (float(*)[128])(smem + 64);
+  if (with_grad) {
+    // phase 2: dL^T [n][m] through an LDS image [BN][BM+8] (each lane owns 4 consecutive m of one
+    // n: one 8/16-byte LDS write), then full-row coalesced stores
+    constexpr int EPC = 16 / sizeof(T);
+    {
+      constexpr int PT = C::BM + 8;
+      T* img = (T*)smem;
+#pragma unroll
+      for (int mi = 0; mi < C::FM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < C::FN; ++ni) {
+          const int nl = wn * C::WTN + ni * 16 + (lane & 15);
+          const int ml = wm * C::WTM + mi * 16 + 4 * q;
+          if constexpr (sizeof(T) == 2) {
+            uint2 pk;
+            pk.x = (uint32_t)f2bf(acc[mi][ni][0]) | ((uint32_t)f2bf(acc[mi][ni][1]) << 16);
+            pk.y = (uint32_t)f2bf(acc[mi][ni][2]) | ((uint32_t)f2bf(acc[mi][ni][3]) << 16);
+            *(uint2*)(img + nl * PT + ml) = pk;
+          } else {
+            *(f32x4*)(img + nl * PT + ml) = acc[mi][ni];
+          }
+        }
+      __syncthreads();
+      constexpr int CPR = C::BM / EPC;
+      for (int i = threadIdx.x; i < C::BN * CPR; i += C::NT) {
+        const int r = i / CPR, cch = i % CPR;
+        *(uint4*)(dLT + (int64_t)(tl.n0 + r) * lddt + tl.m0 + cch * EPC) = *(const uint4*)(img + r * PT + cch * EPC);
+      }
+      __syncthreads();
+    }
+    // phase 3: dL [m][n] through an LDS image [BM][BN+8], full-row coalesced stores
+    {
+      constexpr int PR = C::BN + 8;
+      T* img = (T*)smem;
+#pragma unroll
+      for (int mi = 0; mi < C::FM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < C::FN; ++ni) {
+          const int nl = wn * C::WTN + ni * 16 + (lane & 15);
+          const int ml = wm * C::WTM + mi * 16 + 4 * q;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) img[(ml + j) * PR + nl] = E<T>::cvt(acc[mi][ni][j]);
+        }
+      __syncthreads();
+      constexpr int CPR = C::BN / EPC;
+      for (int i = threadIdx.x; i < C::BM * CPR; i += C::NT) {
+        const int r = i / CPR, cch = i % CPR;
+        *(uint4*)(dL + (int64_t)(tl.m0 + r) * ldd + tl.n0 + cch * EPC) = *(const uint4*)(img + r * PR + cch * EPC);
+      }
+    }
+  }
+  __syncthreads();
+  // block reductions (reuse LDS): BCE and sum(p) -> loss_part[tile]; column sums of dl
+  float* red = (float*)smem;          // [2][32]
+  float* colred = (float*)smem + 64;  // [WGM][BN]
   bce = wave_sum(bce);
   psum = wave_sum(psum);
-  if (lane == 0) { red[0][wid] = bce; red[1][wid] = psum; }
+  if (lane == 0) { red[wid] = bce; red[32 + wid] = psum; }
 #pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
+  for (int ni = 0; ni < C::FN; ++ni) {
     float v = csum[ni];
     v += __shfl_xor(v, 16, 64);
     v += __shfl_xor(v, 32, 64);
-    if (lane < 16) colred[wm][wn * 64 + ni * 16 + lane] = v;
+    if (lane < 16) colred[wm * C::BN + wn * C::WTN + ni * 16 + lane] = v;
   }
   __syncthreads();
-  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
   if (threadIdx.x == 0) {
-    loss_part[blk * 2 + 0] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    loss_part[blk * 2 + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    float a = 0.f, b = 0.f;
+    for (int w = 0; w < C::NT / 64; ++w) { a += red[w]; b += red[32 + w]; }
+    loss_part[tl.t * 2 + 0] = a;
+    loss_part[tl.t * 2 + 1] = b;
   }
-  if (with_grad && threadIdx.x < 128) {
-    const int n = n0 + threadIdx.x;
-    if (n < g.N) colpart[(int64_t)blockIdx.y * ldcol + n] = colred[0][threadIdx.x] + colred[1][threadIdx.x];
+  if (with_grad) {
+    for (int c = threadIdx.x; c < C::BN; c += C::NT) {
+      const int n = tl.n0 + c;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < C::WGM; ++w) v += colred[w * C::BN + c];
+      if (n < g.N) colpart[(int64_t)(tl.m0 / C::BM) * ldcol + n] = v;
+    }
   }
 }
 
@@ -250,25 +356,25 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_recon_loss(
 // Epilogue 3: sampling output layer. mask = logit > 0x33C00000 (== sigmoid_fp32 > 0.5,
 // extras.py:200-201); optional probabilities p = sigmoid(logit) (extras.py:198).
 // ---------------------------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(kThreads, 2) void k_gemm_mask(GemmArgs<T> g, const float* __restrict__ bias,
-                                                         uint8_t* __restrict__ mask, int64_t ldm,
-                                                         float* __restrict__ probs, int64_t ldpr) {
+template <class C, typename T>
+__global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float* __restrict__ bias,
+                                                   uint8_t* __restrict__ mask, int64_t ldm, float* __restrict__ probs,
+                                                   int64_t ldpr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int n0 = blockIdx.x * kTile, m0 = blockIdx.y * kTile;
-  f32x4 acc[4][4];
-  gemm_mainloop<T>(g.P, g.ldp, g.Q, g.ldq, m0, n0, 0, g.K / E<T>::KT, smem, acc);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
+  const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
+  f32x4 acc[C::FM][C::FN];
+  mainloop<C, T>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
 #pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int n = n0 + wn * 64 + ni * 16 + (lane & 15);
+  for (int ni = 0; ni < C::FN; ++ni) {
+    const int n = tl.n0 + wn * C::WTN + ni * 16 + (lane & 15);
     if (n >= g.N) continue;
     const float bn = bias[n];
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < C::FM; ++mi)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int m = m0 + wm * 64 + mi * 16 + 4 * (lane >> 4) + j;
+        const int m = tl.m0 + wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
         if (m >= g.M) continue;
         const float l = acc[mi][ni][j] + bn;
         mask[(int64_t)m * ldm + n] = l > kMaskLogitThreshold ? 1 : 0;
@@ -337,70 +443,137 @@ TimedLaunch::~TimedLaunch() {
 // host launchers
 // ------------------------------------------------------------------------------------------------
 template <typename T>
-static void check_gemm(const GemmArgs<T>& g) {
-  if (g.K % kKPad || g.Mp % kTile || g.Np % kTile || g.M > g.Mp || g.N > g.Np || g.M <= 0 || g.N <= 0)
-    throw Gm2Error("gemm: bad dims M=%d N=%d K=%d Mp=%d Np=%d", g.M, g.N, g.K, g.Mp, g.Np);
+static void check_gemm(const GemmArgs<T>& g, int tile) {
+  if (g.K % kKPad || g.Mp % tile || g.Np % tile || g.M > g.Mp || g.N > g.Np || g.M <= 0 || g.N <= 0)
+    throw Gm2Error("gemm: bad dims M=%d N=%d K=%d Mp=%d Np=%d (tile %d)", g.M, g.N, g.K, g.Mp, g.Np, tile);
   if (g.ldp < g.K || g.ldq < g.K) throw Gm2Error("gemm: ld < K");
   if (((uintptr_t)g.P | (uintptr_t)g.Q) & 15) throw Gm2Error("gemm: operands not 16-B aligned");
   if ((g.ldp * sizeof(T)) % 16 || (g.ldq * sizeof(T)) % 16) throw Gm2Error("gemm: ld not 16-B multiple");
 }
 
+// The big tile needs both padded extents divisible by 256 and enough work to fill the chip
 template <typename T>
-int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc,
-                      int64_t slab, const float* bias, hipStream_t s) {
-  check_gemm(g);
+static bool use_big(const GemmArgs<T>& g) {
+  return g.Mp % 256 == 0 && g.Np % 256 == 0 && (int64_t)g.Mp * g.Np >= (int64_t)2048 * 1024 && g.K >= 512;
+}
+
+template <class C, typename T>
+static int store_impl(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
+                      const float* bias, hipStream_t s) {
   GemmArgs<T> a = g;
   const int kt = E<T>::KT;
   const int nkt = g.K / kt;
   splits = std::max(1, std::min(splits, nkt));
   a.k_per_split = (int)(round_up(nkt, splits) / splits) * kt;
   splits = (int)((g.K + a.k_per_split - 1) / a.k_per_split);
-  dim3 grid(g.Np / kTile, g.Mp / kTile, splits);
+  const int tiles = (g.Mp / C::BM) * (g.Np / C::BN) * splits;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)k_gemm_store<C, T>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS) !=
+        hipSuccess)
+      throw Gm2Error("hipFuncSetAttribute(store)");
+    attr = true;
+  }
   TimedLaunch tl(kKcGemmStore, s);
-  hipLaunchKernelGGL(k_gemm_store<T>, grid, dim3(kThreads), kLdsBytes, s, a, C0, C1 ? C1 : C0,
+  hipLaunchKernelGGL((k_gemm_store<C, T>), dim3(tiles), dim3(C::NT), C::LDS, s, a, C0, C1 ? C1 : C0,
                      C1 ? msplit : (1 << 30), ldc, slab, bias);
   GM2_CHECK_LAUNCH();
   return splits;
 }
 
 template <typename T>
-int gemm_recon_grid_blocks(const GemmArgs<T>& g) { return (g.Np / kTile) * (g.Mp / kTile); }
+int gemm_tile_for(const GemmArgs<T>& g) {
+  return use_big(g) ? 256 : 128;
+}
 
 template <typename T>
-void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const T* X, int64_t ldx, int with_grad,
+int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
+                      const float* bias, hipStream_t s) {
+  if (use_big(g)) {
+    check_gemm(g, 256);
+    return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, s);
+  }
+  check_gemm(g, 128);
+  return store_impl<Small, T>(g, splits, C0, C1, msplit, ldc, slab, bias, s);
+}
+
+template <typename T>
+static bool recon_big(const GemmArgs<T>& g);
+
+template <typename T>
+int gemm_recon_grid_blocks(const GemmArgs<T>& g) {
+  const int t = recon_big(g) ? 256 : 128;
+  return (g.Np / t) * (g.Mp / t);
+}
+
+template <typename T>
+int gemm_recon_row_tiles(const GemmArgs<T>& g) {
+  return g.Mp / (recon_big(g) ? 256 : 128);
+}
+
+template <class C, typename T>
+static void recon_impl(const GemmArgs<T>& g, const float* bias, const uint32_t* X, int64_t ldx, int with_grad,
+                       const float* scal, T* dL, int64_t ldd, T* dLT, int64_t lddt, float* loss_part, float* colpart,
+                       int64_t ldcol, hipStream_t s) {
+  check_gemm(g, C::BM);
+  constexpr int lds = std::max<int>(C::LDS, std::max(C::BM * (C::BN + 8), C::BN * (C::BM + 8)) * (int)sizeof(T));
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)k_gemm_recon_loss<C, T>, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+        hipSuccess)
+      throw Gm2Error("hipFuncSetAttribute(recon)");
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_gemm_recon_loss<C, T>), dim3((g.Mp / C::BM) * (g.Np / C::BN)), dim3(C::NT), lds, s, g, bias,
+                     X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol);
+}
+
+// the fp32 parity path stays on the 128-tile (a 256-row fp32 dL image would not fit the LDS)
+template <typename T>
+static bool recon_big(const GemmArgs<T>& g) {
+  return sizeof(T) == 2 && use_big(g);
+}
+
+template <typename T>
+void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const uint32_t* X, int64_t ldx, int with_grad,
                             const float* scal, T* dL, int64_t ldd, T* dLT, int64_t lddt, float* loss_part,
                             float* colpart, int64_t ldcol, hipStream_t s) {
-  check_gemm(g);
-  dim3 grid(g.Np / kTile, g.Mp / kTile, 1);
   TimedLaunch tl(kKcReconLoss, s);
-  hipLaunchKernelGGL(k_gemm_recon_loss<T>, grid, dim3(kThreads), kLdsBytes, s, g, bias, X, ldx, with_grad, scal,
-                     dL, ldd, dLT, lddt, loss_part, colpart, ldcol);
+  bool done = false;
+  if constexpr (sizeof(T) == 2) {
+    if (recon_big(g)) {
+      recon_impl<Big, T>(g, bias, X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol, s);
+      done = true;
+    }
+  }
+  if (!done) recon_impl<Small, T>(g, bias, X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol, s);
   GM2_CHECK_LAUNCH();
 }
 
 template <typename T>
-void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs,
-                      int64_t ldpr, hipStream_t s) {
-  check_gemm(g);
-  dim3 grid(g.Np / kTile, g.Mp / kTile, 1);
+void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs, int64_t ldpr,
+                      hipStream_t s) {
+  check_gemm(g, 128);
   TimedLaunch tl(kKcMask, s);
-  hipLaunchKernelGGL(k_gemm_mask<T>, grid, dim3(kThreads), kLdsBytes, s, g, bias, mask, ldm, probs, ldpr);
+  hipLaunchKernelGGL((k_gemm_mask<Small, T>), dim3((g.Mp / 128) * (g.Np / 128)), dim3(Small::NT), Small::LDS, s, g,
+                     bias, mask, ldm, probs, ldpr);
   GM2_CHECK_LAUNCH();
 }
 
-template int launch_gemm_store<float>(const GemmArgs<float>&, int, float*, float*, int, int64_t, int64_t,
-                                       const float*, hipStream_t);
-template int launch_gemm_store<bf16_t>(const GemmArgs<bf16_t>&, int, float*, float*, int, int64_t, int64_t,
-                                        const float*, hipStream_t);
-template void launch_gemm_recon_loss<float>(const GemmArgs<float>&, const float*, const float*, int64_t, int,
-                                            const float*, float*, int64_t, float*, int64_t, float*, float*,
-                                            int64_t, hipStream_t);
-template void launch_gemm_recon_loss<bf16_t>(const GemmArgs<bf16_t>&, const float*, const bf16_t*, int64_t, int,
-                                             const float*, bf16_t*, int64_t, bf16_t*, int64_t, float*, float*,
-                                             int64_t, hipStream_t);
+#define GM2_INST(T)                                                                                              \
+  template int launch_gemm_store<T>(const GemmArgs<T>&, int, float*, float*, int, int64_t, int64_t, const float*, \
+                                    hipStream_t);                                                                \
+  template int gemm_recon_grid_blocks<T>(const GemmArgs<T>&);                                                   \
+  template int gemm_recon_row_tiles<T>(const GemmArgs<T>&);                                                     \
+  template int gemm_tile_for<T>(const GemmArgs<T>&);                                                            \
+  template void launch_gemm_recon_loss<T>(const GemmArgs<T>&, const float*, const uint32_t*, int64_t, int,        \
+                                          const float*,                                                         \
+                                          T*, int64_t, T*, int64_t, float*, float*, int64_t, hipStream_t);
+GM2_INST(float)
+GM2_INST(bf16_t)
+#undef GM2_INST
 template void launch_gemm_mask<float>(const GemmArgs<float>&, const float*, uint8_t*, int64_t, float*, int64_t,
                                       hipStream_t);
-template int gemm_recon_grid_blocks<float>(const GemmArgs<float>&);
-template int gemm_recon_grid_blocks<bf16_t>(const GemmArgs<bf16_t>&);
 
 }  // namespace gm2

@@ -79,7 +79,11 @@ int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
 template <typename T>
 int gemm_recon_grid_blocks(const GemmArgs<T>& g);
 template <typename T>
-void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const T* X, int64_t ldx, int with_grad,
+int gemm_recon_row_tiles(const GemmArgs<T>& g);
+template <typename T>
+int gemm_tile_for(const GemmArgs<T>& g);
+template <typename T>
+void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const uint32_t* xbits, int64_t ldxb, int with_grad,
                             const float* scal, T* dL, int64_t ldd, T* dLT, int64_t lddt, float* loss_part,
                             float* colpart, int64_t ldcol, hipStream_t s);
 template <typename T>
@@ -89,11 +93,12 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
 // ---- kernels.hip ----
 constexpr int kBnRowChunk = 128;  // rows per BatchNorm partial-statistics chunk
 
-// gather strain rows of the resident u8 matrix into X [Bp][ldx] and X^T [ldxt rows][Bp] (T);
-// zero-fills columns >= G and rows >= B up to the padded extents
+// gather strain rows of the resident u8 matrix into X [Bp][ldx] and X^T [ldxt rows][Bp] (T), plus
+// the bit-packed target X^T bits [Gp][ldxb words] (bit b%32 of word b/32 = X[b][g]) that the
+// reconstruction-loss epilogue reads; zero-fills columns >= G and rows >= B up to the padded extents
 template <typename T>
 void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* rows, int B, int G, T* X, int64_t ldx,
-                        int Gp, T* XT, int64_t ldxt, int Bp, hipStream_t s);
+                        int Gp, T* XT, int64_t ldxt, int Bp, uint32_t* xbits, int64_t ldxb, hipStream_t s);
 
 // BN forward: y = sum of S slabs + bias -> Y; per-chunk (mean, M2) partials
 void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, const float* bias, int B, int H,
@@ -123,6 +128,9 @@ void launch_reparam_bwd(const float* dzslabs, int S, int64_t slab, int64_t ldsla
 // out[n] = sum_r part[r*ld + n]  (deterministic order)
 void launch_colsum(const float* part, int rows, int64_t ld, int n, float* out0, float* out1, int nsplit,
                    hipStream_t s);
+// C0/C1 (row split at msplit) = sum of S split-K slabs [S][M][N] (slab stride `slab`)
+void launch_slab_sum(const float* slabs, int S, int64_t slab, int M, int N, float* C0, float* C1, int msplit,
+                     int64_t ldc, hipStream_t s);
 // out[i] = sum of partial buffers in double, fixed order (loss record slots)
 void launch_reduce_to(const float* part, int n, int stride, int count, double* out, hipStream_t s);
 
@@ -145,6 +153,14 @@ struct TensorTable {
 
 template <typename T>
 void launch_shadow_sync(const TensorTable& tt, const float* params, hipStream_t s);
+// fused L1 + clip + Adam over the full 30-tensor table (tile0 = first 4096-element block of each
+// tensor), writing natural-layout shadows of the tensors that have one
+template <typename T>
+void launch_adam_fused(const TensorTable& tt, const float* grads, float* params, float* m, float* v, const float* scal,
+                       const float* clip, hipStream_t s);
+// transposed shadows from natural shadows (table entries with shadowT; tile0 counts 64x64 tiles)
+template <typename T>
+void launch_shadow_transpose(const TensorTable& tt, hipStream_t s);
 // sum((g + lambda*sign(p))^2) and sum(|p|) over all params -> partials; then finalize
 void launch_grad_stats(const float* params, const float* grads, int64_t n, const float* scal, double* part,
                        int nblocks, hipStream_t s);

@@ -18,7 +18,8 @@ constexpr double kBnMomentum = 0.1;   // nn.BatchNorm1d default momentum
 template <typename T>
 __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data, int64_t ld_data,
                                               const int32_t* __restrict__ rows, int B, int G, T* __restrict__ X,
-                                              int64_t ldx, T* __restrict__ XT, int64_t ldxt) {
+                                              int64_t ldx, T* __restrict__ XT, int64_t ldxt,
+                                              uint32_t* __restrict__ xbits, int64_t ldxb) {
   __shared__ float tile[128][65];
   const int c0 = blockIdx.x * 128, r0 = blockIdx.y * 64;
   const int t = threadIdx.x;
@@ -46,9 +47,19 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data
   }
   __syncthreads();
   // X^T: 128 rows (columns of X) x 64 (batch rows)
-  for (int i = t; i < 128 * 64; i += 256) {
-    const int c = i >> 6, rl = i & 63;
-    XT[(int64_t)(c0 + c) * ldxt + r0 + rl] = E<T>::cvt(tile[c][rl]);
+  if (XT) {
+    for (int i = t; i < 128 * 64; i += 256) {
+      const int c = i >> 6, rl = i & 63;
+      XT[(int64_t)(c0 + c) * ldxt + r0 + rl] = E<T>::cvt(tile[c][rl]);
+    }
+  }
+  // bit-packed X^T: thread t -> column t/2, 32-row half t%2
+  if (xbits) {
+    const int c = t >> 1, h = t & 1;
+    uint32_t w = 0;
+#pragma unroll
+    for (int b = 0; b < 32; ++b) w |= (tile[c][h * 32 + b] != 0.f ? 1u : 0u) << b;
+    xbits[(int64_t)(c0 + c) * ldxb + (r0 >> 5) + h] = w;
   }
 }
 
@@ -489,6 +500,125 @@ __global__ __launch_bounds__(256) void k_adam(const float* __restrict__ g, float
   }
 }
 
+// fused L1 + clip + Adam over one tensor table entry per block group, writing the fp32 master and
+// the natural-layout GEMM shadow in the same pass (30 B/param of HBM traffic instead of 30 + 6)
+template <typename T>
+__global__ __launch_bounds__(256) void k_adam_fused(TensorTable tt, const float* __restrict__ g, float* __restrict__ p,
+                                                  float* __restrict__ m, float* __restrict__ v,
+                                                  const float* __restrict__ scal, const float* __restrict__ clip) {
+  int ti = 0;
+  while (ti + 1 < tt.n && (int64_t)blockIdx.x >= tt.t[ti + 1].tile0) ++ti;
+  const TensorDesc& d = tt.t[ti];
+  const int64_t numel = d.rows * d.cols;
+  const int64_t e0 = ((int64_t)blockIdx.x - d.tile0) * 4096;  // 4096 elements per block
+  const float lam = scal[kScalLambda], negstep = scal[kScalNegStep], bc2s = scal[kScalBc2Sqrt];
+  const float w1 = scal[kScalOneMinusB1], b2 = scal[kScalBeta2], w2 = scal[kScalOneMinusB2];
+  const float aeps = scal[kScalAdamEps];
+  const float cc = clip[0];
+  T* sh = (T*)d.shadow;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t e = e0 + (int64_t)(k * 256 + threadIdx.x) * 4;  // 4 consecutive elements
+    if (e >= numel) break;
+    const int64_t gi = d.off + e;
+    float4 pv, gv, mv, vv;
+    const bool full = e + 4 <= numel;
+    if (full) {
+      pv = *(const float4*)(p + gi);
+      gv = *(const float4*)(g + gi);
+      mv = *(const float4*)(m + gi);
+      vv = *(const float4*)(v + gi);
+    } else {
+      float* a[4] = {&pv.x, &pv.y, &pv.z, &pv.w};
+      float* b[4] = {&gv.x, &gv.y, &gv.z, &gv.w};
+      float* c[4] = {&mv.x, &mv.y, &mv.z, &mv.w};
+      float* dd[4] = {&vv.x, &vv.y, &vv.z, &vv.w};
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = e + u < numel;
+        *a[u] = ok ? p[gi + u] : 0.f;
+        *b[u] = ok ? g[gi + u] : 0.f;
+        *c[u] = ok ? m[gi + u] : 0.f;
+        *dd[u] = ok ? v[gi + u] : 0.f;
+      }
+    }
+    float pe[4] = {pv.x, pv.y, pv.z, pv.w}, ge[4] = {gv.x, gv.y, gv.z, gv.w};
+    float me[4] = {mv.x, mv.y, mv.z, mv.w}, ve[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float gg = (ge[u] + lam * sgnf(pe[u])) * cc;
+      me[u] = me[u] + w1 * (gg - me[u]);           // exp_avg.lerp_(grad, 1 - beta1)
+      ve[u] = ve[u] * b2;
+      ve[u] = ve[u] + w2 * gg * gg;                // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+      const float denom = sqrtf(ve[u]) / bc2s + aeps;
+      pe[u] = pe[u] + negstep * (me[u] / denom);   // param.addcdiv_(exp_avg, denom, -step_size)
+    }
+    if (full) {
+      *(float4*)(p + gi) = make_float4(pe[0], pe[1], pe[2], pe[3]);
+      *(float4*)(m + gi) = make_float4(me[0], me[1], me[2], me[3]);
+      *(float4*)(v + gi) = make_float4(ve[0], ve[1], ve[2], ve[3]);
+    } else {
+      for (int u = 0; u < 4; ++u)
+        if (e + u < numel) { p[gi + u] = pe[u]; m[gi + u] = me[u]; v[gi + u] = ve[u]; }
+    }
+    if (sh) {
+      int64_t r = e / d.cols, c = e - r * d.cols;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (e + u < numel) sh[(d.srow0 + r) * d.sld + c] = E<T>::cvt(pe[u]);
+        if (++c == d.cols) { c = 0; ++r; }
+      }
+    }
+  }
+}
+
+// transposed GEMM shadows from the natural ones (T -> T, 64x64 tiles through LDS)
+template <typename T>
+__global__ __launch_bounds__(256) void k_shadow_transpose(TensorTable tt) {
+  __shared__ float tile[64][65];
+  int ti = 0;
+  while (ti + 1 < tt.n && (int64_t)blockIdx.x >= tt.t[ti + 1].tile0) ++ti;
+  const TensorDesc& d = tt.t[ti];
+  const int64_t local = blockIdx.x - d.tile0;
+  const int64_t tcols = (d.cols + 63) / 64;
+  const int64_t r0 = (local / tcols) * 64, c0 = (local % tcols) * 64;
+  const T* sh = (const T*)d.shadow;
+  T* shT = (T*)d.shadowT;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int rl = i >> 6, cl = i & 63;
+    const int64_t r = r0 + rl, c = c0 + cl;
+    tile[cl][rl] = (r < d.rows && c < d.cols) ? E<T>::ld(sh + (d.srow0 + r) * d.sld + c) : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int cl = i >> 6, rl = i & 63;
+    const int64_t r = r0 + rl, c = c0 + cl;
+    if (r < d.rows && c < d.cols) shT[c * d.tld + d.srow0 + r] = E<T>::cvt(tile[cl][rl]);
+  }
+}
+
+// C (row-split into C0/C1) = sum of S fp32 split-K slabs [S][M][N] (fixed order: deterministic)
+__global__ __launch_bounds__(256) void k_slab_sum(const float* __restrict__ slabs, int S, int64_t slab, int M, int N,
+                                                float* __restrict__ C0, float* __restrict__ C1, int msplit,
+                                                int64_t ldc) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < total; i += (int64_t)gridDim.x * 1024) {
+    float4 a = *(const float4*)(slabs + i);
+    for (int s = 1; s < S; ++s) {
+      const float4 b = *(const float4*)(slabs + s * slab + i);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    const float e[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t k = i + u;
+      if (k >= total) break;
+      const int m = (int)(k / N), n = (int)(k - (int64_t)m * N);
+      if (m < msplit) C0[(int64_t)m * ldc + n] = e[u];
+      else C1[(int64_t)(m - msplit) * ldc + n] = e[u];
+    }
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
@@ -496,11 +626,11 @@ __global__ __launch_bounds__(256) void k_adam(const float* __restrict__ g, float
 // ------------------------------------------------------------------------------------------------
 template <typename T>
 void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* rows, int B, int G, T* X, int64_t ldx,
-                        int Gp, T* XT, int64_t ldxt, int Bp, hipStream_t s) {
+                        int Gp, T* XT, int64_t ldxt, int Bp, uint32_t* xbits, int64_t ldxb, hipStream_t s) {
   if (Gp % 128 || Bp % 64 || ld_data % 16 || ld_data < Gp || ((uintptr_t)data & 15))
     throw Gm2Error("gather: bad layout (Gp=%d Bp=%d ld=%lld)", Gp, Bp, (long long)ld_data);
   hipLaunchKernelGGL(k_gather<T>, dim3(Gp / 128, Bp / 64), dim3(256), 0, s, data, ld_data, rows, B, G, X, ldx, XT,
-                     ldxt);
+                     ldxt, xbits, ldxb);
   GM2_CHECK_LAUNCH();
 }
 
@@ -581,6 +711,35 @@ void launch_shadow_sync(const TensorTable& tt, const float* params, hipStream_t 
   GM2_CHECK_LAUNCH();
 }
 
+template <typename T>
+void launch_adam_fused(const TensorTable& tt, const float* grads, float* params, float* m, float* v, const float* scal,
+                       const float* clip, hipStream_t s) {
+  const TensorDesc& last = tt.t[tt.n - 1];
+  const int64_t blocks = last.tile0 + (last.rows * last.cols + 4095) / 4096;
+  for (int i = 0; i < tt.n; ++i)
+    if (tt.t[i].off % 4) throw Gm2Error("adam: tensor offset not 16-B aligned");
+  hipLaunchKernelGGL(k_adam_fused<T>, dim3((unsigned)blocks), dim3(256), 0, s, tt, grads, params, m, v, scal, clip);
+  GM2_CHECK_LAUNCH();
+}
+
+template <typename T>
+void launch_shadow_transpose(const TensorTable& tt, hipStream_t s) {
+  if (tt.n <= 0) return;
+  const TensorDesc& last = tt.t[tt.n - 1];
+  const int64_t tiles = last.tile0 + ((last.rows + 63) / 64) * ((last.cols + 63) / 64);
+  hipLaunchKernelGGL(k_shadow_transpose<T>, dim3((unsigned)tiles), dim3(256), 0, s, tt);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_slab_sum(const float* slabs, int S, int64_t slab, int M, int N, float* C0, float* C1, int msplit,
+                     int64_t ldc, hipStream_t s) {
+  if (slab % 4) throw Gm2Error("slab_sum: slab %% 4");
+  const int64_t nb = std::min<int64_t>(4096, ((int64_t)M * N / 4 + 255) / 256);
+  hipLaunchKernelGGL(k_slab_sum, dim3((unsigned)nb), dim3(256), 0, s, slabs, S, slab, M, N, C0, C1 ? C1 : C0,
+                     C1 ? msplit : (1 << 30), ldc);
+  GM2_CHECK_LAUNCH();
+}
+
 int grad_stats_blocks(int64_t n) { return (int)std::min<int64_t>(2048, std::max<int64_t>(1, (n + 255) / 256)); }
 
 void launch_grad_stats(const float* params, const float* grads, int64_t n, const float* scal, double* part,
@@ -604,7 +763,7 @@ void launch_adam(const float* grads, float* params, float* m, float* v, int64_t 
 
 #define GM2_INST(T)                                                                                             \
   template void launch_gather_rows<T>(const uint8_t*, int64_t, const int32_t*, int, int, T*, int64_t, int, T*,  \
-                                      int64_t, int, hipStream_t);                                               \
+                                      int64_t, int, uint32_t*, int64_t, hipStream_t);                           \
   template void launch_bn_fwd_apply<T>(const float*, int64_t, const float*, int, int, int, int, const float*,   \
                                        const float*, float*, float*, float*, T*, T*, int64_t, hipStream_t);     \
   template void launch_bn_bwd_apply<T>(const float*, int, int64_t, const float*, int64_t, const float*,         \
@@ -615,7 +774,10 @@ void launch_adam(const float* grads, float* params, float* m, float* v, int64_t 
   template void launch_reparam_bwd<T>(const float*, int, int64_t, int64_t, const float*, const float*,         \
                                       const float*, int, int, int, T*, int64_t, T*, int64_t, int, float*,       \
                                       hipStream_t);                                                             \
-  template void launch_shadow_sync<T>(const TensorTable&, const float*, hipStream_t);
+  template void launch_shadow_sync<T>(const TensorTable&, const float*, hipStream_t);                          \
+  template void launch_adam_fused<T>(const TensorTable&, const float*, float*, float*, float*, const float*,    \
+                                     const float*, hipStream_t);                                                \
+  template void launch_shadow_transpose<T>(const TensorTable&, hipStream_t);
 GM2_INST(float)
 GM2_INST(bf16_t)
 #undef GM2_INST
