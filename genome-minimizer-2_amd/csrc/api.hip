@@ -77,9 +77,10 @@ struct Layout {
   Dims d;
   int prec;
   int64_t es;
-  // GEMM shadows (T)
-  int64_t sE0, sE1, sE1T, sE2, sE2T, sHD, sHDT, sD0, sD0T, sD1, sD1T, sD2, sD2T, sD3, sD3T;
-  int64_t X, XT, XB, Y[6], A[6], AT[6], save[6], HD, Z, ZT, dL, dLT, slabs, slab_cap, dY, dYT, dH, dHT;
+  // GEMM shadows (T), natural [out][in] layout, zero-padded: each serves as a K-major operand in
+  // the forward GEMM and as an MN-major operand ([K=out][N=in]) in the backward dX GEMM
+  int64_t sE0, sE1, sE2, sHD, sD0, sD1, sD2, sD3;
+  int64_t X, XB, Y[6], A[6], save[6], HD, Z, dL, slabs, slab_cap, dY, dH;
   int64_t bnpart, colpart, colpart_cap, losspart, losspart_cap, klpart, gradpart, clip, total;
 };
 
@@ -97,42 +98,29 @@ Layout make_layout(const gm2_dims* gd, int prec) {
     return at;
   };
   const int64_t es = o.es, H = d.H, Bm = d.Bm;
-  o.sE0 = take(H * d.Gp * es);
-  o.sE1 = take(H * H * es);
-  o.sE1T = take(H * H * es);
+  o.sE0 = take(H * d.Gp * es);       // [H][Gp]
+  o.sE1 = take(H * H * es);          // [H][H]
   o.sE2 = take(H * H * es);
-  o.sE2T = take(H * H * es);
-  o.sHD = take(d.L2r * H * es);
-  o.sHDT = take(H * d.K2L * es);
-  o.sD0 = take(H * d.Lp * es);
-  o.sD0T = take(d.Lr * H * es);
+  o.sHD = take(d.L2r * H * es);      // [L2r][H]: rows 0..L-1 mean_layer, L..2L-1 logvar_layer
+  o.sD0 = take(H * d.Lr * es);       // [H][Lr]
   o.sD1 = take(H * H * es);
-  o.sD1T = take(H * H * es);
   o.sD2 = take(H * H * es);
-  o.sD2T = take(H * H * es);
-  o.sD3 = take(d.Gp * H * es);
-  o.sD3T = take(H * d.Gp * es);
-  o.X = take(Bm * d.Gp * es);
-  o.XT = take(d.Gp * Bm * es);
-  o.XB = take(d.Gp * (Bm / 32) * 4);
+  o.sD3 = take(d.Gp * H * es);       // [Gp][H]
+  o.X = take(Bm * d.Gp * es);        // gathered strain rows [Bm][Gp]
+  o.XB = take(d.Gp * (Bm / 32) * 4); // bit-packed X^T target [Gp][Bm/32]
   for (int i = 0; i < 6; ++i) {
-    o.Y[i] = take(Bm * H * 4);
-    o.A[i] = take(Bm * H * es);
-    o.AT[i] = take(H * Bm * es);
-    o.save[i] = take(2 * H * 4);
+    o.Y[i] = take(Bm * H * 4);       // pre-BN fp32
+    o.A[i] = take(Bm * H * es);      // post-ReLU
+    o.save[i] = take(2 * H * 4);     // batch mean / invstd
   }
-  o.HD = take(Bm * 2 * d.L * 4);
-  o.Z = take(Bm * d.Lp * es);
-  o.ZT = take(d.Lr * Bm * es);
-  o.dL = take(Bm * d.Gp * es);
-  o.dLT = take(d.Gp * Bm * es);
-  const int64_t maxN = std::max<int64_t>({H, 2 * d.L, d.Lp, 128});
+  o.HD = take(Bm * 2 * d.L * 4);     // mu | logvar fp32
+  o.Z = take(Bm * d.Lr * es);        // z [Bm][Lr]
+  o.dL = take(Bm * d.Gp * es);       // dL/dlogit [Bm][Gp]
+  const int64_t maxN = std::max<int64_t>({H, 2 * d.L, d.Lr, 128});
   o.slab_cap = std::max<int64_t>(1024LL * kTile * kTile, Bm * maxN);
   o.slabs = take(o.slab_cap * 4);
   o.dY = take(Bm * H * es);
-  o.dYT = take(H * Bm * es);
-  o.dH = take(Bm * d.K2L * es);
-  o.dHT = take(d.L2r * Bm * es);
+  o.dH = take(Bm * d.L2r * es);      // d(mu | logvar) [Bm][L2r]
   o.bnpart = take((Bm / kBnRowChunk) * H * 8);
   o.colpart_cap = std::max<int64_t>({(Bm / kTile) * d.Gp, (Bm / 64) * H, (Bm / 64) * 2 * d.L});
   o.colpart = take(o.colpart_cap * 4);
@@ -168,8 +156,8 @@ int pick_splits(int tiles, int nk, int tile) {
 // GEMM into the fp32 slab scratch (split-K slices summed by the consumer). Returns #slabs.
 template <typename T>
 int gemm_to_slabs(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64_t ldq, int Np, int M, int N,
-                  int K, int64_t ldc) {
-  GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0};
+                  int K, int64_t ldc, int pk = 1, int qk = 1) {
+  GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0, pk, qk};
   const int tile = gemm_tile_for<T>(g);
   const int S = pick_splits((Mp / tile) * (Np / tile), K / E<T>::KT, tile);
   const int64_t slab = (int64_t)Mp * ldc;
@@ -181,8 +169,8 @@ int gemm_to_slabs(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, 
 // split over K into slabs and summed by k_slab_sum (deterministic order).
 template <typename T>
 void gemm_to(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64_t ldq, int Np, int M, int N, int K,
-             float* C0, float* C1, int msplit, int64_t ldc) {
-  GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0};
+             float* C0, float* C1, int msplit, int64_t ldc, int pk = 1, int qk = 1) {
+  GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0, pk, qk};
   const int tile = gemm_tile_for<T>(g);
   int S = pick_splits((Mp / tile) * (Np / tile), K / E<T>::KT, tile);
   const int64_t slab = round_up((int64_t)M * N, 4);
@@ -199,10 +187,9 @@ void gemm_to(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64
 const int kBlk[6][4] = {{E0W, E0B, E1G, E1BT}, {E3W, E3B, E4G, E4BT}, {E6W, E6B, E7G, E7BT},
                         {D0W, D0B, D1G, D1BT}, {D3W, D3B, D4G, D4BT}, {D6W, D6B, D7G, D7BT}};
 
-// Tensor tables. kind 0: the 9 Linear weights with natural + transposed shadows (tile0 counts
-// 64x64 tiles; used by the fp32 -> shadow sync). kind 1: all 30 parameters in reference order, the
-// weights with their natural shadow (tile0 counts 4096-element blocks; fused Adam). kind 2: the
-// weights that have a transposed shadow (tile0 counts 64x64 tiles; shadow transpose).
+// Tensor tables. kind 0: the 9 Linear weights with their natural-layout shadow (tile0 counts
+// 64x64 tiles; fp32 -> shadow sync). kind 1: all 30 parameters in reference order, weights with
+// their shadow (tile0 counts 4096-element blocks; fused Adam writes the shadow).
 template <typename T>
 TensorTable make_table(const Ctx<T>& c, int kind = 0) {
   const Dims& d = c.d;
@@ -211,9 +198,7 @@ TensorTable make_table(const Ctx<T>& c, int kind = 0) {
   auto tiles_of = [&](const TensorDesc& e) {
     return kind == 1 ? (e.rows * e.cols + 4095) / 4096 : ((e.rows + 63) / 64) * ((e.cols + 63) / 64);
   };
-  auto add = [&](int pi, int64_t rows, int64_t cols, int64_t sh, int64_t sld, int64_t srow0, int64_t shT,
-                 int64_t tld) {
-    if (kind == 2 && shT < 0) return;
+  auto add = [&](int pi, int64_t rows, int64_t cols, int64_t sh, int64_t sld, int64_t srow0) {
     TensorDesc& e = tt.t[tt.n];
     e.off = d.off[pi];
     e.rows = rows;
@@ -221,32 +206,32 @@ TensorTable make_table(const Ctx<T>& c, int kind = 0) {
     e.shadow = sh >= 0 ? (void*)(c.ws + sh) : nullptr;
     e.sld = sld;
     e.srow0 = srow0;
-    e.shadowT = (shT >= 0 && kind != 1) ? (void*)(c.ws + shT) : nullptr;
-    e.tld = tld;
+    e.shadowT = nullptr;
+    e.tld = 0;
     e.tile0 = tt.n == 0 ? 0 : tt.t[tt.n - 1].tile0 + tiles_of(tt.t[tt.n - 1]);
     tt.n++;
   };
   const int64_t H = d.H, G = d.G, L = d.L;
   auto vec = [&](int pi, int64_t n) {
-    if (kind == 1) add(pi, 1, n, -1, 0, 0, -1, 0);
+    if (kind == 1) add(pi, 1, n, -1, 0, 0);
   };
-  add(E0W, H, G, l.sE0, d.Gp, 0, -1, 0);
+  add(E0W, H, G, l.sE0, d.Gp, 0);
   vec(E0B, H); vec(E1G, H); vec(E1BT, H);
-  add(E3W, H, H, l.sE1, H, 0, l.sE1T, H);
+  add(E3W, H, H, l.sE1, H, 0);
   vec(E3B, H); vec(E4G, H); vec(E4BT, H);
-  add(E6W, H, H, l.sE2, H, 0, l.sE2T, H);
+  add(E6W, H, H, l.sE2, H, 0);
   vec(E6B, H); vec(E7G, H); vec(E7BT, H);
-  add(MUW, L, H, l.sHD, H, 0, l.sHDT, d.K2L);
+  add(MUW, L, H, l.sHD, H, 0);
   vec(MUB, L);
-  add(LVW, L, H, l.sHD, H, L, l.sHDT, d.K2L);
+  add(LVW, L, H, l.sHD, H, L);
   vec(LVB, L);
-  add(D0W, H, L, l.sD0, d.Lp, 0, l.sD0T, H);
+  add(D0W, H, L, l.sD0, d.Lr, 0);
   vec(D0B, H); vec(D1G, H); vec(D1BT, H);
-  add(D3W, H, H, l.sD1, H, 0, l.sD1T, H);
+  add(D3W, H, H, l.sD1, H, 0);
   vec(D3B, H); vec(D4G, H); vec(D4BT, H);
-  add(D6W, H, H, l.sD2, H, 0, l.sD2T, H);
+  add(D6W, H, H, l.sD2, H, 0);
   vec(D6B, H); vec(D7G, H); vec(D7BT, H);
-  add(D9W, G, H, l.sD3, H, 0, l.sD3T, d.Gp);
+  add(D9W, G, H, l.sD3, H, 0);
   vec(D9B, G);
   return tt;
 }
@@ -266,29 +251,29 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   if (!b->data) throw Gm2Error("null data");
   const int Bp = (int)round_up(B, kTile);
   const int H = (int)d.H, L = (int)d.L;
-  // 1) strain rows -> X, X^T
-  launch_gather_rows<T>(b->data, b->ld_data, b->rows, B, (int)d.G, c.t(l.X), d.Gp, (int)d.Gp,
-                        train ? c.t(l.XT) : nullptr, d.Bm, Bp, (uint32_t*)(c.ws + l.XB), d.Bm / 32, c.s);
-  // 2) encoder blocks
+  // 1) strain rows -> X [Bp][Gp] (T) + bit-packed target
+  launch_gather_rows<T>(b->data, b->ld_data, b->rows, B, (int)d.G, c.t(l.X), d.Gp, (int)d.Gp, nullptr, 0, Bp,
+                        (uint32_t*)(c.ws + l.XB), d.Bm / 32, c.s);
+  // 2) encoder blocks, heads + reparameterisation, decoder blocks (all NT GEMMs)
   const T* in = c.t(l.X);
   int64_t ldin = d.Gp;
   int Kin = (int)d.Gp;
   const int64_t shadow_in[6] = {l.sE0, l.sE1, l.sE2, l.sD0, l.sD1, l.sD2};
   for (int i = 0; i < 6; ++i) {
-    if (i == 3) {  // heads + reparameterization between encoder and decoder
+    if (i == 3) {
       const int S = gemm_to_slabs<T>(c, c.t(l.A[2]), H, Bp, c.t(l.sHD), H, (int)d.L2r, B, 2 * L, H, 2 * L);
       launch_reparam<T>(c.f(l.slabs), S, (int64_t)Bp * 2 * L, L, prm + d.off[MUB], prm + d.off[LVB], b->eps, B, Bp,
-                        c.f(l.HD), c.t(l.Z), d.Lp, c.t(l.ZT), d.Bm, (int)d.Lr, c.f(l.klpart), c.s);
+                        c.f(l.HD), c.t(l.Z), d.Lr, nullptr, 0, 0, c.f(l.klpart), c.s);
       in = c.t(l.Z);
-      ldin = d.Lp;
+      ldin = d.Lr;
       Kin = (int)d.Lp;
     }
-    const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(shadow_in[i]), Kin, H, B, H, Kin, H);
+    const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(shadow_in[i]), i == 3 ? d.Lr : Kin, H, B, H, Kin, H);
     launch_bn_fwd_partial(c.f(l.slabs), S, (int64_t)Bp * H, H, prm + d.off[kBlk[i][1]], B, H, c.f(l.Y[i]),
                           c.f(l.bnpart), c.s);
     launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train, prm + d.off[kBlk[i][2]],
                            prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
-                           c.f(l.save[i]), c.t(l.A[i]), train ? c.t(l.AT[i]) : nullptr, d.Bm, c.s);
+                           c.f(l.save[i]), c.t(l.A[i]), nullptr, 0, c.s);
     in = c.t(l.A[i]);
     ldin = H;
     Kin = H;
@@ -296,8 +281,7 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   // 3) output layer + reconstruction loss (+ dlogits)
   GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, B, (int)d.G, H, Bp, (int)d.Gp, 0};
   launch_gemm_recon_loss<T>(g, prm + d.off[D9B], (const uint32_t*)(c.ws + l.XB), d.Bm / 32, with_grad, scal, c.t(l.dL),
-                            d.Gp, c.t(l.dLT), d.Bm,
-                            c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
+                            d.Gp, nullptr, 0, c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
   const int nblk = gemm_recon_grid_blocks<T>(g);
   launch_reduce_to(c.f(l.losspart), nblk, 2, 2, loss + 0, c.s);
   launch_reduce_to(c.f(l.klpart), Bp / 64, 1, 1, loss + 2, c.s);
@@ -305,44 +289,45 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
     launch_colsum(c.f(l.colpart), gemm_recon_row_tiles<T>(g), d.Gp, (int)d.G, grads + d.off[D9B], nullptr, 0, c.s);
 }
 
+// Backward. Every operand is read in the layout its producer wrote: weight gradients use MN-major P
+// and Q (dW[out][in] = sum_b dY[b][out] * in[b][in]), input gradients an MN-major weight
+// (dX[b][in] = sum_out dY[b][out] * W[out][in]); no transposed copy exists anywhere.
 template <typename T>
 void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, const float* scal) {
   const Dims& d = c.d;
   const Layout& l = c.lo;
   const int B = (int)b->n, Bp = (int)round_up(B, kTile);
   const int H = (int)d.H, L = (int)d.L, G = (int)d.G;
-  const int64_t Bm = d.Bm;
-  // output layer: dW9 = dL^T . A5 ; dA5 = dL . W9
-  gemm_to<T>(c, c.t(l.dLT), Bm, (int)d.Gp, c.t(l.AT[5]), Bm, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H);
-  int S = gemm_to_slabs<T>(c, c.t(l.dL), d.Gp, Bp, c.t(l.sD3T), d.Gp, H, B, H, (int)d.Gp, H);
-  const int64_t shadowT[6] = {-1, l.sE1T, l.sE2T, l.sD0T, l.sD1T, l.sD2T};
+  const int Gp = (int)d.Gp, Lr = (int)d.Lr, L2r = (int)d.L2r;
+  // output layer: dW9[g][h] = sum_b dL[b][g] A5[b][h] ; dA5[b][h] = sum_g dL[b][g] W9[g][h]
+  gemm_to<T>(c, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
+  int S = gemm_to_slabs<T>(c, c.t(l.dL), Gp, Bp, c.t(l.sD3), H, H, B, H, Gp, H, 1, 0);
+  const int64_t shadow_w[6] = {l.sE0, l.sE1, l.sE2, l.sD0, l.sD1, l.sD2};
   for (int i = 5; i >= 0; --i) {
-    const int64_t slab = (int64_t)Bp * (i == 2 ? H : H);
+    const int64_t slab = (int64_t)Bp * H;
     launch_bn_bwd_partial(c.f(l.slabs), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
                           prm + d.off[kBlk[i][3]], B, H, c.f(l.bnpart), c.s);
     launch_bn_bwd_apply<T>(c.f(l.slabs), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
                            prm + d.off[kBlk[i][3]], c.f(l.bnpart), B, Bp, H, gr + d.off[kBlk[i][2]],
-                           gr + d.off[kBlk[i][3]], c.t(l.dY), c.t(l.dYT), Bm, c.f(l.colpart), c.s);
+                           gr + d.off[kBlk[i][3]], c.t(l.dY), nullptr, 0, c.f(l.colpart), c.s);
     launch_colsum(c.f(l.colpart), Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, c.s);
-    // weight gradient of this block's Linear: dW = dY^T . in^T
-    if (i == 0) {
-      gemm_to<T>(c, c.t(l.dYT), Bm, H, c.t(l.XT), Bm, (int)d.Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G);
+    if (i == 0) {  // input layer: weight gradient only
+      gemm_to<T>(c, c.t(l.dY), H, H, c.t(l.X), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 0, 0);
       break;
     }
-    if (i == 3) {
-      gemm_to<T>(c, c.t(l.dYT), Bm, H, c.t(l.ZT), Bm, (int)d.Lr, H, L, Bp, gr + d.off[D0W], nullptr, 0, L);
-      // dz = dY3 . W_d0  -> reparam backward -> dH (mu | logvar)
-      S = gemm_to_slabs<T>(c, c.t(l.dY), H, Bp, c.t(l.sD0T), H, (int)d.Lr, B, L, H, L);
-      launch_reparam_bwd<T>(c.f(l.slabs), S, (int64_t)Bp * L, L, c.f(l.HD), b->eps, scal, B, Bp, L, c.t(l.dH), d.K2L,
-                            c.t(l.dHT), Bm, (int)d.L2r, c.f(l.colpart), c.s);
+    if (i == 3) {  // decoder input layer, then back through the reparameterisation and the heads
+      gemm_to<T>(c, c.t(l.dY), H, H, c.t(l.Z), Lr, Lr, H, L, Bp, gr + d.off[D0W], nullptr, 0, L, 0, 0);
+      S = gemm_to_slabs<T>(c, c.t(l.dY), H, Bp, c.t(l.sD0), Lr, Lr, B, L, H, L, 1, 0);
+      launch_reparam_bwd<T>(c.f(l.slabs), S, (int64_t)Bp * L, L, c.f(l.HD), b->eps, scal, B, Bp, L, c.t(l.dH), L2r,
+                            nullptr, 0, 0, c.f(l.colpart), c.s);
       launch_colsum(c.f(l.colpart), Bp / 64, 2 * L, 2 * L, gr + d.off[MUB], gr + d.off[LVB], L, c.s);
-      gemm_to<T>(c, c.t(l.dHT), Bm, (int)d.L2r, c.t(l.AT[2]), Bm, H, 2 * L, H, Bp, gr + d.off[MUW],
-                 gr + d.off[LVW], L, H);
-      S = gemm_to_slabs<T>(c, c.t(l.dH), d.K2L, Bp, c.t(l.sHDT), d.K2L, H, B, H, (int)d.K2L, H);
+      gemm_to<T>(c, c.t(l.dH), L2r, L2r, c.t(l.A[2]), H, H, 2 * L, H, Bp, gr + d.off[MUW], gr + d.off[LVW], L, H, 0,
+                 0);
+      S = gemm_to_slabs<T>(c, c.t(l.dH), L2r, Bp, c.t(l.sHD), H, H, B, H, (int)d.K2L, H, 1, 0);
       continue;
     }
-    gemm_to<T>(c, c.t(l.dYT), Bm, H, c.t(l.AT[i - 1]), Bm, H, H, H, Bp, gr + d.off[kBlk[i][0]], nullptr, 0, H);
-    S = gemm_to_slabs<T>(c, c.t(l.dY), H, Bp, c.t(shadowT[i]), H, H, B, H, H, H);
+    gemm_to<T>(c, c.t(l.dY), H, H, c.t(l.A[i - 1]), H, H, H, H, Bp, gr + d.off[kBlk[i][0]], nullptr, 0, H, 0, 0);
+    S = gemm_to_slabs<T>(c, c.t(l.dY), H, Bp, c.t(shadow_w[i]), H, H, B, H, H, H, 1, 0);
   }
 }
 
@@ -353,20 +338,22 @@ void decode_chain(const Ctx<T>& c, const float* prm, float* bn, int n, uint8_t* 
   const Layout& l = c.lo;
   const int Bp = (int)round_up(n, kTile), H = (int)d.H;
   const T* in = c.t(l.Z);
-  int64_t ldin = d.Lp;
+  int64_t ldin = d.Lr;
   int Kin = (int)d.Lp;
+  int64_t ldw = d.Lr;
   const int64_t shadow_in[3] = {l.sD0, l.sD1, l.sD2};
   for (int j = 0; j < 3; ++j) {
     const int i = 3 + j;
-    const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(shadow_in[j]), Kin, H, n, H, Kin, H);
+    const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(shadow_in[j]), ldw, H, n, H, Kin, H);
     launch_bn_fwd_partial(c.f(l.slabs), S, (int64_t)Bp * H, H, prm + d.off[kBlk[i][1]], n, H, c.f(l.Y[i]),
                           c.f(l.bnpart), c.s);
     launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), n, Bp, H, 0, prm + d.off[kBlk[i][2]],
                            prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, nullptr,
-                           c.t(l.A[i]), nullptr, d.Bm, c.s);
+                           c.t(l.A[i]), nullptr, 0, c.s);
     in = c.t(l.A[i]);
     ldin = H;
     Kin = H;
+    ldw = H;
   }
   GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, n, (int)d.G, H, Bp, (int)d.Gp, 0};
   launch_gemm_mask<T>(g, prm + d.off[D9B], mask, ldm, probs, ldpr, c.s);
@@ -459,11 +446,9 @@ int gm2_adam_step(const gm2_dims* d, int prec, float* params, const float* grads
     if (prec == GM2_F32) {
       Ctx<float> c(lo, ws, stream);
       launch_adam_fused<float>(make_table(c, 1), grads, params, m, v, scalars, clip, c.s);
-      launch_shadow_transpose<float>(make_table(c, 2), c.s);
     } else {
       Ctx<bf16_t> c(lo, ws, stream);
       launch_adam_fused<bf16_t>(make_table(c, 1), grads, params, m, v, scalars, clip, c.s);
-      launch_shadow_transpose<bf16_t>(make_table(c, 2), c.s);
     }
   });
 }
@@ -491,7 +476,7 @@ int gm2_decode_mask(const gm2_dims* d, const float* params, const float* bn_runn
     if (ld_mask < lo.d.G || (probs && ld_probs < lo.d.G)) throw Gm2Error("decode: ld < G");
     Ctx<float> c(lo, ws, stream);
     // z [n][L] -> Z [Bm][Lp] (pad columns stay zero from workspace init)
-    HIP_OK(hipMemcpy2DAsync(c.f(lo.Z), lo.d.Lp * 4, z, lo.d.L * 4, lo.d.L * 4, n, hipMemcpyDeviceToDevice, c.s));
+    HIP_OK(hipMemcpy2DAsync(c.f(lo.Z), lo.d.Lr * 4, z, lo.d.L * 4, lo.d.L * 4, n, hipMemcpyDeviceToDevice, c.s));
     decode_chain<float>(c, params, const_cast<float*>(bn_running), (int)n, mask, ld_mask, probs, ld_probs);
   });
 }
@@ -508,8 +493,8 @@ int gm2_encode(const gm2_dims* d, int prec, const gm2_batch* batch, const float*
       const int B = (int)b.n, Bp = (int)round_up(B, kTile), H = (int)dd.H, L = (int)dd.L;
       if (B <= 0 || B > dd.Bm) throw Gm2Error("encode rows outside (0, batch_max]");
       float* bn = const_cast<float*>(bn_running);
-      launch_gather_rows<T>(b.data, b.ld_data, b.rows, B, (int)dd.G, c.t(lo.X), dd.Gp, (int)dd.Gp, nullptr, dd.Bm,
-                            Bp, nullptr, 0, c.s);
+      launch_gather_rows<T>(b.data, b.ld_data, b.rows, B, (int)dd.G, c.t(lo.X), dd.Gp, (int)dd.Gp, nullptr, 0, Bp,
+                            nullptr, 0, c.s);
       const T* in = c.t(lo.X);
       int64_t ldin = dd.Gp;
       int Kin = (int)dd.Gp;
@@ -520,14 +505,14 @@ int gm2_encode(const gm2_dims* d, int prec, const gm2_batch* batch, const float*
                               c.f(lo.bnpart), c.s);
         launch_bn_fwd_apply<T>(c.f(lo.Y[i]), H, c.f(lo.bnpart), B, Bp, H, 0, params + dd.off[kBlk[i][2]],
                                params + dd.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
-                               nullptr, c.t(lo.A[i]), nullptr, dd.Bm, c.s);
+                               nullptr, c.t(lo.A[i]), nullptr, 0, c.s);
         in = c.t(lo.A[i]);
         ldin = H;
         Kin = H;
       }
       const int S = gemm_to_slabs<T>(c, c.t(lo.A[2]), H, Bp, c.t(lo.sHD), H, (int)dd.L2r, B, 2 * L, H, 2 * L);
       launch_reparam<T>(c.f(lo.slabs), S, (int64_t)Bp * 2 * L, L, params + dd.off[MUB], params + dd.off[LVB], nullptr,
-                        B, Bp, c.f(lo.HD), c.t(lo.Z), dd.Lp, c.t(lo.ZT), dd.Bm, (int)dd.Lr, c.f(lo.klpart), c.s);
+                        B, Bp, c.f(lo.HD), c.t(lo.Z), dd.Lr, nullptr, 0, 0, c.f(lo.klpart), c.s);
       if (mu) HIP_OK(hipMemcpy2DAsync(mu, L * 4, c.f(lo.HD), 2 * L * 4, L * 4, B, hipMemcpyDeviceToDevice, c.s));
       if (logvar)
         HIP_OK(hipMemcpy2DAsync(logvar, L * 4, c.f(lo.HD) + L, 2 * L * 4, L * 4, B, hipMemcpyDeviceToDevice, c.s));
@@ -537,13 +522,13 @@ int gm2_encode(const gm2_dims* d, int prec, const gm2_batch* batch, const float*
   });
 }
 
-int gm2_gemm_nt(int prec, const void* P, int64_t ldp, const void* Q, int64_t ldq, float* C, int64_t ldc, int64_t M,
-                int64_t N, int64_t K, int splits, float* slab_ws, void* stream) {
+int gm2_gemm(int prec, int pk, int qk, const void* P, int64_t ldp, const void* Q, int64_t ldq, float* C, int64_t ldc,
+             int64_t M, int64_t N, int64_t K, int splits, float* slab_ws, void* stream) {
   return guarded([&] {
     auto run = [&](auto tag) {
       using T = decltype(tag);
       GemmArgs<T> g{(const T*)P, ldp, (const T*)Q, ldq, (int)M, (int)N, (int)K, (int)round_up(M, kTile),
-                    (int)round_up(N, kTile), 0};
+                    (int)round_up(N, kTile), 0, pk ? 1 : 0, qk ? 1 : 0};
       if (splits <= 1) {
         launch_gemm_store<T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, (hipStream_t)stream);
       } else {

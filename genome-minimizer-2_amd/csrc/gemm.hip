@@ -67,11 +67,12 @@ __device__ __forceinline__ TileXY tile_of(int tm, int tn) {
   return {pm * C::BM, pn * C::BN, split, pm * tn + pn};
 }
 
+// ---- operand staging (HBM -> LDS with global_load_lds_dwordx4; LDS destination lane-linear) ----
+// K-major operand (stored [rows][ld], K contiguous): the tile is ROWS rows x 128 B (one K-step);
+// 16-B chunk c of row r lives at chunk position c ^ ((r>>1)&7)  -> conflict-free ds_read_b128.
 template <class C, typename T, int ROWS>
-__device__ __forceinline__ void stage_rows(const T* __restrict__ P, int64_t ldp, int row0, int k0, char* lds,
-                                           int wid, int lane) {
-  // ROWS rows x 128 B = ROWS*8 16-byte chunks; wave instruction j covers chunks
-  // [j*NT + wid*64, +64): the LDS destination is lane-linear (glds semantics).
+__device__ __forceinline__ void stage_kmajor(const T* __restrict__ P, int64_t ldp, int row0, int k0, char* lds,
+                                             int wid, int lane) {
   constexpr int EPC = 16 / sizeof(T);
   constexpr int PER = ROWS * 8 / C::NT;
 #pragma unroll
@@ -84,10 +85,73 @@ __device__ __forceinline__ void stage_rows(const T* __restrict__ P, int64_t ldp,
   }
 }
 
+// MN-major operand (stored [K][ld], its M or N dimension contiguous): the tile is KT k-rows x
+// R elements; 16-B chunk c of k-row k lives at chunk position c ^ swz(k). swz keeps chunk pairs
+// together and spreads the 8 k-rows one 32-lane half of a ds_read_b64_tr_b16 touches over 8
+// distinct 32-B bank groups (conflict-free transposed reads).
+__device__ __forceinline__ int swz_mn(int k) { return 2 * ((k & 3) | ((k >> 1) & 4)); }
+
+template <class C, typename T, int R>
+__device__ __forceinline__ void stage_mnmajor(const T* __restrict__ P, int64_t ldp, int col0, int k0, char* lds,
+                                              int wid, int lane) {
+  constexpr int EPC = 16 / sizeof(T);
+  constexpr int CPR = R / EPC;                // chunks per k-row
+  constexpr int PER = E<T>::KT * CPR / C::NT;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = j * C::NT + wid * 64 + lane;
+    const int k = i / CPR;
+    const int c = (i % CPR) ^ swz_mn(k);
+    const T* src = P + (int64_t)(k0 + k) * ldp + col0 + c * EPC;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (j * C::NT + wid * 64) * 16), 16, 0, 0);
+  }
+}
+
 __device__ __forceinline__ int frag_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+// bf16 fragment of operand rows [r0, r0+16) for k-substep s (32 k): lane l holds row r0 + (l&15),
+// k = 32s + 8(l>>4) + j, j = 0..7 (the 16x16x32 MFMA A/B lane map).
+template <bool KMAJ, int R>
+__device__ __forceinline__ bf16x8 frag_bf16(const char* tile, int r0, int s, int lane) {
+  if constexpr (KMAJ) {
+    return *(const bf16x8*)(tile + frag_off(r0 + (lane & 15), s * 4 + (lane >> 4)));
+  } else {
+    constexpr int RB = R * 2;  // bytes per k-row
+    const int i = lane & 15, q = i >> 2, p = i & 3;
+    const int k = s * 32 + 8 * (lane >> 4) + q;
+    const int c = (r0 >> 3) + (p >> 1);
+    const char* a1 = tile + k * RB + ((c ^ swz_mn(k)) << 4) + (p & 1) * 8;
+    const char* a2 = tile + (k + 4) * RB + ((c ^ swz_mn(k + 4)) << 4) + (p & 1) * 8;
+    const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
+    const bf16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a2);
+    return bf16x8{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+  }
+}
+
+// f32 fragment for k-substep s (16 k): lane l holds row r0 + (l&15), k = 16s + 4(l>>4) + j, j = 0..3
+template <bool KMAJ, int R>
+__device__ __forceinline__ f32x4 frag_f32(const char* tile, int r0, int s, int lane) {
+  if constexpr (KMAJ) {
+    return *(const f32x4*)(tile + frag_off(r0 + (lane & 15), s * 4 + (lane >> 4)));
+  } else {
+    constexpr int RB = R * 4;
+    const int r = r0 + (lane & 15);
+    f32x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = s * 16 + 4 * (lane >> 4) + j;
+      v[j] = *(const float*)(tile + k * RB + (((r >> 2) ^ swz_mn(k)) << 4) + (r & 3) * 4);
+    }
+    return v;
+  }
+}
+
 // Main loop. acc[mi][ni][j] = C[m0 + wm*WTM + mi*16 + 4*(lane>>4) + j][n0 + wn*WTN + ni*16 + (lane&15)]
-template <class C, typename T>
+// AK / BK: P / Q stored K-major (true) or MN-major (false).
+template <class C, typename T, bool AK, bool BK>
 __device__ __forceinline__ void mainloop(const T* __restrict__ P, int64_t ldp, const T* __restrict__ Q, int64_t ldq,
                                          int m0, int n0, int kbeg, int nk, char* smem,
                                          f32x4 (&acc)[C::FM][C::FN]) {
@@ -100,44 +164,44 @@ __device__ __forceinline__ void mainloop(const T* __restrict__ P, int64_t ldp, c
     for (int b = 0; b < C::FN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (nk <= 0) return;
 
-  stage_rows<C, T, C::BM>(P, ldp, m0, kbeg, smem, wid, lane);
-  stage_rows<C, T, C::BN>(Q, ldq, n0, kbeg, smem + C::BM * 128, wid, lane);
+  auto stage = [&](char* buf, int k0) {
+    if constexpr (AK) stage_kmajor<C, T, C::BM>(P, ldp, m0, k0, buf, wid, lane);
+    else stage_mnmajor<C, T, C::BM>(P, ldp, m0, k0, buf, wid, lane);
+    if constexpr (BK) stage_kmajor<C, T, C::BN>(Q, ldq, n0, k0, buf + C::BM * 128, wid, lane);
+    else stage_mnmajor<C, T, C::BN>(Q, ldq, n0, k0, buf + C::BM * 128, wid, lane);
+  };
+  stage(smem, kbeg);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
     char* cur = smem + (kt & 1) * C::STAGE;
-    if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * C::STAGE;
-      const int kn = kbeg + (kt + 1) * KT;
-      stage_rows<C, T, C::BM>(P, ldp, m0, kn, nxt, wid, lane);
-      stage_rows<C, T, C::BN>(Q, ldq, n0, kn, nxt + C::BM * 128, wid, lane);
-    }
+    if (kt + 1 < nk) stage(smem + ((kt + 1) & 1) * C::STAGE, kbeg + (kt + 1) * KT);
     const char* sA = cur;
     const char* sB = cur + C::BM * 128;
+    if constexpr (sizeof(T) == 2) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int c = s * 4 + (lane >> 4);
-      if constexpr (sizeof(T) == 2) {
+      for (int s = 0; s < 2; ++s) {
         bf16x8 b[C::FN];
 #pragma unroll
-        for (int ni = 0; ni < C::FN; ++ni)
-          b[ni] = *(const bf16x8*)(sB + frag_off(wn * C::WTN + ni * 16 + (lane & 15), c));
+        for (int ni = 0; ni < C::FN; ++ni) b[ni] = frag_bf16<BK, C::BN>(sB, wn * C::WTN + ni * 16, s, lane);
 #pragma unroll
         for (int mi = 0; mi < C::FM; ++mi) {
-          const bf16x8 a = *(const bf16x8*)(sA + frag_off(wm * C::WTM + mi * 16 + (lane & 15), c));
+          const bf16x8 a = frag_bf16<AK, C::BM>(sA, wm * C::WTM + mi * 16, s, lane);
 #pragma unroll
           for (int ni = 0; ni < C::FN; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[ni], acc[mi][ni], 0, 0, 0);
         }
-      } else {
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
         f32x4 b[C::FN];
 #pragma unroll
-        for (int ni = 0; ni < C::FN; ++ni)
-          b[ni] = *(const f32x4*)(sB + frag_off(wn * C::WTN + ni * 16 + (lane & 15), c));
+        for (int ni = 0; ni < C::FN; ++ni) b[ni] = frag_f32<BK, C::BN>(sB, wn * C::WTN + ni * 16, s, lane);
 #pragma unroll
         for (int mi = 0; mi < C::FM; ++mi) {
-          const f32x4 a = *(const f32x4*)(sA + frag_off(wm * C::WTM + mi * 16 + (lane & 15), c));
+          const f32x4 a = frag_f32<AK, C::BM>(sA, wm * C::WTM + mi * 16, s, lane);
 #pragma unroll
           for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -155,7 +219,7 @@ __device__ __forceinline__ void mainloop(const T* __restrict__ P, int64_t ldp, c
 // Epilogue 1: fp32 store. Rows m < msplit go to C0, rows >= msplit to C1 (row m - msplit); the
 // split-K slice z writes slab z (C0 + z*slab). Optional per-column bias.
 // ---------------------------------------------------------------------------------------------
-template <class C, typename T>
+template <class C, typename T, bool AK, bool BK>
 __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __restrict__ C0, float* __restrict__ C1,
                                                     int msplit, int64_t ldc, int64_t slab,
                                                     const float* __restrict__ bias) {
@@ -165,7 +229,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
   const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = (kend - kbeg) / E<T>::KT;
   f32x4 acc[C::FM][C::FN];
-  mainloop<C, T>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
+  mainloop<C, T, AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   float* Cz = C0 + (int64_t)tl.split * slab;
 #pragma unroll
@@ -229,7 +293,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const 
   const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
   const TileXY tl = tile_of<C>(tm, tn);
   f32x4 acc[C::FM][C::FN];
-  mainloop<C, T>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+  mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   const int q = lane >> 4;
   const float wgam = scal[kScalWGamma];
@@ -269,10 +333,10 @@ __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const 
       }
     }
   }
-  if (with_grad) {
-    // phase 2: dL^T [n][m] through an LDS image [BN][BM+8] (each lane owns 4 consecutive m of one
-    // n: one 8/16-byte LDS write), then full-row coalesced stores
-    constexpr int EPC = 16 / sizeof(T);
+  constexpr int EPC = 16 / sizeof(T);
+  if (with_grad && dLT) {
+    // phase 2 (optional): dL^T [n][m] through an LDS image [BN][BM+8] (each lane owns 4
+    // consecutive m of one n: one 8/16-byte LDS write), then full-row coalesced stores
     {
       constexpr int PT = C::BM + 8;
       T* img = (T*)smem;
@@ -299,6 +363,8 @@ __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const 
       }
       __syncthreads();
     }
+  }
+  if (with_grad) {
     // phase 3: dL [m][n] through an LDS image [BM][BN+8], full-row coalesced stores
     {
       constexpr int PR = C::BN + 8;
@@ -363,7 +429,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
   f32x4 acc[C::FM][C::FN];
-  mainloop<C, T>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+  mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
 #pragma unroll
   for (int ni = 0; ni < C::FN; ++ni) {
@@ -446,7 +512,7 @@ template <typename T>
 static void check_gemm(const GemmArgs<T>& g, int tile) {
   if (g.K % kKPad || g.Mp % tile || g.Np % tile || g.M > g.Mp || g.N > g.Np || g.M <= 0 || g.N <= 0)
     throw Gm2Error("gemm: bad dims M=%d N=%d K=%d Mp=%d Np=%d (tile %d)", g.M, g.N, g.K, g.Mp, g.Np, tile);
-  if (g.ldp < g.K || g.ldq < g.K) throw Gm2Error("gemm: ld < K");
+  if ((g.pk ? g.ldp < g.K : g.ldp < g.Mp) || (g.qk ? g.ldq < g.K : g.ldq < g.Np)) throw Gm2Error("gemm: ld too small");
   if (((uintptr_t)g.P | (uintptr_t)g.Q) & 15) throw Gm2Error("gemm: operands not 16-B aligned");
   if ((g.ldp * sizeof(T)) % 16 || (g.ldq * sizeof(T)) % 16) throw Gm2Error("gemm: ld not 16-B multiple");
 }
@@ -455,6 +521,20 @@ static void check_gemm(const GemmArgs<T>& g, int tile) {
 template <typename T>
 static bool use_big(const GemmArgs<T>& g) {
   return g.Mp % 256 == 0 && g.Np % 256 == 0 && (int64_t)g.Mp * g.Np >= (int64_t)2048 * 1024 && g.K >= 512;
+}
+
+template <class C, typename T, bool AK, bool BK>
+static void store_launch(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
+                         const float* bias, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)k_gemm_store<C, T, AK, BK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            C::LDS) != hipSuccess)
+      throw Gm2Error("hipFuncSetAttribute(store)");
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_gemm_store<C, T, AK, BK>), dim3(tiles), dim3(C::NT), C::LDS, s, a, C0, C1 ? C1 : C0,
+                     C1 ? msplit : (1 << 30), ldc, slab, bias);
 }
 
 template <class C, typename T>
@@ -467,16 +547,11 @@ static int store_impl(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
   a.k_per_split = (int)(round_up(nkt, splits) / splits) * kt;
   splits = (int)((g.K + a.k_per_split - 1) / a.k_per_split);
   const int tiles = (g.Mp / C::BM) * (g.Np / C::BN) * splits;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)k_gemm_store<C, T>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS) !=
-        hipSuccess)
-      throw Gm2Error("hipFuncSetAttribute(store)");
-    attr = true;
-  }
   TimedLaunch tl(kKcGemmStore, s);
-  hipLaunchKernelGGL((k_gemm_store<C, T>), dim3(tiles), dim3(C::NT), C::LDS, s, a, C0, C1 ? C1 : C0,
-                     C1 ? msplit : (1 << 30), ldc, slab, bias);
+  if (g.pk && g.qk) store_launch<C, T, true, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, s);
+  else if (g.pk && !g.qk) store_launch<C, T, true, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, s);
+  else if (!g.pk && !g.qk) store_launch<C, T, false, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, s);
+  else throw Gm2Error("gemm: layout (P MN-major, Q K-major) not instantiated");
   GM2_CHECK_LAUNCH();
   return splits;
 }

@@ -50,6 +50,9 @@ enum Scal {
   kNumScal = 16
 };
 
+// C[M][N] = sum_k P(m, k) * Q(n, k). pk / qk: the operand is stored K-major ([rows][ld], K
+// contiguous: P(m,k) = P[m*ld + k]) or MN-major ([K][ld]: P(m,k) = P[k*ld + m]). MN-major
+// operands are read with ds_read_b64_tr_b16 (bf16) and need no transposed copy.
 template <typename T>
 struct GemmArgs {
   const T* P;
@@ -57,8 +60,9 @@ struct GemmArgs {
   const T* Q;
   int64_t ldq;
   int M, N, K;   // logical sizes (K already padded to 64, pads zero)
-  int Mp, Np;    // allocated row counts of P / Q (multiples of 128)
+  int Mp, Np;    // padded M / N extents covered by the operand buffers (multiples of 128)
   int k_per_split;
+  int pk = 1, qk = 1;
 };
 
 // ---- live per-kernel timing (bench.py): hipEvent pairs around every launch of one class ----

@@ -276,9 +276,11 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
     tile[c][rl] = dx;
   }
   __syncthreads();
-  for (int i = t; i < 64 * 64; i += 256) {
-    const int cc = i >> 6, rl = i & 63;
-    dYT[(int64_t)(c0 + cc) * ldyt + r0 + rl] = E<T>::cvt(tile[cc][rl]);
+  if (dYT) {
+    for (int i = t; i < 64 * 64; i += 256) {
+      const int cc = i >> 6, rl = i & 63;
+      dYT[(int64_t)(c0 + cc) * ldyt + r0 + rl] = E<T>::cvt(tile[cc][rl]);
+    }
   }
   __syncthreads();
   float* red = &tile[0][0];
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(256) void k_reparam(const float* __restrict__ slabs
       kl += ((1.0f + lv) - mu * mu) - expf(lv);
     }
     Z[(int64_t)r * ldz + l] = E<T>::cvt(z);
-    ZT[(int64_t)l * ldzt + r] = E<T>::cvt(z);
+    if (ZT) ZT[(int64_t)l * ldzt + r] = E<T>::cvt(z);
   }
   kl = wave_sum(kl);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = kl;
@@ -355,8 +357,10 @@ __global__ __launch_bounds__(256) void k_reparam_bwd(const float* __restrict__ d
     }
     dH[(int64_t)r * ldh + l] = E<T>::cvt(gmu);
     dH[(int64_t)r * ldh + L + l] = E<T>::cvt(glv);
-    dHT[(int64_t)l * ldht + r] = E<T>::cvt(gmu);
-    dHT[(int64_t)(L + l) * ldht + r] = E<T>::cvt(glv);
+    if (dHT) {
+      dHT[(int64_t)l * ldht + r] = E<T>::cvt(gmu);
+      dHT[(int64_t)(L + l) * ldht + r] = E<T>::cvt(glv);
+    }
     smu += gmu;
     slv += glv;
   }

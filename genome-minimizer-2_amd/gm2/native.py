@@ -26,7 +26,7 @@ S_ONE_MINUS_B1, S_BETA2, S_ONE_MINUS_B2, S_ADAM_EPS = 6, 7, 8, 9
 EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_offsets",
            "gm2_workspace_size", "gm2_workspace_init", "gm2_sync_shadows", "gm2_train_fwd_bwd",
            "gm2_grad_norm", "gm2_adam_step", "gm2_eval_forward", "gm2_decode_mask", "gm2_encode",
-           "gm2_gemm_nt", "gm2_timing_begin", "gm2_timing_end"]
+           "gm2_gemm", "gm2_timing_begin", "gm2_timing_end"]
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
 
 
@@ -66,7 +66,7 @@ def lib():
         "gm2_eval_forward": (C.c_int, [dp, i32, C.POINTER(Batch), vp, vp, vp, vp, vp, vp]),
         "gm2_decode_mask": (C.c_int, [dp, vp, vp, vp, i64, vp, i64, vp, i64, vp, vp]),
         "gm2_encode": (C.c_int, [dp, i32, C.POINTER(Batch), vp, vp, vp, vp, vp, vp]),
-        "gm2_gemm_nt": (C.c_int, [i32, vp, i64, vp, i64, vp, i64, i64, i64, i64, i32, vp, vp]),
+        "gm2_gemm": (C.c_int, [i32, i32, i32, vp, i64, vp, i64, vp, i64, i64, i64, i64, i32, vp, vp]),
         "gm2_timing_begin": (C.c_int, [i32]),
         "gm2_timing_end": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     }
@@ -164,9 +164,9 @@ def encode(ws: Workspace, batch: Batch, params, bn, mu, logvar):
                            ws.ptr, stream()), "gm2_encode")
 
 
-def gemm_nt(prec, P, ldp, Q, ldq, Cout, ldc, M, N, K, splits=1, slab=None):
-    check(lib().gm2_gemm_nt(prec, ptr(P), ldp, ptr(Q), ldq, ptr(Cout), ldc, M, N, K, splits, ptr(slab), stream()),
-          "gm2_gemm_nt")
+def gemm(prec, P, ldp, Q, ldq, Cout, ldc, M, N, K, splits=1, slab=None, p_kmajor=True, q_kmajor=True):
+    check(lib().gm2_gemm(prec, int(p_kmajor), int(q_kmajor), ptr(P), ldp, ptr(Q), ldq, ptr(Cout), ldc, M, N, K,
+                         splits, ptr(slab), stream()), "gm2_gemm")
 
 
 def timing_begin(classes: int):

@@ -131,10 +131,14 @@ int gm2_decode_mask(const gm2_dims* d, const float* params, const float* bn_runn
 int gm2_encode(const gm2_dims* d, int precision, const gm2_batch* batch, const float* params,
                const float* bn_running, float* mu, float* logvar, void* ws, void* stream);
 
-/* Raw NT GEMM primitive, exposed for kernel-level tests: C[M][ldc] (fp32) = P[M][K] * Q[N][K]^T,
- * P/Q of `precision` element type with >= roundup(M|N,128) allocated rows, K % 64 == 0. */
-int gm2_gemm_nt(int precision, const void* P, int64_t ldp, const void* Q, int64_t ldq, float* C,
-                int64_t ldc, int64_t M, int64_t N, int64_t K, int splits, float* slab_ws, void* stream);
+/* Raw GEMM primitive, exposed for kernel-level tests: C[M][ldc] (fp32) = sum_k P(m,k) Q(n,k).
+ * p_kmajor / q_kmajor = 1: the operand is stored [rows][ld] with K contiguous (P(m,k) = P[m*ld+k]);
+ * 0: stored [K][ld] with M (N) contiguous (P(m,k) = P[k*ld+m]). Elements of `precision` type;
+ * the M (N) extent is padded to a multiple of 128 in the allocation, K % 64 == 0, pads zero.
+ * (P MN-major with Q K-major is not instantiated.) */
+int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t ldp, const void* Q,
+             int64_t ldq, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, int splits,
+             float* slab_ws, void* stream);
 
 /* Live kernel timing for the benchmark's roofline figure: between gm2_timing_begin(classes) and
  * gm2_timing_end, every launch of a selected kernel class is bracketed by a hipEvent pair on its

@@ -29,37 +29,50 @@ if torch.cuda.is_available():
     from gm2.data import ResidentMatrix
 
 
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
 @pytest.mark.parametrize("prec", ["f32", "bf16"])
 @pytest.mark.parametrize("M,N,K,splits", [(128, 128, 64, 1), (200, 300, 192, 1), (256, 1024, 1024, 1),
-                                          (300, 256, 4096, 4), (1000, 130, 320, 1)])
-def test_gemm_nt(prec, M, N, K, splits):
+                                          (300, 256, 4096, 4), (1000, 130, 320, 1), (2048, 1024, 512, 1)])
+def test_gemm(prec, layout, M, N, K, splits):
+    """C = P.Q^T with each operand K-major ([rows][K]) or MN-major ([K][rows], read through
+    ds_read_b64_tr_b16 / ds_read_b32): nt = both K-major (forward), nn = Q MN-major (input
+    gradients), tn = both MN-major (weight gradients). fp32 accumulation of exact products."""
     g = torch.Generator().manual_seed(M * 7 + N * 13 + K)
     Mp, Np = -(-M // 128) * 128, -(-N // 128) * 128
     P = torch.randn(Mp, K, generator=g)
     Q = torch.randn(Np, K, generator=g)
     if prec == "bf16":
         P, Q = P.bfloat16().float(), Q.bfloat16().float()
-        Pd, Qd, pr = P.bfloat16().cuda(), Q.bfloat16().cuda(), native.GM2_BF16
-    else:
-        Pd, Qd, pr = P.cuda(), Q.cuda(), native.GM2_F32
+    pk, qk = {"nt": (True, True), "nn": (True, False), "tn": (False, False)}[layout]
+    Ps = P if pk else P.T.contiguous()
+    Qs = Q if qk else Q.T.contiguous()
+    dt = torch.bfloat16 if prec == "bf16" else torch.float32
+    pr = native.GM2_BF16 if prec == "bf16" else native.GM2_F32
+    Pd, Qd = Ps.to(dt).cuda(), Qs.to(dt).cuda()
     C = torch.full((M, N), float("nan"), device="cuda")
-    slab = torch.empty(splits * M * N, device="cuda") if splits > 1 else None
-    native.gemm_nt(pr, Pd, K, Qd, K, C, N, M, N, K, splits, slab)
+    slab = torch.empty(splits * M * N + 4, device="cuda") if splits > 1 else None
+    native.gemm(pr, Pd, Ps.shape[1], Qd, Qs.shape[1], C, N, M, N, K, splits, slab, pk, qk)
     ref = (P[:M].double() @ Q[:N].double().T)
     err = (C.cpu().double() - ref).abs().max().item()
     scale = (P[:M].double().abs() @ Q[:N].double().abs().T).max().item()
     assert torch.isfinite(C).all()
-    assert err <= 2e-6 * scale, (err, scale)  # fp32 accumulation of exact products
+    assert err <= 2e-6 * scale, (err, scale)
 
 
-def test_gemm_asymmetric_layout():
-    """A = I against an asymmetric B catches a transposed C/D map (guide §3)."""
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+def test_gemm_asymmetric_layout(prec, layout):
+    """A = I against an asymmetric B catches a transposed C/D map or tr-read map (guide §3)."""
     K = 128
-    P = torch.zeros(128, K)
-    P[:, :128] = torch.eye(128)
-    Q = torch.arange(128 * K, dtype=torch.float32).reshape(128, K) % 97
+    P = torch.eye(128)
+    Q = (torch.arange(128 * K, dtype=torch.float32).reshape(128, K) % 97)
+    pk, qk = {"nt": (True, True), "nn": (True, False), "tn": (False, False)}[layout]
+    Ps = P if pk else P.T.contiguous()
+    Qs = Q if qk else Q.T.contiguous()
+    dt = torch.bfloat16 if prec == "bf16" else torch.float32
+    pr = native.GM2_BF16 if prec == "bf16" else native.GM2_F32
     C = torch.empty(128, 128, device="cuda")
-    native.gemm_nt(native.GM2_F32, P.cuda(), K, Q.cuda(), K, C, 128, 128, 128, K)
+    native.gemm(pr, Ps.to(dt).cuda(), 128, Qs.to(dt).cuda(), 128, C, 128, 128, 128, K, 1, None, pk, qk)
     np.testing.assert_array_equal(C.cpu().numpy(), Q.T.numpy())
 
 
