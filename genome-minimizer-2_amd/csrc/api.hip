@@ -2,7 +2,10 @@
 // train / eval / sample hot path. Host-side only; kernels live in gemm.hip and kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -80,8 +83,8 @@ struct Layout {
   // GEMM shadows (T), natural [out][in] layout, zero-padded: each serves as a K-major operand in
   // the forward GEMM and as an MN-major operand ([K=out][N=in]) in the backward dX GEMM
   int64_t sE0, sE1, sE2, sHD, sD0, sD1, sD2, sD3;
-  int64_t X, XB, Y[6], A[6], save[6], HD, Z, dL, slabs, slab_cap, dY, dH;
-  int64_t bnpart, colpart, colpart_cap, losspart, losspart_cap, klpart, gradpart, clip, total;
+  int64_t X, XB, Y[6], A[6], save[6], HD, Z, dL, slabs, slab_cap, side_slabs, side_cap, dY[6], DA, dH;
+  int64_t bncoef, bnpart, colpart, colpart_cap, losspart, losspart_cap, klpart, gradpart, clip, total;
 };
 
 Layout make_layout(const gm2_dims* gd, int prec) {
@@ -119,9 +122,14 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   const int64_t maxN = std::max<int64_t>({H, 2 * d.L, d.Lr, 128});
   o.slab_cap = std::max<int64_t>(1024LL * kTile * kTile, Bm * maxN);
   o.slabs = take(o.slab_cap * 4);
-  o.dY = take(Bm * H * es);
+  // weight-gradient GEMMs run on a side stream: their own split-K scratch, one dY per layer
+  o.side_cap = std::max<int64_t>(8LL * H * std::max<int64_t>(H, d.L2r), 1024LL * kTile * kTile);
+  o.side_slabs = take(o.side_cap * 4);
+  for (int i = 0; i < 6; ++i) o.dY[i] = take(Bm * H * es);
+  o.DA = take(Bm * H * 4);           // summed split-K input gradient (fp32)
   o.dH = take(Bm * d.L2r * es);      // d(mu | logvar) [Bm][L2r]
   o.bnpart = take((Bm / kBnRowChunk) * H * 8);
+  o.bncoef = take(5 * H * 4);
   o.colpart_cap = std::max<int64_t>({(Bm / kTile) * d.Gp, (Bm / 64) * H, (Bm / 64) * 2 * d.L});
   o.colpart = take(o.colpart_cap * 4);
   o.losspart_cap = std::max<int64_t>((d.Gp / kTile) * (Bm / kTile) * 2, Bm / 64);
@@ -139,18 +147,54 @@ struct Ctx {
   char* ws;
   hipStream_t s;
   const Dims& d;
-  Ctx(const Layout& l, void* w, void* st) : lo(l), ws((char*)w), s((hipStream_t)st), d(l.d) {}
+  int64_t slab_off, slab_cap;  // split-K scratch of this stream
+  Ctx(const Layout& l, void* w, void* st)
+      : lo(l), ws((char*)w), s((hipStream_t)st), d(l.d), slab_off(l.slabs), slab_cap(l.slab_cap) {}
+  Ctx side(hipStream_t st) const {
+    Ctx c(lo, ws, st);
+    c.slab_off = lo.side_slabs;
+    c.slab_cap = lo.side_cap;
+    return c;
+  }
   T* t(int64_t off) const { return (T*)(ws + off); }
   float* f(int64_t off) const { return (float*)(ws + off); }
 };
 
-// split-K so that a launch has ~1 block per CU (256-tile, 1 block/CU resident) or ~2 (128-tile)
-int pick_splits(int tiles, int nk, int tile) {
-  const int target = tile == 256 ? 256 : 512;
-  int s = (target + tiles - 1) / tiles;
-  s = std::min(s, 8);
-  s = std::min(s, std::max(1, nk / 8));
-  return std::max(1, s);
+// ---------------------------------------------------------------------------------------------
+// side stream for the weight-gradient GEMMs (fork/join through events; capture-safe). One per
+// device, created on first use. GM2_SIDE_STREAM=0 keeps everything on the caller's stream.
+// ---------------------------------------------------------------------------------------------
+struct SideRes {
+  hipStream_t side = nullptr;
+  std::vector<hipEvent_t> ev;
+  size_t next = 0;
+};
+
+SideRes* side_res() {
+  static const bool enabled = [] {
+    const char* e = getenv("GM2_SIDE_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  if (!enabled) return nullptr;
+  static std::mutex mu;
+  static std::map<int, SideRes> per_dev;
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  SideRes& r = per_dev[dev];
+  if (!r.side) {
+    HIP_OK(hipStreamCreateWithFlags(&r.side, hipStreamNonBlocking));
+    r.ev.resize(64);
+    for (auto& e : r.ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  return &r;
+}
+
+// make `to` wait for everything enqueued on `from` so far
+void order(SideRes* r, hipStream_t from, hipStream_t to) {
+  hipEvent_t e = r->ev[r->next++ % r->ev.size()];
+  HIP_OK(hipEventRecord(e, from));
+  HIP_OK(hipStreamWaitEvent(to, e, 0));
 }
 
 // GEMM into the fp32 slab scratch (split-K slices summed by the consumer). Returns #slabs.
@@ -158,11 +202,10 @@ template <typename T>
 int gemm_to_slabs(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64_t ldq, int Np, int M, int N,
                   int K, int64_t ldc, int pk = 1, int qk = 1) {
   GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0, pk, qk};
-  const int tile = gemm_tile_for<T>(g);
-  const int S = pick_splits((Mp / tile) * (Np / tile), K / E<T>::KT, tile);
+  const int S = plan_gemm<T>(g).splits;
   const int64_t slab = (int64_t)Mp * ldc;
-  if ((int64_t)S * slab > c.lo.slab_cap) throw Gm2Error("slab capacity exceeded");
-  return launch_gemm_store<T>(g, S, c.f(c.lo.slabs), nullptr, 0, ldc, slab, nullptr, c.s);
+  if ((int64_t)S * slab > c.slab_cap) throw Gm2Error("slab capacity exceeded");
+  return launch_gemm_store<T>(g, S, c.f(c.slab_off), nullptr, 0, ldc, slab, nullptr, c.s);
 }
 
 // GEMM into C0/C1 (fp32, row split at msplit). Launches with too few tiles to fill the chip are
@@ -171,16 +214,15 @@ template <typename T>
 void gemm_to(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64_t ldq, int Np, int M, int N, int K,
              float* C0, float* C1, int msplit, int64_t ldc, int pk = 1, int qk = 1) {
   GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0, pk, qk};
-  const int tile = gemm_tile_for<T>(g);
-  int S = pick_splits((Mp / tile) * (Np / tile), K / E<T>::KT, tile);
+  int S = plan_gemm<T>(g).splits;
   const int64_t slab = round_up((int64_t)M * N, 4);
-  if ((int64_t)S * slab > c.lo.slab_cap) S = 1;
+  if ((int64_t)S * slab > c.slab_cap) S = 1;
   if (S <= 1) {
     launch_gemm_store<T>(g, 1, C0, C1, msplit, ldc, 0, nullptr, c.s);
     return;
   }
-  S = launch_gemm_store<T>(g, S, c.f(c.lo.slabs), nullptr, 0, N, slab, nullptr, c.s);
-  launch_slab_sum(c.f(c.lo.slabs), S, slab, M, N, C0, C1, C1 ? msplit : M, ldc, c.s);
+  S = launch_gemm_store<T>(g, S, c.f(c.slab_off), nullptr, 0, N, slab, nullptr, c.s);
+  launch_slab_sum(c.f(c.slab_off), S, slab, M, N, C0, C1, C1 ? msplit : M, ldc, c.s);
 }
 
 // the 6 BatchNorm blocks: (linear weight, linear bias, bn gamma, bn beta)
@@ -271,9 +313,9 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
     const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(shadow_in[i]), i == 3 ? d.Lr : Kin, H, B, H, Kin, H);
     launch_bn_fwd_partial(c.f(l.slabs), S, (int64_t)Bp * H, H, prm + d.off[kBlk[i][1]], B, H, c.f(l.Y[i]),
                           c.f(l.bnpart), c.s);
-    launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train, prm + d.off[kBlk[i][2]],
-                           prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
-                           c.f(l.save[i]), c.t(l.A[i]), nullptr, 0, c.s);
+    launch_bn_fwd_finalize(c.f(l.bnpart), B, H, train, prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
+                           bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, c.f(l.save[i]), c.f(l.bncoef), c.s);
+    launch_bn_fwd_apply2<T>(c.f(l.Y[i]), H, c.f(l.bncoef), B, Bp, H, c.t(l.A[i]), c.s);
     in = c.t(l.A[i]);
     ldin = H;
     Kin = H;
@@ -299,36 +341,50 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   const int B = (int)b->n, Bp = (int)round_up(B, kTile);
   const int H = (int)d.H, L = (int)d.L, G = (int)d.G;
   const int Gp = (int)d.Gp, Lr = (int)d.Lr, L2r = (int)d.L2r;
+  // weight gradients go to a side stream: they are off the critical path (dY -> dX -> BN -> ...)
+  // and fill the tails of its launches; the join at the end orders them before the caller's work
+  SideRes* sr = side_res();
+  const Ctx<T> w = sr ? c.side(sr->side) : c;
+  auto fork = [&] {
+    if (sr) order(sr, c.s, w.s);
+  };
   // output layer: dW9[g][h] = sum_b dL[b][g] A5[b][h] ; dA5[b][h] = sum_g dL[b][g] W9[g][h]
-  gemm_to<T>(c, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
+  fork();
+  gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
   int S = gemm_to_slabs<T>(c, c.t(l.dL), Gp, Bp, c.t(l.sD3), H, H, B, H, Gp, H, 1, 0);
   const int64_t shadow_w[6] = {l.sE0, l.sE1, l.sE2, l.sD0, l.sD1, l.sD2};
   for (int i = 5; i >= 0; --i) {
     const int64_t slab = (int64_t)Bp * H;
-    launch_bn_bwd_partial(c.f(l.slabs), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
-                          prm + d.off[kBlk[i][3]], B, H, c.f(l.bnpart), c.s);
-    launch_bn_bwd_apply<T>(c.f(l.slabs), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
-                           prm + d.off[kBlk[i][3]], c.f(l.bnpart), B, Bp, H, gr + d.off[kBlk[i][2]],
-                           gr + d.off[kBlk[i][3]], c.t(l.dY), nullptr, 0, c.f(l.colpart), c.s);
+    const bool sum = S > 1;
+    launch_bn_bwd_partial(c.f(c.slab_off), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
+                          prm + d.off[kBlk[i][3]], B, H, c.f(l.bnpart), sum ? c.f(l.DA) : nullptr, c.s);
+    launch_bn_bwd_finalize(c.f(l.bnpart), B, H, c.f(l.save[i]), prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
+                           gr + d.off[kBlk[i][2]], gr + d.off[kBlk[i][3]], c.f(l.bncoef), c.s);
+    launch_bn_bwd_apply2<T>(sum ? c.f(l.DA) : c.f(c.slab_off), c.f(l.Y[i]), H, c.f(l.bncoef), B, Bp, H,
+                            c.t(l.dY[i]), c.f(l.colpart), c.s);
     launch_colsum(c.f(l.colpart), Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, c.s);
-    if (i == 0) {  // input layer: weight gradient only
-      gemm_to<T>(c, c.t(l.dY), H, H, c.t(l.X), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 0, 0);
+    const T* dY = c.t(l.dY[i]);
+    if (i == 0) {  // input layer: weight gradient only (on the main stream: nothing left to overlap)
+      gemm_to<T>(c, dY, H, H, c.t(l.X), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 0, 0);
       break;
     }
+    fork();
     if (i == 3) {  // decoder input layer, then back through the reparameterisation and the heads
-      gemm_to<T>(c, c.t(l.dY), H, H, c.t(l.Z), Lr, Lr, H, L, Bp, gr + d.off[D0W], nullptr, 0, L, 0, 0);
-      S = gemm_to_slabs<T>(c, c.t(l.dY), H, Bp, c.t(l.sD0), Lr, Lr, B, L, H, L, 1, 0);
-      launch_reparam_bwd<T>(c.f(l.slabs), S, (int64_t)Bp * L, L, c.f(l.HD), b->eps, scal, B, Bp, L, c.t(l.dH), L2r,
-                            nullptr, 0, 0, c.f(l.colpart), c.s);
+      gemm_to<T>(w, dY, H, H, c.t(l.Z), Lr, Lr, H, L, Bp, gr + d.off[D0W], nullptr, 0, L, 0, 0);
+      S = gemm_to_slabs<T>(c, dY, H, Bp, c.t(l.sD0), Lr, Lr, B, L, H, L, 1, 0);
+      launch_reparam_bwd<T>(c.f(c.slab_off), S, (int64_t)Bp * L, L, c.f(l.HD), b->eps, scal, B, Bp, L, c.t(l.dH),
+                            L2r, nullptr, 0, 0, c.f(l.colpart), c.s);
       launch_colsum(c.f(l.colpart), Bp / 64, 2 * L, 2 * L, gr + d.off[MUB], gr + d.off[LVB], L, c.s);
-      gemm_to<T>(c, c.t(l.dH), L2r, L2r, c.t(l.A[2]), H, H, 2 * L, H, Bp, gr + d.off[MUW], gr + d.off[LVW], L, H, 0,
+      fork();
+      gemm_to<T>(w, c.t(l.dH), L2r, L2r, c.t(l.A[2]), H, H, 2 * L, H, Bp, gr + d.off[MUW], gr + d.off[LVW], L, H, 0,
                  0);
       S = gemm_to_slabs<T>(c, c.t(l.dH), L2r, Bp, c.t(l.sHD), H, H, B, H, (int)d.K2L, H, 1, 0);
       continue;
     }
-    gemm_to<T>(c, c.t(l.dY), H, H, c.t(l.A[i - 1]), H, H, H, H, Bp, gr + d.off[kBlk[i][0]], nullptr, 0, H, 0, 0);
-    S = gemm_to_slabs<T>(c, c.t(l.dY), H, Bp, c.t(shadow_w[i]), H, H, B, H, H, H, 1, 0);
+    gemm_to<T>(w, dY, H, H, c.t(l.A[i - 1]), H, H, H, H, Bp, gr + d.off[kBlk[i][0]], nullptr, 0, H, 0, 0);
+    S = gemm_to_slabs<T>(c, dY, H, Bp, c.t(shadow_w[i]), H, H, B, H, H, H, 1, 0);
   }
+  if (sr) order(sr, w.s, c.s);  // join
 }
 
 template <typename T>
@@ -347,9 +403,9 @@ void decode_chain(const Ctx<T>& c, const float* prm, float* bn, int n, uint8_t* 
     const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(shadow_in[j]), ldw, H, n, H, Kin, H);
     launch_bn_fwd_partial(c.f(l.slabs), S, (int64_t)Bp * H, H, prm + d.off[kBlk[i][1]], n, H, c.f(l.Y[i]),
                           c.f(l.bnpart), c.s);
-    launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), n, Bp, H, 0, prm + d.off[kBlk[i][2]],
-                           prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, nullptr,
-                           c.t(l.A[i]), nullptr, 0, c.s);
+    launch_bn_fwd_finalize(c.f(l.bnpart), n, H, 0, prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
+                           bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, nullptr, c.f(l.bncoef), c.s);
+    launch_bn_fwd_apply2<T>(c.f(l.Y[i]), H, c.f(l.bncoef), n, Bp, H, c.t(l.A[i]), c.s);
     in = c.t(l.A[i]);
     ldin = H;
     Kin = H;
@@ -503,9 +559,9 @@ int gm2_encode(const gm2_dims* d, int prec, const gm2_batch* batch, const float*
         const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(sh[i]), Kin, H, B, H, Kin, H);
         launch_bn_fwd_partial(c.f(lo.slabs), S, (int64_t)Bp * H, H, params + dd.off[kBlk[i][1]], B, H, c.f(lo.Y[i]),
                               c.f(lo.bnpart), c.s);
-        launch_bn_fwd_apply<T>(c.f(lo.Y[i]), H, c.f(lo.bnpart), B, Bp, H, 0, params + dd.off[kBlk[i][2]],
-                               params + dd.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
-                               nullptr, c.t(lo.A[i]), nullptr, 0, c.s);
+        launch_bn_fwd_finalize(c.f(lo.bnpart), B, H, 0, params + dd.off[kBlk[i][2]], params + dd.off[kBlk[i][3]],
+                               bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, nullptr, c.f(lo.bncoef), c.s);
+        launch_bn_fwd_apply2<T>(c.f(lo.Y[i]), H, c.f(lo.bncoef), B, Bp, H, c.t(lo.A[i]), c.s);
         in = c.t(lo.A[i]);
         ldin = H;
         Kin = H;

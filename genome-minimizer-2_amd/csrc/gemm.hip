@@ -232,21 +232,33 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
   mainloop<C, T, AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   float* Cz = C0 + (int64_t)tl.split * slab;
+  // Stage one wave-row band (WTM x BN fp32) at a time through the (now free) staging LDS, then
+  // store whole rows: each wave instruction writes 256 contiguous bytes of one C row (the
+  // accumulator's own layout would write four 64-byte pieces of four rows).
+  float* img = (float*)smem;
+  static_assert(C::WTM * C::BN * 4 <= C::LDS, "epilogue band must fit the staging LDS");
 #pragma unroll
-  for (int ni = 0; ni < C::FN; ++ni) {
-    const int n = tl.n0 + wn * C::WTN + ni * 16 + (lane & 15);
-    if (n >= g.N) continue;
-    const float bn = bias ? bias[n] : 0.f;
+  for (int h = 0; h < C::WGM; ++h) {
+    if (wm == h) {
 #pragma unroll
-    for (int mi = 0; mi < C::FM; ++mi)
+      for (int mi = 0; mi < C::FM; ++mi)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = tl.m0 + wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
-        if (m >= g.M) continue;
-        const float v = acc[mi][ni][j] + bn;
+        for (int ni = 0; ni < C::FN; ++ni)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            img[(mi * 16 + 4 * (lane >> 4) + j) * C::BN + wn * C::WTN + ni * 16 + (lane & 15)] = acc[mi][ni][j];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < C::WTM * C::BN; i += C::NT) {
+      const int r = i / C::BN, cc = i % C::BN;
+      const int m = tl.m0 + h * C::WTM + r, n = tl.n0 + cc;
+      if (m < g.M && n < g.N) {
+        const float v = img[i] + (bias ? bias[n] : 0.f);
         if (m < msplit) Cz[(int64_t)m * ldc + n] = v;
         else C1[(int64_t)(m - msplit) * ldc + n] = v;
       }
+    }
+    __syncthreads();
   }
 }
 
@@ -517,10 +529,24 @@ static void check_gemm(const GemmArgs<T>& g, int tile) {
   if ((g.ldp * sizeof(T)) % 16 || (g.ldq * sizeof(T)) % 16) throw Gm2Error("gemm: ld not 16-B multiple");
 }
 
-// The big tile needs both padded extents divisible by 256 and enough work to fill the chip
+// Tile / split-K plan. Big tiles when they alone fill the chip, or when K is long enough that a
+// split-K slab round trip is cheap next to the work; otherwise the 128-tile, split only when it
+// leaves most CUs idle (and never below 8 K-steps per slice).
+template <typename T>
+GemmPlan plan_gemm(const GemmArgs<T>& g) {
+  const int nk = g.K / E<T>::KT;
+  const int tiles_big = (g.Mp % 256 == 0 && g.Np % 256 == 0) ? (g.Mp / 256) * (g.Np / 256) : 0;
+  const int tiles_small = (g.Mp / 128) * (g.Np / 128);
+  auto cap = [&](int s) { return std::max(1, std::min({s, 8, std::max(1, nk / 8)})); };
+  if (tiles_big >= 256) return {256, 1};
+  if (tiles_big > 0 && g.K >= 8192) return {256, cap((256 + tiles_big - 1) / tiles_big)};
+  if (tiles_small >= 192) return {128, 1};
+  return {128, cap((256 + tiles_small - 1) / tiles_small)};
+}
+
 template <typename T>
 static bool use_big(const GemmArgs<T>& g) {
-  return g.Mp % 256 == 0 && g.Np % 256 == 0 && (int64_t)g.Mp * g.Np >= (int64_t)2048 * 1024 && g.K >= 512;
+  return plan_gemm(g).tile == 256;
 }
 
 template <class C, typename T, bool AK, bool BK>
@@ -557,13 +583,9 @@ static int store_impl(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
 }
 
 template <typename T>
-int gemm_tile_for(const GemmArgs<T>& g) {
-  return use_big(g) ? 256 : 128;
-}
-
-template <typename T>
 int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
                       const float* bias, hipStream_t s) {
+  if (splits < 0) splits = plan_gemm(g).splits;
   if (use_big(g)) {
     check_gemm(g, 256);
     return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, s);
@@ -607,7 +629,7 @@ static void recon_impl(const GemmArgs<T>& g, const float* bias, const uint32_t* 
 // the fp32 parity path stays on the 128-tile (a 256-row fp32 dL image would not fit the LDS)
 template <typename T>
 static bool recon_big(const GemmArgs<T>& g) {
-  return sizeof(T) == 2 && use_big(g);
+  return sizeof(T) == 2 && g.Mp % 256 == 0 && g.Np % 256 == 0 && (g.Mp / 256) * (g.Np / 256) >= 128;
 }
 
 template <typename T>
@@ -641,7 +663,7 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
                                     hipStream_t);                                                                \
   template int gemm_recon_grid_blocks<T>(const GemmArgs<T>&);                                                   \
   template int gemm_recon_row_tiles<T>(const GemmArgs<T>&);                                                     \
-  template int gemm_tile_for<T>(const GemmArgs<T>&);                                                            \
+  template GemmPlan plan_gemm<T>(const GemmArgs<T>&);                                                          \
   template void launch_gemm_recon_loss<T>(const GemmArgs<T>&, const float*, const uint32_t*, int64_t, int,        \
                                           const float*,                                                         \
                                           T*, int64_t, T*, int64_t, float*, float*, int64_t, hipStream_t);

@@ -77,6 +77,7 @@ struct TimedLaunch {  // records an event pair around a launch when its class is
 };
 
 // ---- gemm.hip ----
+// splits < 0: use plan_gemm's split-K factor. Returns the number of slabs written.
 template <typename T>
 int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc,
                       int64_t slab, const float* bias, hipStream_t s);
@@ -84,8 +85,11 @@ template <typename T>
 int gemm_recon_grid_blocks(const GemmArgs<T>& g);
 template <typename T>
 int gemm_recon_row_tiles(const GemmArgs<T>& g);
+struct GemmPlan {
+  int tile, splits;
+};
 template <typename T>
-int gemm_tile_for(const GemmArgs<T>& g);
+GemmPlan plan_gemm(const GemmArgs<T>& g);
 template <typename T>
 void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const uint32_t* xbits, int64_t ldxb, int with_grad,
                             const float* scal, T* dL, int64_t ldd, T* dLT, int64_t lddt, float* loss_part,
@@ -112,14 +116,26 @@ template <typename T>
 void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
                          const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,
                          T* AT, int64_t ldat, hipStream_t s);
-// BN backward: partials of sum(do), sum((y-mean)*do) with do = dA * [bn_out > 0]
+// BN backward: partials of sum(do), sum((y-mean)*do) with do = dA * [bn_out > 0]; optionally
+// writes the summed split-K dA (dsum) so the apply pass reads one slab instead of S
 void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
-                           const float* gamma, const float* beta, int B, int H, float* part, hipStream_t s);
+                           const float* gamma, const float* beta, int B, int H, float* part, float* dsum,
+                           hipStream_t s);
 template <typename T>
 void launch_bn_bwd_apply(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
                          const float* gamma, const float* beta, const float* part, int B, int Bp, int H,
                          float* dgamma, float* dbeta, T* dY, T* dYT, int64_t ldyt, float* colpart,
                          hipStream_t s);
+// BatchNorm v2 (finalize once per column, vectorised elementwise passes)
+void launch_bn_fwd_finalize(const float* part, int B, int H, int train, const float* gamma, const float* beta,
+                            float* rmean, float* rvar, float* save, float* coef, hipStream_t s);
+template <typename T>
+void launch_bn_fwd_apply2(const float* Y, int64_t ld, const float* coef, int B, int Bp, int H, T* A, hipStream_t s);
+void launch_bn_bwd_finalize(const float* part, int B, int H, const float* save, const float* gamma,
+                            const float* beta, float* dgamma, float* dbeta, float* cf, hipStream_t s);
+template <typename T>
+void launch_bn_bwd_apply2(const float* da, const float* Y, int64_t ld, const float* cf, int B, int Bp, int H, T* dY,
+                          float* colpart, hipStream_t s);
 // reparameterization + KL (model.py:100-104, loss_components.py:77)
 template <typename T>
 void launch_reparam(const float* slabs, int S, int64_t slab, int L, const float* bmu, const float* blv,

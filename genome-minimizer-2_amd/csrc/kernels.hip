@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict_
                                                       const float* __restrict__ Y, int64_t ld,
                                                       const float* __restrict__ save, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, int B, int H,
-                                                      float2* __restrict__ part) {
+                                                      float2* __restrict__ part, float* __restrict__ dsum) {
   __shared__ float red[2][4][64];
   const int c = threadIdx.x & 63;
   const int col = blockIdx.x * 64 + c;
@@ -206,6 +206,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict_
     const int64_t o = (int64_t)(r0 + rl) * ld + col;
     float da = dslabs[o];
     for (int s = 1; s < S; ++s) da += dslabs[(int64_t)s * slab + o];
+    if (dsum) dsum[o] = da;
     const float y = Y[o];
     const float d = fmaf(y, alpha, bprime) > 0.f ? da : 0.f;
     s1 += d;
@@ -623,6 +624,163 @@ __global__ __launch_bounds__(256) void k_slab_sum(const float* __restrict__ slab
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// BatchNorm v2: per-column finalize kernels (the fp64 chunk merge runs once per column) and
+// vectorised elementwise apply passes (4 columns per thread).
+// coef layout: [0][H] alpha = invstd*gamma, [1][H] beta' = fma(-mean, alpha, beta)
+// bwd cf layout: [0] mean, [1] alpha, [2] beta', [3] sum(do)/B, [4] sum((y-mean)do)*invstd^2/B
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bn_fwd_finalize(const float2* __restrict__ part, int B, int H, int train,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       float* __restrict__ rmean, float* __restrict__ rvar,
+                                                       float* __restrict__ save, float* __restrict__ coef) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= H) return;
+  float invstd, meanf;
+  if (train) {
+    double mean, var;
+    bn_merge(part, B, H, col, mean, var);
+    invstd = (float)(1.0 / sqrt(var + kBnEps));
+    meanf = (float)mean;
+    save[col] = meanf;
+    save[H + col] = invstd;
+    const double unb = B > 1 ? var * (double)B / (double)(B - 1) : var;
+    rmean[col] = (float)(kBnMomentum * mean + (1.0 - kBnMomentum) * (double)rmean[col]);
+    rvar[col] = (float)(kBnMomentum * unb + (1.0 - kBnMomentum) * (double)rvar[col]);
+  } else {
+    // eval transform bit-identical to the reference CPU path (pinned in tests): float
+    // invstd = 1/sqrt(rv + eps), alpha = gamma*invstd, beta' = fma(-mean, alpha, beta)
+    meanf = rmean[col];
+    invstd = 1.0f / sqrtf(rvar[col] + (float)kBnEps);
+    if (save) { save[col] = meanf; save[H + col] = invstd; }
+  }
+  const float alpha = invstd * gamma[col];
+  coef[col] = alpha;
+  coef[H + col] = fmaf(-meanf, alpha, beta[col]);
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(T* dst, float a, float b, float c, float d) {
+  if constexpr (sizeof(T) == 2) {
+    uint2 pk;
+    pk.x = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+    pk.y = (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16);
+    *(uint2*)dst = pk;
+  } else {
+    *(float4*)dst = make_float4(a, b, c, d);
+  }
+}
+
+// A = relu(y*alpha + beta') for rows < B, 0 for rows in [B, Bp)
+template <typename T>
+__global__ __launch_bounds__(256) void k_bn_fwd_apply2(const float* __restrict__ Y, int64_t ld,
+                                                     const float* __restrict__ coef, int B, int Bp, int H,
+                                                     T* __restrict__ A) {
+  const int q4 = H / 4;
+  const int64_t total = (int64_t)Bp * q4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int r = (int)(i / q4), c = (int)(i % q4) * 4;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < B) {
+      const float4 y = *(const float4*)(Y + (int64_t)r * ld + c);
+      const float4 al = *(const float4*)(coef + c);
+      const float4 be = *(const float4*)(coef + H + c);
+      o.x = fmaxf(fmaf(y.x, al.x, be.x), 0.f);
+      o.y = fmaxf(fmaf(y.y, al.y, be.y), 0.f);
+      o.z = fmaxf(fmaf(y.z, al.z, be.z), 0.f);
+      o.w = fmaxf(fmaf(y.w, al.w, be.w), 0.f);
+    }
+    store4<T>(A + (int64_t)r * ld + c, o.x, o.y, o.z, o.w);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float2* __restrict__ part, int B, int H,
+                                                       const float* __restrict__ save, const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float* __restrict__ dgamma,
+                                                       float* __restrict__ dbeta, float* __restrict__ cf) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= H) return;
+  double s1 = 0.0, s2 = 0.0;
+  const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
+  for (int ch = 0; ch < nch; ++ch) {
+    const float2 p = part[(int64_t)ch * H + col];
+    s1 += p.x;
+    s2 += p.y;
+  }
+  const float mean = save[col], invstd = save[H + col];
+  const float alpha = invstd * gamma[col];
+  dgamma[col] = (float)(s2 * invstd);
+  dbeta[col] = (float)s1;
+  cf[col] = mean;
+  cf[H + col] = alpha;
+  cf[2 * H + col] = fmaf(-mean, alpha, beta[col]);
+  cf[3 * H + col] = (float)(s1 / B);
+  cf[4 * H + col] = (float)(s2 * (double)invstd * invstd / B);
+}
+
+// dx = (do - grad_mean - (y-mean)*proj_scale) * alpha, do = da*[y*alpha+beta' > 0]; rows >= B -> 0.
+// Block: 256 columns x 64 rows (4 row groups); per-(64-row chunk, column) sums of dx -> colpart.
+template <typename T>
+__global__ __launch_bounds__(256) void k_bn_bwd_apply2(const float* __restrict__ da, const float* __restrict__ Y,
+                                                     int64_t ld, const float* __restrict__ cf, int B, int H,
+                                                     T* __restrict__ dY, float* __restrict__ colpart) {
+  __shared__ float4 red[4][64];
+  const int cg = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + cg * 4;
+  const int r0 = blockIdx.y * 64;
+  const bool ok = c < H;  // H % 128 == 0: the last block may cover only 128 of its 256 columns
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok) {
+    const float4 mean = *(const float4*)(cf + c), al = *(const float4*)(cf + H + c);
+    const float4 be = *(const float4*)(cf + 2 * H + c), gm = *(const float4*)(cf + 3 * H + c);
+    const float4 ps = *(const float4*)(cf + 4 * H + c);
+    for (int rl = rg; rl < 64; rl += 4) {
+      const int r = r0 + rl;
+      float4 dx = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < B) {
+        const int64_t o = (int64_t)r * ld + c;
+        const float4 a = *(const float4*)(da + o);
+        const float4 y = *(const float4*)(Y + o);
+        const float d0 = fmaf(y.x, al.x, be.x) > 0.f ? a.x : 0.f;
+        const float d1 = fmaf(y.y, al.y, be.y) > 0.f ? a.y : 0.f;
+        const float d2 = fmaf(y.z, al.z, be.z) > 0.f ? a.z : 0.f;
+        const float d3 = fmaf(y.w, al.w, be.w) > 0.f ? a.w : 0.f;
+        dx.x = (d0 - gm.x - (y.x - mean.x) * ps.x) * al.x;
+        dx.y = (d1 - gm.y - (y.y - mean.y) * ps.y) * al.y;
+        dx.z = (d2 - gm.z - (y.z - mean.z) * ps.z) * al.z;
+        dx.w = (d3 - gm.w - (y.w - mean.w) * ps.w) * al.w;
+      }
+      acc.x += dx.x; acc.y += dx.y; acc.z += dx.z; acc.w += dx.w;
+      store4<T>(dY + (int64_t)r * ld + c, dx.x, dx.y, dx.z, dx.w);
+    }
+  }
+  red[rg][cg] = acc;
+  __syncthreads();
+  if (rg == 0 && ok) {
+    float4 v = red[0][cg];
+    for (int k = 1; k < 4; ++k) { v.x += red[k][cg].x; v.y += red[k][cg].y; v.z += red[k][cg].z; v.w += red[k][cg].w; }
+    *(float4*)(colpart + (int64_t)blockIdx.y * H + c) = v;
+  }
+}
+
+// out[c] = sum_r part[r][c]: 64 columns x 4 row groups per block, fixed order (deterministic)
+__global__ __launch_bounds__(256) void k_colsum2(const float* __restrict__ part, int rows, int64_t ld, int n,
+                                               float* __restrict__ out0, float* __restrict__ out1, int nsplit) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (c < n)
+    for (int r = rg; r < rows; r += 4) s += part[(int64_t)r * ld + c];
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && c < n) {
+    const float v = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+    if (c < nsplit) out0[c] = v;
+    else out1[c - nsplit] = v;
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
@@ -657,10 +815,11 @@ void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, i
 }
 
 void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
-                           const float* gamma, const float* beta, int B, int H, float* part, hipStream_t s) {
+                           const float* gamma, const float* beta, int B, int H, float* part, float* dsum,
+                           hipStream_t s) {
   const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
   hipLaunchKernelGGL(k_bn_bwd_partial, dim3(H / 64, nch), dim3(256), 0, s, dslabs, S, slab, Y, ld, save, gamma,
-                     beta, B, H, (float2*)part);
+                     beta, B, H, (float2*)part, dsum);
   GM2_CHECK_LAUNCH();
 }
 
@@ -696,8 +855,38 @@ void launch_reparam_bwd(const float* dzslabs, int S, int64_t slab, int64_t ldsla
 
 void launch_colsum(const float* part, int rows, int64_t ld, int n, float* out0, float* out1, int nsplit,
                    hipStream_t s) {
-  hipLaunchKernelGGL(k_colsum, dim3((n + 255) / 256), dim3(256), 0, s, part, rows, ld, n, out0, out1 ? out1 : out0,
+  hipLaunchKernelGGL(k_colsum2, dim3((n + 63) / 64), dim3(256), 0, s, part, rows, ld, n, out0, out1 ? out1 : out0,
                      out1 ? nsplit : n);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_bn_fwd_finalize(const float* part, int B, int H, int train, const float* gamma, const float* beta,
+                            float* rmean, float* rvar, float* save, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((H + 255) / 256), dim3(256), 0, s, (const float2*)part, B, H, train,
+                     gamma, beta, rmean, rvar, save, coef);
+  GM2_CHECK_LAUNCH();
+}
+
+template <typename T>
+void launch_bn_fwd_apply2(const float* Y, int64_t ld, const float* coef, int B, int Bp, int H, T* A, hipStream_t s) {
+  if (H % 4 || ld % 4) throw Gm2Error("bn_apply: H %% 4");
+  const int64_t nb = std::min<int64_t>(2048, ((int64_t)Bp * H / 4 + 255) / 256);
+  hipLaunchKernelGGL(k_bn_fwd_apply2<T>, dim3((unsigned)nb), dim3(256), 0, s, Y, ld, coef, B, Bp, H, A);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_bn_bwd_finalize(const float* part, int B, int H, const float* save, const float* gamma,
+                            const float* beta, float* dgamma, float* dbeta, float* cf, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((H + 255) / 256), dim3(256), 0, s, (const float2*)part, B, H, save, gamma,
+                     beta, dgamma, dbeta, cf);
+  GM2_CHECK_LAUNCH();
+}
+
+template <typename T>
+void launch_bn_bwd_apply2(const float* da, const float* Y, int64_t ld, const float* cf, int B, int Bp, int H, T* dY,
+                          float* colpart, hipStream_t s) {
+  if (H % 128) throw Gm2Error("bn_bwd_apply: H %% 128");
+  hipLaunchKernelGGL(k_bn_bwd_apply2<T>, dim3((H + 255) / 256, Bp / 64), dim3(256), 0, s, da, Y, ld, cf, B, H, dY, colpart);
   GM2_CHECK_LAUNCH();
 }
 
@@ -779,6 +968,9 @@ void launch_adam(const float* grads, float* params, float* m, float* v, int64_t 
                                       const float*, int, int, int, T*, int64_t, T*, int64_t, int, float*,       \
                                       hipStream_t);                                                             \
   template void launch_shadow_sync<T>(const TensorTable&, const float*, hipStream_t);                          \
+  template void launch_bn_fwd_apply2<T>(const float*, int64_t, const float*, int, int, int, T*, hipStream_t);  \
+  template void launch_bn_bwd_apply2<T>(const float*, const float*, int64_t, const float*, int, int, int, T*,    \
+                                        float*, hipStream_t);                                                  \
   template void launch_adam_fused<T>(const TensorTable&, const float*, float*, float*, float*, const float*,    \
                                      const float*, hipStream_t);                                                \
   template void launch_shadow_transpose<T>(const TensorTable&, hipStream_t);
