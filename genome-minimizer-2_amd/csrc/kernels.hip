@@ -20,10 +20,10 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data
                                               const int32_t* __restrict__ rows, int B, int G, T* __restrict__ X,
                                               int64_t ldx, T* __restrict__ XT, int64_t ldxt,
                                               uint32_t* __restrict__ xbits, int64_t ldxb) {
-  __shared__ float tile[128][65];
+  __shared__ uint8_t tile[128][68];  // [column][row] bytes (pitch 68: conflict-light column reads)
   const int c0 = blockIdx.x * 128, r0 = blockIdx.y * 64;
   const int t = threadIdx.x;
-  const int ch = t & 7;          // 16-column chunk
+  const int ch = t & 7;  // 16-column chunk
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     const int rl = pass * 32 + (t >> 3);
@@ -33,33 +33,46 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data
       const int64_t src = rows ? (int64_t)rows[r] : (int64_t)r;
       v = *(const uint4*)(data + src * ld_data + c0 + ch * 16);
     }
-    const uint8_t* b = (const uint8_t*)&v;
-    float f[16];
+    uint8_t b[16];
+    *(uint4*)b = v;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int c = c0 + ch * 16 + i;
-      f[i] = (c < G) ? (float)b[i] : 0.f;
-      tile[ch * 16 + i][rl] = f[i];
+      if (c0 + ch * 16 + i >= G) b[i] = 0;
+      tile[ch * 16 + i][rl] = b[i];
     }
+    // 16 elements -> 2 (bf16) or 4 (fp32) 16-byte stores
     T* dst = X + (int64_t)r * ldx + c0 + ch * 16;
+    if constexpr (sizeof(T) == 2) {
+      uint32_t w[8];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) dst[i] = E<T>::cvt(f[i]);
+      for (int i = 0; i < 8; ++i) w[i] = (b[2 * i] ? 0x3F80u : 0u) | ((b[2 * i + 1] ? 0x3F80u : 0u) << 16);
+      *(uint4*)dst = make_uint4(w[0], w[1], w[2], w[3]);
+      *(uint4*)(dst + 8) = make_uint4(w[4], w[5], w[6], w[7]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *(float4*)(dst + 4 * i) = make_float4((float)b[4 * i], (float)b[4 * i + 1], (float)b[4 * i + 2], (float)b[4 * i + 3]);
+    }
   }
   __syncthreads();
-  // X^T: 128 rows (columns of X) x 64 (batch rows)
-  if (XT) {
+  if (XT) {  // optional explicit transpose (unused by the current schedule)
     for (int i = t; i < 128 * 64; i += 256) {
       const int c = i >> 6, rl = i & 63;
-      XT[(int64_t)(c0 + c) * ldxt + r0 + rl] = E<T>::cvt(tile[c][rl]);
+      XT[(int64_t)(c0 + c) * ldxt + r0 + rl] = E<T>::cvt((float)tile[c][rl]);
     }
   }
-  // bit-packed X^T: thread t -> column t/2, 32-row half t%2
+  // bit-packed X^T by ballot: wave w, lane = row; 32 columns per wave, one ballot per column
   if (xbits) {
-    const int c = t >> 1, h = t & 1;
-    uint32_t w = 0;
-#pragma unroll
-    for (int b = 0; b < 32; ++b) w |= (tile[c][h * 32 + b] != 0.f ? 1u : 0u) << b;
-    xbits[(int64_t)(c0 + c) * ldxb + (r0 >> 5) + h] = w;
+    const int w = t >> 6, lane = t & 63;
+    uint64_t mine = 0;
+#pragma unroll 4
+    for (int k = 0; k < 32; ++k) {
+      const uint64_t m = __ballot(tile[w * 32 + k][lane] != 0);
+      if (lane == k) mine = m;
+    }
+    if (lane < 32)
+      *(uint2*)(xbits + (int64_t)(c0 + w * 32 + lane) * ldxb + (r0 >> 5)) =
+          make_uint2((uint32_t)mine, (uint32_t)(mine >> 32));
   }
 }
 
@@ -107,21 +120,27 @@ __global__ __launch_bounds__(256) void k_bn_fwd_partial(const float* __restrict_
   if (rg == 0) part[(int64_t)blockIdx.y * H + col] = make_float2(mean, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
 }
 
-// Chan merge of per-chunk (mean, M2) -> batch mean and biased variance (double)
+// Chan's parallel merge of per-chunk (mean, M2) -> batch mean and biased variance, in two passes
+// (mean = sum n_c mean_c / B ; M2 = sum M2_c + n_c (mean_c - mean)^2), fp64, loads unrolled
 __device__ inline void bn_merge(const float2* __restrict__ part, int B, int H, int col, double& mean, double& var) {
-  double n = 0.0, mu = 0.0, M2 = 0.0;
   const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
+  double s = 0.0;
+#pragma unroll 8
+  for (int ch = 0; ch < nch; ++ch) {
+    const double nb = (double)min(kBnRowChunk, B - ch * kBnRowChunk);
+    s += nb * (double)part[(int64_t)ch * H + col].x;
+  }
+  const double mu = s / (double)B;
+  double M2 = 0.0;
+#pragma unroll 8
   for (int ch = 0; ch < nch; ++ch) {
     const double nb = (double)min(kBnRowChunk, B - ch * kBnRowChunk);
     const float2 p = part[(int64_t)ch * H + col];
-    const double delta = (double)p.x - mu;
-    const double nt = n + nb;
-    mu += delta * nb / nt;
-    M2 += (double)p.y + delta * delta * n * nb / nt;
-    n = nt;
+    const double dlt = (double)p.x - mu;
+    M2 += (double)p.y + nb * dlt * dlt;
   }
   mean = mu;
-  var = M2 / n;
+  var = M2 / (double)B;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -438,6 +457,18 @@ __global__ __launch_bounds__(256) void k_shadow_sync(TensorTable tt, const float
 // ---------------------------------------------------------------------------------------------
 // clip_grad_norm_ statistics (+ L1 term) and the fused L1 + clip + Adam update
 // ---------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void store4(T* dst, float a, float b, float c, float d) {
+  if constexpr (sizeof(T) == 2) {
+    uint2 pk;
+    pk.x = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+    pk.y = (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16);
+    *(uint2*)dst = pk;
+  } else {
+    *(float4*)dst = make_float4(a, b, c, d);
+  }
+}
+
 __device__ __forceinline__ float sgnf(float x) { return (float)((x > 0.f) - (x < 0.f)); }
 
 __global__ __launch_bounds__(256) void k_grad_stats(const float* __restrict__ p, const float* __restrict__ g,
@@ -446,11 +477,28 @@ __global__ __launch_bounds__(256) void k_grad_stats(const float* __restrict__ p,
   __shared__ double red[2][4];
   const float lam = scal[kScalLambda];
   double ss = 0.0, ab = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float pv = p[i];
-    const float gv = g[i] + lam * sgnf(pv);
-    ss += (double)gv * gv;
-    ab += fabs((double)pv);
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  if (lam != 0.f) {  // L1 present: the norm needs sign(p), the loss needs sum|p|
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+      const float4 pv = *(const float4*)(p + 4 * i), gv = *(const float4*)(g + 4 * i);
+      const float a = gv.x + lam * sgnf(pv.x), b = gv.y + lam * sgnf(pv.y);
+      const float c = gv.z + lam * sgnf(pv.z), d = gv.w + lam * sgnf(pv.w);
+      ss += (double)a * a + (double)b * b + (double)c * c + (double)d * d;
+      ab += (double)fabsf(pv.x) + (double)fabsf(pv.y) + (double)fabsf(pv.z) + (double)fabsf(pv.w);
+    }
+    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+      const float a = g[i] + lam * sgnf(p[i]);
+      ss += (double)a * a;
+      ab += fabs((double)p[i]);
+    }
+  } else {  // no L1 term (v0): gradients only, half the traffic
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+      const float4 gv = *(const float4*)(g + 4 * i);
+      ss += (double)gv.x * gv.x + (double)gv.y * gv.y + (double)gv.z * gv.z + (double)gv.w * gv.w;
+    }
+    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+      ss += (double)g[i] * g[i];
   }
   ss = wave_sum_d(ss);
   ab = wave_sum_d(ab);
@@ -567,10 +615,14 @@ __global__ __launch_bounds__(256) void k_adam_fused(TensorTable tt, const float*
     }
     if (sh) {
       int64_t r = e / d.cols, c = e - r * d.cols;
+      if (full && (d.cols & 3) == 0 && (d.sld & 3) == 0) {  // 4 elements of one row: one 8/16-B store
+        store4<T>(sh + (d.srow0 + r) * d.sld + c, pe[0], pe[1], pe[2], pe[3]);
+      } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (e + u < numel) sh[(d.srow0 + r) * d.sld + c] = E<T>::cvt(pe[u]);
-        if (++c == d.cols) { c = 0; ++r; }
+        for (int u = 0; u < 4; ++u) {
+          if (e + u < numel) sh[(d.srow0 + r) * d.sld + c] = E<T>::cvt(pe[u]);
+          if (++c == d.cols) { c = 0; ++r; }
+        }
       }
     }
   }
@@ -659,18 +711,6 @@ __global__ __launch_bounds__(256) void k_bn_fwd_finalize(const float2* __restric
   coef[H + col] = fmaf(-meanf, alpha, beta[col]);
 }
 
-template <typename T>
-__device__ __forceinline__ void store4(T* dst, float a, float b, float c, float d) {
-  if constexpr (sizeof(T) == 2) {
-    uint2 pk;
-    pk.x = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
-    pk.y = (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16);
-    *(uint2*)dst = pk;
-  } else {
-    *(float4*)dst = make_float4(a, b, c, d);
-  }
-}
-
 // A = relu(y*alpha + beta') for rows < B, 0 for rows in [B, Bp)
 template <typename T>
 __global__ __launch_bounds__(256) void k_bn_fwd_apply2(const float* __restrict__ Y, int64_t ld,
@@ -702,6 +742,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float2* __restric
   if (col >= H) return;
   double s1 = 0.0, s2 = 0.0;
   const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
+#pragma unroll 8
   for (int ch = 0; ch < nch; ++ch) {
     const float2 p = part[(int64_t)ch * H + col];
     s1 += p.x;

@@ -76,7 +76,8 @@ enum {
  *   [0] sum of BCE elements           (ReconstructionLoss, loss_components.py:49-50)
  *   [1] sum of reconstructed p        (GeneAbundanceLoss before w*gamma; p >= 0 so |.| = id)
  *   [2] sum(1 + lv - mu^2 - exp(lv))  (KLDivergenceLoss before -0.5*beta)
- *   [3] sum |theta| over all params   (l1_regularization before lambda; gm2_grad_norm)
+ *   [3] sum |theta| over all params   (l1_regularization before lambda; gm2_grad_norm; only
+ *                                      when lambda != 0, else 0 — the reference returns 0 then)
  *   [4] total gradient L2 norm after L1 (clip_grad_norm_ total_norm; gm2_grad_norm)       */
 #define GM2_LOSS_SLOTS 8
 
