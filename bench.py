@@ -41,6 +41,25 @@ def decode_flops_per_genome(G, H, L):
     return 2 * (L * H + 2 * H * H + H * G)
 
 
+DEFAULTS = dict(batch=4096, genes=55039, hidden=1024, latent=64, precision="bf16")
+
+
+def pmc_traffic(a, kernel_prefix):
+    """HBM bytes per launch of `kernel_prefix` from the newest committed PMC summary
+    (profiles/rNN_pmc_traffic.json, written by tools_pmc.py from separate FETCH_SIZE / WRITE_SIZE
+    rocprofv3 passes of this same command). Only valid for the default workload; else None."""
+    import glob
+    if any(getattr(a, k) != v for k, v in DEFAULTS.items()):
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    rows = [r for r in json.load(open(files[-1]))["kernels"] if r["kernel"].startswith(kernel_prefix)]
+    if not rows:
+        return None, None
+    return rows[0]["traffic_bytes"], os.path.relpath(files[-1], ROOT)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -167,6 +186,7 @@ def main():
     k_avg_ms = k_ms / max(k_n, 1)
     k_flops = 2.0 * B * H * G
     achieved = k_flops / (k_avg_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(a, "k_gemm_recon_loss")
     out = {
         "metric": "strain-vectors/sec (train+sample), v0 preset, 1/2/4/8 MI355X vs host CPU",
         "value": round(value, 1), "unit": "strain-vectors/s", "n_gpus": world, "steps": a.steps,
@@ -182,7 +202,8 @@ def main():
                      "peak": PEAK_BF16_TFLOPS if prec == native.GM2_BF16 else PEAK_F32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / (PEAK_BF16_TFLOPS if prec == native.GM2_BF16
                                                                  else PEAK_F32_TFLOPS), 4),
-                     "traffic": None, "launch_ms": round(k_avg_ms, 4), "launches": k_n,
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "launch_ms": round(k_avg_ms, 4), "launches": k_n,
                      "flops_per_launch": k_flops},
     }
     if rank == 0 and not a.no_sample:
@@ -221,10 +242,12 @@ def sample_bench(a, dev):
     gps = n / dt
     kflops = 2.0 * chunk * H * G
     ach = kflops / (k_ms / max(k_n, 1) * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(a, "k_gemm_mask")
     return {"genomes_per_s": round(gps, 1), "preset": "v1", "genomes": n, "chunk": chunk, "dtype": "f32",
             "decode_tflops": round(gps * decode_flops_per_genome(G, H, L) / 1e12, 2),
             "roofline": {"bound": "mfma", "kernel": "k_gemm_mask<f32>", "achieved": round(ach, 2),
                          "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_TFLOPS, 4),
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "launch_ms": round(k_ms / max(k_n, 1), 4)}}
 
 

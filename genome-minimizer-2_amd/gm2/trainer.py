@@ -156,6 +156,21 @@ def _dist():
     return None
 
 
+def rank_slice(n, rank, world):
+    """Contiguous share [lo, hi) of a global batch of n rows for `rank` of `world` (SURVEY.md §8e:
+    one shuffled global permutation, identical on every rank, split contiguously)."""
+    return (n * rank) // world, (n * (rank + 1)) // world
+
+
+def reduce_batch(dist, grads, rec_row):
+    """The one data-path exchange of a DDP step: SUM of the per-rank gradients (the losses are
+    sum-reductions, so the sum over row shards is the full-batch gradient) and of the per-rank
+    loss sums [BCE, sum p, KL] of the loss record. L1, clipping and Adam follow on the reduced
+    values, identically on every rank."""
+    dist.all_reduce(grads)
+    dist.all_reduce(rec_row[:3])
+
+
 class VAETrainer:
     """trainer.py:84-189 on libgm2. `eps_rng`: 'device' draws the reparameterization noise with
     torch's generator on the model's device (what the reference does on a GPU: randn_like on a
@@ -217,7 +232,7 @@ class VAETrainer:
     def _rank_slice(self, n):
         dist = _dist()
         world, rank = (dist.get_world_size(), dist.get_rank()) if dist else (1, 0)
-        return (n * rank) // world, (n * (rank + 1)) // world
+        return rank_slice(n, rank, world)
 
     def _epoch_values(self, raw, pers, n_rows):
         epoch_losses = None
@@ -261,8 +276,7 @@ class VAETrainer:
             batch = native.make_batch(mat.data, mat.ld, rows[lo:hi], hi - lo, eps)
             native.train_fwd_bwd(ws, batch, model.params, self.grads, model.bn, scal[bi], rec[bi])
             if dist:
-                dist.all_reduce(self.grads)
-                dist.all_reduce(rec[bi, :3])
+                reduce_batch(dist, self.grads, rec[bi])
             native.grad_norm(ws, model.params, self.grads, scal[bi], rec[bi])
             native.adam_step(ws, model.params, self.grads, self.optimizer.exp_avg, self.optimizer.exp_avg_sq,
                              scal[bi])

@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Drop-in CLI for the hot path of genome-minimizer-2's main.py (main.py:62-147, :647-692).
+
+Implemented modes, same flags and file layout as the reference:
+  --mode training --preset v0..v3 [--epochs N]     run_single_experiment (main.py:449-493)
+  --mode sample --model-path ..._vK.pt --genes-path essential_gene_positions.pkl
+        [--num-samples N] [--sampling-mode default|focused] [--noise-level s]   run_sampling (:219-446)
+Both route through the gfx950 kernels of libgm2.so (gm2 package); there is no CPU path.
+
+Modes outside the MI355X hot path (explore, preprocess, minimizer, experiment, convert-samples;
+SURVEY.md §2) exit with code 2 and a message. Data files are looked up under the project root as in
+utils/directories.py:13-20 (default: $GM2_PROJECT_ROOT or the current directory; --project-root).
+Return codes follow main.py:647-692: 0 success, 1 failure.
+
+Additions (no reference equivalent): --precision bf16|f32 for the training GEMMs (sampling always
+decodes in exact fp32), --mask-dtype float64|uint8 for the saved masks (the reference writes float64
+via `.astype(float)`, main.py:369-371 / extras.py:200-201; uint8 keeps 1e6-genome runs in memory),
+--no-csv to skip the genes x samples CSV.
+"""
+import argparse
+import os
+import pickle
+import sys
+import traceback
+from pathlib import Path
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "genome-minimizer-2_amd"))
+
+MODES = ["training", "experiment", "minimizer", "explore", "preprocess", "sample", "convert-samples"]
+IMPLEMENTED = ("training", "sample")
+
+
+def parse_arguments(argv=None):
+    p = argparse.ArgumentParser(description="genome-minimizer-2 VAE hot path on MI355X")
+    p.add_argument("--mode", choices=MODES, default="training")
+    p.add_argument("--preset", choices=["v0", "v1", "v2", "v3"], default="v3")
+    p.add_argument("--epochs", type=int, default=None)
+    p.add_argument("--model-path", type=str)
+    p.add_argument("--genes-path", type=str)
+    p.add_argument("--output-file", type=str)
+    p.add_argument("--num-samples", type=int, default=1)
+    p.add_argument("--sampling-mode", choices=["default", "focused"], default="default")
+    p.add_argument("--noise-level", type=float, default=0.1)
+    p.add_argument("--project-root", type=str, default=os.environ.get("GM2_PROJECT_ROOT", os.getcwd()))
+    p.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
+    p.add_argument("--mask-dtype", choices=["float64", "uint8"], default="float64")
+    p.add_argument("--no-csv", action="store_true")
+    return p.parse_args(argv)
+
+
+def data_paths(root):
+    """utils/directories.py:13-20."""
+    d = os.path.join(root, "data")
+    return {"Main Dataset": os.path.join(d, "F4_complete_presence_absence.csv"),
+            "Phylogroups": os.path.join(d, "accessionID_phylogroup_BD.csv"),
+            "Essential Genes": os.path.join(d, "essential_genes.csv")}
+
+
+def check_data_availability(root):
+    """main.py:149-170."""
+    missing = [f"{k}: {v}" for k, v in data_paths(root).items() if not os.path.exists(v)]
+    if missing:
+        print("✗  Missing required data files:")
+        for m in missing:
+            print(f"   - {m}")
+        return False
+    print("✓ All required data files found")
+    return True
+
+
+def _precision(args):
+    from gm2 import native
+    return native.GM2_F32 if args.precision == "f32" else native.GM2_BF16
+
+
+def run_single_experiment(args):
+    """main.py:449-493: preset config, optional epoch override, run the experiment."""
+    from gm2.experiments import PRESETS, IntegratedExperimentRunner
+    config = PRESETS[args.preset]()
+    if args.epochs:
+        config.n_epochs = args.epochs
+    print(f"\n{'=' * 80}\nRunning {config.experiment_name} experiment")
+    print(f"Hidden dim: {config.hidden_dim}, Latent dim: {config.latent_dim}")
+    print(f"Epochs: {config.n_epochs}, Trainer: {config.trainer_version}\n{'=' * 80}")
+    paths = data_paths(args.project_root)
+    runner = IntegratedExperimentRunner(config, project_root=args.project_root, precision=_precision(args),
+                                        dataset_csv=paths["Main Dataset"], phylogroups_csv=paths["Phylogroups"])
+    results = runner.run_complete_experiment()
+    print(f"\n{config.experiment_name.upper()} COMPLETED!")
+    return results
+
+
+def detect_version(model_path):
+    """main.py:292-304: preset from the checkpoint file name."""
+    name = Path(model_path).name.lower()
+    for v in ("v0", "v1", "v2", "v3"):
+        if v in name:
+            return v
+    return None
+
+
+def focused_samples(model, latent_dim, num_samples, noise_level, device):
+    """main.py:351-370: 100 default samples, the one with fewest genes, then its output-space
+    nearest sample's z (the same index), decoded again under z* + noise_level * N(0, I)."""
+    import numpy as np
+    import torch
+    from gm2.extras import sample_from_model
+    binary_temp, cont_temp, z_temp = sample_from_model(model, latent_dim, 100, device)
+    min_ones_index = np.argmin(binary_temp.sum(axis=1))
+    dist = np.linalg.norm(cont_temp - cont_temp[min_ones_index], axis=1)
+    closest = np.argmin(dist)
+    z_star = z_temp[closest].unsqueeze(0)
+    noise = torch.randn(num_samples, latent_dim, device=device) * noise_level
+    z = z_star + noise
+    mask, _ = model.decode_mask(z)
+    return mask, z
+
+
+def run_sampling(args):
+    """main.py:219-446 without the plots / PCA (out of scope): load the checkpoint, decode in fp32,
+    threshold, count essential genes, save masks (.npy) and the genes x samples CSV."""
+    import numpy as np
+    import torch
+    from gm2.data import load_and_validate_data
+    from gm2.experiments import PRESETS
+    from gm2.extras import count_essential_genes, load_model, sample_from_model, write_samples_to_dataframe
+
+    if not args.model_path:
+        print("✗ Model path required for sampling mode")
+        return False
+    if not os.path.exists(args.model_path):
+        print(f"✗ Model file not found: {args.model_path}")
+        return False
+    if not args.genes_path or not os.path.exists(args.genes_path):
+        print(f"✗ Model file not found: {args.genes_path}. Run preprocessing first.")
+        return False
+    paths = data_paths(args.project_root)
+    _, merged, _ = load_and_validate_data(paths["Main Dataset"], paths["Phylogroups"])
+    all_genes = merged.columns[:-1]
+    input_dim = len(all_genes)
+    print(f"Detected input dimension: {input_dim}")
+    with open(args.genes_path, "rb") as f:
+        # the user's own preprocessing output, read the way the reference reads it (main.py:273-274)
+        essential_gene_positions = pickle.load(f)
+    version = detect_version(args.model_path)
+    if version is None:
+        print("✗ Could not detect version")
+        return False
+    config = PRESETS[version]()
+    out_dir = Path(args.project_root) / "models" / f"{version}_model" / "sampling_results"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    device = torch.device("cuda", torch.cuda.current_device())
+    model = load_model(input_dim, config.hidden_dim, config.latent_dim, args.model_path)
+    print(f"- Architecture: {input_dim} -> {config.hidden_dim} -> {config.latent_dim}")
+    print(f"- Samples: {args.num_samples}\n- Mode: {args.sampling_mode}\n- Output: {out_dir}")
+    if args.sampling_mode == "default":
+        binary, _, _ = sample_from_model(model, config.latent_dim, args.num_samples, device,
+                                         binary_dtype=np.uint8, return_probs=False)
+    else:
+        mask, _ = focused_samples(model, config.latent_dim, args.num_samples, args.noise_level, device)
+        binary = mask.cpu().numpy()
+    sizes = binary.sum(axis=1, dtype=np.int64)
+    ess = count_essential_genes(binary, essential_gene_positions)
+    print(f"\n✓ Sampling Results:\n- Generated samples: {binary.shape[0]}")
+    print(f"- Median genome size: {np.median(sizes):.0f} genes")
+    print(f"- Genome size range: {np.min(sizes):.0f} - {np.max(sizes):.0f}")
+    print(f"- Median essential genes: {np.median(ess):.0f}")
+    print(f"- Essential range: {np.min(ess):.0f} - {np.max(ess):.0f}")
+    out = binary.astype(np.float64) if args.mask_dtype == "float64" else binary
+    np.save(out_dir / f"{config.trainer_version}_binary_samples_{args.sampling_mode}.npy", out)
+    if not args.no_csv:
+        write_samples_to_dataframe(out, all_genes, f"{out_dir}/{config.trainer_version}_data_full_samples_df.csv")
+    print(f"\n✓ SAMPLING COMPLETE!\n- Results saved to: {out_dir}")
+    return True
+
+
+def main(argv=None):
+    args = parse_arguments(argv)
+    print(f"\nRunning in {args.mode} mode (MI355X / gfx950 build)")
+    if args.mode not in IMPLEMENTED:
+        print(f"✗ --mode {args.mode} is outside the MI355X hot path of this build (SURVEY.md §2); "
+              "use the reference for it")
+        return 2
+    if not check_data_availability(args.project_root):
+        print("\n✗ Cannot proceed without required data files")
+        return 1
+    try:
+        if args.mode == "sample":
+            return 0 if run_sampling(args) else 1
+        results = run_single_experiment(args)
+        if results is None:
+            return 1
+    except KeyboardInterrupt:
+        print("\n\n✗ Process interrupted by user")
+        return 1
+    except Exception as e:  # main.py:686-692
+        print(f"\n✗ Unexpected error: {e}")
+        traceback.print_exc()
+        return 1
+    print("\n" + "=" * 80 + "\nPROCESS COMPLETED!\n" + "=" * 80)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

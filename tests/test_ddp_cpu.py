@@ -1,0 +1,104 @@
+"""World-size-2 data-parallel step on CPU (gloo): the host side of the DDP path of gm2.trainer
+(rank_slice + reduce_batch, then clip + Adam on the reduced gradient) with the oracle standing in
+for the per-rank fused kernels. Checks that the shards partition every batch, that the reduced
+gradient and loss sums equal the sum of the per-shard values, and that both ranks end the step with
+bit-identical parameters (the property that lets every rank keep a full replica)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from gm2.trainer import rank_slice, reduce_batch
+from oracle import vae_oracle as O
+
+G, H, L, B = 40, 16, 4, 27
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _shard_step(P, S, x, eps, lo, hi):
+    g = O.manual_grads(P, S, x[lo:hi], eps[lo:hi], 0.7, 0.0, 0.0)
+    recon, mu, lv = O.forward(P, {k: v.clone() for k, v in S.items()}, x[lo:hi], eps[lo:hi], train=True)
+    rec = torch.zeros(8, dtype=torch.float64)
+    rec[0] = torch.nn.functional.binary_cross_entropy(recon, x[lo:hi], reduction="sum").double()
+    rec[1] = recon.sum().double()
+    rec[2] = torch.sum(1 + lv - mu.pow(2) - lv.exp()).double()
+    return g, rec
+
+
+def _inputs():
+    torch.manual_seed(3)
+    P = O.init_params(G, H, L)
+    S = O.init_bn_state(H)
+    x = (torch.rand(B, G) < 0.4).float()
+    eps = torch.randn(B, L)
+    return P, S, x, eps
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    P, S, x, eps = _inputs()
+    lo, hi = rank_slice(B, rank, world)
+    g, rec = _shard_step(P, S, x, eps, lo, hi)
+    names = list(P.keys())
+    flat = torch.cat([g[n].reshape(-1) for n in names])
+    reduce_batch(dist, flat, rec)
+    # unflatten, clip on the reduced gradient, Adam: identical on every rank
+    red, off = {}, 0
+    for n in names:
+        k = P[n].numel()
+        red[n] = flat[off:off + k].view_as(P[n]).clone()
+        off += k
+    O.clip_grads(red, 1.0)
+    O.adam_step(P, red, O.AdamState())
+    params = torch.cat([P[n].reshape(-1) for n in names])
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), grad=flat.numpy(), rec=rec.numpy(), params=params.numpy(),
+             lo=lo, hi=hi)
+    dist.destroy_process_group()
+
+
+def test_rank_slice_partitions():
+    for n in (1, 2, 7, 32, 4096, 4097):
+        for world in (1, 2, 3, 8):
+            spans = [rank_slice(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def test_two_rank_step(tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = np.load(tmp_path / "r0.npz"), np.load(tmp_path / "r1.npz")
+    assert int(r0["hi"]) == int(r1["lo"]) and int(r0["lo"]) == 0 and int(r1["hi"]) == B
+    np.testing.assert_array_equal(r0["params"], r1["params"])
+    np.testing.assert_array_equal(r0["grad"], r1["grad"])
+    # reduced values == sum of the per-shard values computed in one process
+    P, S, x, eps = _inputs()
+    names = list(P.keys())
+    exp_g, exp_rec = 0, 0
+    for lo, hi in (rank_slice(B, 0, 2), rank_slice(B, 1, 2)):
+        g, rec = _shard_step(P, S, x, eps, lo, hi)
+        exp_g = exp_g + torch.cat([g[n].reshape(-1) for n in names]).numpy()
+        exp_rec = exp_rec + rec.numpy()
+    np.testing.assert_allclose(r0["grad"], exp_g, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(r0["rec"][:3], exp_rec[:3], rtol=1e-12)
+
+
+@pytest.mark.parametrize("world", [2])
+def test_main_cli_modes_without_gpu(world, tmp_path):
+    import main as cli
+    assert cli.main(["--mode", "minimizer"]) == 2
+    assert cli.main(["--mode", "explore"]) == 2
+    assert cli.main(["--mode", "training", "--project-root", str(tmp_path)]) == 1  # no data files
+    assert cli.detect_version("/x/saved_VAE_v2.pt") == "v2" and cli.detect_version("model.pt") is None

@@ -1,0 +1,39 @@
+"""Diagnostic: GPU (fp32) vs oracle parameter drift after 1..NEP epochs of a preset run."""
+import sys
+import numpy as np
+import torch
+sys.path[:0] = ['.', 'genome-minimizer-2_amd', 'tests']
+from oracle import vae_oracle as O
+from gm2 import native
+from gm2.data import ResidentMatrix, StrainLoader
+from gm2.experiments import PRESETS, run_preset
+from gm2.model import VAE
+from gm2.trainer import Adam, StepLR
+from test_gpu_trainer import _no_constant_columns, _prebn_bias_names
+
+G, H, L, N, BS = 200, 128, 16, 150, 32
+x = _no_constant_columns(N, G, 11)
+tr_idx, va_idx = np.arange(0, 96), np.arange(96, 126)
+preset = sys.argv[1] if len(sys.argv) > 1 else "v1"
+for nep in (1, 2, 3):
+    seed = 300 + int(preset[1])
+    torch.manual_seed(seed)
+    P = O.init_params(G, H, L); S = O.init_bn_state(H)
+    xt = torch.tensor(x, dtype=torch.float32)
+    o_tr, o_va, _ = O.run_preset(P, S, O.PRESETS[preset], nep, xt[tr_idx], xt[va_idx], BS)
+    torch.manual_seed(seed)
+    m = VAE(G, H, L, precision=native.GM2_F32)
+    mat = ResidentMatrix(x)
+    cfg = PRESETS[preset](); cfg.n_epochs, cfg.hidden_dim, cfg.latent_dim = nep, H, L
+    opt = Adam(m, lr=cfg.learning_rate); sch = StepLR(opt, 20, 0.5)
+    from gm2 import trainer as T
+    tr, va, _ = run_preset(cfg, m, opt, sch, StrainLoader(mat, tr_idx, BS, True), StrainLoader(mat, va_idx, BS, False), eps_rng="cpu")
+    sd = m.state_dict()
+    rows = []
+    for k, v in P.items():
+        d = (sd[k].cpu() - v).abs()
+        rows.append((float(d.max()), int((d > 1e-5).sum()), k))
+    rows.sort(reverse=True)
+    print(f"{preset} nep={nep} tr {np.array(tr)-np.array(o_tr)} va {np.array(va)-np.array(o_va)}")
+    for r in rows[:8]:
+        print("   ", r)
