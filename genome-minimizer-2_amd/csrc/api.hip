@@ -585,9 +585,11 @@ int gm2_gemm(int prec, int pk, int qk, const void* P, int64_t ldp, const void* Q
       using T = decltype(tag);
       GemmArgs<T> g{(const T*)P, ldp, (const T*)Q, ldq, (int)M, (int)N, (int)K, (int)round_up(M, kTile),
                     (int)round_up(N, kTile), 0, pk ? 1 : 0, qk ? 1 : 0};
-      if (splits <= 1) {
+      if (splits < 0) splits = plan_gemm(g).splits;  // the hot path's own tile / split-K plan
+      if (splits == 0 || splits == 1) {
         launch_gemm_store<T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, (hipStream_t)stream);
       } else {
+        if (!slab_ws) throw Gm2Error("gemm: split-K needs slab_ws");
         const int S = launch_gemm_store<T>(g, splits, slab_ws, nullptr, 0, ldc, (int64_t)M * ldc, nullptr,
                                            (hipStream_t)stream);
         // sum the slabs column-block-wise: treat [S][M*ldc] as rows

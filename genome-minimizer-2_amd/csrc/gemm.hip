@@ -21,6 +21,8 @@
 #include "gm2_common.hpp"
 #include "gm2_kernels.hpp"
 
+#include <cstdlib>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -216,10 +218,174 @@ __device__ __forceinline__ void mainloop(const T* __restrict__ P, int64_t ldp, c
 }
 
 // ---------------------------------------------------------------------------------------------
+// Ping-pong main loop for the 256x256 bf16 tile (8 waves = two groups of four, one wave of each
+// group per SIMD). Each K-tile (64 k) is consumed in 4 phases, one 64x32 quadrant of each wave's
+// 128x64 sub-tile per phase (16 MFMAs): (a0,b0) (a0,b1) (a1,b0) (a1,b1), where a = which 64 of
+// the wave's 128 rows and b = which 32 of its 64 columns. The stage of a K-tile is split into the
+// four matching half-tiles, each its own 16 KB LDS region of the tile's buffer:
+//   A_a : the rows {g*128 + a*64 + 0..63 : g = 0,1}   (both groups' a-halves)
+//   B_b : the cols {w*64 + b*32 + 0..31 : w = 0..3}
+// Phase p of tile t: [L] ds_read this quadrant's new fragments from buffer t&1, [G] issue one
+// half-tile of tile t+1 into buffer (t+1)&1 (A0, B0, B1, A1 at p = 0..3), [W] counted vmcnt,
+// barrier, MFMAs, barrier. Group 1 runs one barrier behind group 0, so on every SIMD one wave
+// computes while the other reads LDS and issues loads (MI355X_MICROARCH.md "Two waves per SIMD").
+// Ordering (barrier instances counted globally, phase n = 4t+p):
+//  * RAW: a half-tile issued at phase n_i is covered by every wave's vmcnt at phase n_w and read
+//    at phase >= n_w + 1: A0(t+1), B0(t+1) retired at 4t+3, read at 4(t+1); B1 issued 4t+2,
+//    retired 4t+4, read 4t+5; A1 issued 4t+3, retired 4t+5, read 4t+6. Steady-state wait
+//    vmcnt(4) = two later half-tiles x 2 loads per thread; none at p = 2.
+//  * WAR: a region of buffer (t+1)&1 is restaged >= 4 phases after its last read in tile t-1
+//    (the rule needs >= 2).
+// ---------------------------------------------------------------------------------------------
+namespace pp {
+constexpr int REGION = 128 * 128;  // bytes of one half-tile region (128 rows x 128 B, or 64 k x 256 B)
+constexpr int BUF = 4 * REGION;    // one K-tile: A0, A1, B0, B1
+__device__ __forceinline__ int a_row(int r, int a) { return (r >> 6) * 128 + a * 64 + (r & 63); }
+__device__ __forceinline__ int b_row(int r, int b) { return (r >> 5) * 64 + b * 32 + (r & 31); }
+
+// one half-tile: 1024 16-B chunks, 2 per thread (lane-linear LDS destination, swizzled source)
+template <bool KMAJ, bool ISA>
+__device__ __forceinline__ void stage_half(const bf16_t* __restrict__ P, int64_t ld, int base, int half, int k0,
+                                           char* region, int tid) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = j * 512 + tid;
+    const bf16_t* src;
+    if constexpr (KMAJ) {
+      const int row = i >> 3;
+      const int c = (i & 7) ^ ((row >> 1) & 7);
+      const int g = ISA ? a_row(row, half) : b_row(row, half);
+      src = P + (int64_t)(base + g) * ld + k0 + c * 8;
+    } else {
+      const int k = i >> 4;
+      const int e = ((i & 15) ^ swz_mn(k)) * 8;
+      const int g = ISA ? a_row(e, half) : b_row(e, half);
+      src = P + (int64_t)(k0 + k) * ld + base + g;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(region + (j * 512 + (tid & ~63)) * 16), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+}  // namespace pp
+
+template <bool AK, bool BK>
+__device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_t ldp, const bf16_t* __restrict__ Q,
+                                            int64_t ldq, int m0, int n0, int kbeg, int nk, char* smem,
+                                            f32x4 (&acc)[8][4]) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // wave-uniform in an SGPR: the stagger barriers below must be branched around, not exec-masked
+  const int wm = __builtin_amdgcn_readfirstlane(wid >> 2), wn = wid & 3;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk <= 0) return;
+  // half-tile h (0 = A0, 1 = B0, 2 = B1, 3 = A1) of K-tile t -> its region
+  auto region = [&](int t, int h) -> char* {
+    const int off = h == 0 ? 0 : h == 3 ? 1 : h + 1;  // A0 0, A1 1, B0 2, B1 3
+    return smem + (t & 1) * pp::BUF + off * pp::REGION;
+  };
+  auto issue = [&](int t, int h) {
+    const int k0 = kbeg + t * 64;
+    char* r = region(t, h);
+    if (h == 0 || h == 3) pp::stage_half<AK, true>(P, ldp, m0, h == 0 ? 0 : 1, k0, r, tid);
+    else pp::stage_half<BK, false>(Q, ldq, n0, h == 1 ? 0 : 1, k0, r, tid);
+  };
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  auto read_a = [&](int t, int a) {
+    const char* r = region(t, a == 0 ? 0 : 3);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fa[mi][s] = frag_bf16<AK, 128>(r, wm * 64 + mi * 16, s, lane);
+  };
+  auto read_b = [&](int t, int b, bf16x8 (&fb)[2][2]) {
+    const char* r = region(t, b == 0 ? 1 : 2);
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fb[ni][s] = frag_bf16<BK, 128>(r, wn * 32 + ni * 16, s, lane);
+  };
+  auto mma = [&](int a, int b, const bf16x8 (&fb)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          acc[a * 4 + mi][b * 2 + ni] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi][s], fb[ni][s], acc[a * 4 + mi][b * 2 + ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // prologue: all four half-tiles of tile 0; A0, B0 retired before the first reads
+#pragma unroll
+  for (int h = 0; h < 4; ++h) issue(0, h);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  pp::barrier();
+  if (wm == 1) pp::barrier();  // stagger: group 1 one barrier behind
+  for (int t = 0; t < nk; ++t) {
+    const bool more = t + 1 < nk;
+    // phase 0: (a0, b0)
+    read_a(t, 0);
+    read_b(t, 0, fb0);
+    if (more) {
+      issue(t + 1, 0);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires B1(t)
+    } else {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    }
+    pp::barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0, 0, fb0);
+    pp::barrier();
+    // phase 1: (a0, b1)
+    read_b(t, 1, fb1);
+    if (more) {
+      issue(t + 1, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires A1(t)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pp::barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0, 1, fb1);
+    pp::barrier();
+    // phase 2: (a1, b0)
+    read_a(t, 1);
+    if (more) issue(t + 1, 2);
+    pp::barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(1, 0, fb0);
+    pp::barrier();
+    // phase 3: (a1, b1)
+    if (more) {
+      issue(t + 1, 3);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires A0(t+1), B0(t+1)
+    }
+    pp::barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    mma(1, 1, fb1);
+    pp::barrier();
+  }
+  if (wm == 0) pp::barrier();  // re-align the groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Epilogue 1: fp32 store. Rows m < msplit go to C0, rows >= msplit to C1 (row m - msplit); the
 // split-K slice z writes slab z (C0 + z*slab). Optional per-column bias.
 // ---------------------------------------------------------------------------------------------
-template <class C, typename T, bool AK, bool BK>
+template <class C, typename T, bool AK, bool BK, bool PP>
 __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __restrict__ C0, float* __restrict__ C1,
                                                     int msplit, int64_t ldc, int64_t slab,
                                                     const float* __restrict__ bias) {
@@ -229,7 +395,10 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
   const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = (kend - kbeg) / E<T>::KT;
   f32x4 acc[C::FM][C::FN];
-  mainloop<C, T, AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
+  if constexpr (PP)
+    mainloop_pp<AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
+  else
+    mainloop<C, T, AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   float* Cz = C0 + (int64_t)tl.split * slab;
   // Stage one wave-row band (WTM x BN fp32) at a time through the (now free) staging LDS, then
@@ -292,7 +461,7 @@ __device__ __forceinline__ void recon_elem(float l, float x, float wgam, float& 
   }
 }
 
-template <class C, typename T>
+template <class C, typename T, bool PP>
 __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const float* __restrict__ bias,
                                                          const uint32_t* __restrict__ xbits, int64_t ldxb,
                                                          int with_grad, const float* __restrict__ scal,
@@ -305,7 +474,10 @@ __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const 
   const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
   const TileXY tl = tile_of<C>(tm, tn);
   f32x4 acc[C::FM][C::FN];
-  mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+  if constexpr (PP)
+    mainloop_pp<true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+  else
+    mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   const int q = lane >> 4;
   const float wgam = scal[kScalWGamma];
@@ -549,18 +721,37 @@ static bool use_big(const GemmArgs<T>& g) {
   return plan_gemm(g).tile == 256;
 }
 
-template <class C, typename T, bool AK, bool BK>
-static void store_launch(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
-                         const float* bias, hipStream_t s) {
+// GM2_GEMM_PP=1 selects the ping-pong main loop for the 256x256 bf16 tiles (experimental until
+// measured on the GPU; the default is the two-stage loop)
+static bool pp_enabled() {
+  static const int on = [] {
+    const char* e = std::getenv("GM2_GEMM_PP");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return on != 0;
+}
+
+template <class C, typename T, bool AK, bool BK, bool PP>
+static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
+                           const float* bias, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)k_gemm_store<C, T, AK, BK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)k_gemm_store<C, T, AK, BK, PP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             C::LDS) != hipSuccess)
       throw Gm2Error("hipFuncSetAttribute(store)");
     attr = true;
   }
-  hipLaunchKernelGGL((k_gemm_store<C, T, AK, BK>), dim3(tiles), dim3(C::NT), C::LDS, s, a, C0, C1 ? C1 : C0,
+  hipLaunchKernelGGL((k_gemm_store<C, T, AK, BK, PP>), dim3(tiles), dim3(C::NT), C::LDS, s, a, C0, C1 ? C1 : C0,
                      C1 ? msplit : (1 << 30), ldc, slab, bias);
+}
+
+template <class C, typename T, bool AK, bool BK>
+static void store_launch(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
+                         const float* bias, hipStream_t s) {
+  if constexpr (std::is_same_v<C, Big> && sizeof(T) == 2) {
+    if (pp_enabled()) return store_launch_k<C, T, AK, BK, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, s);
+  }
+  store_launch_k<C, T, AK, BK, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, s);
 }
 
 template <class C, typename T>
@@ -608,22 +799,34 @@ int gemm_recon_row_tiles(const GemmArgs<T>& g) {
   return g.Mp / (recon_big(g) ? 256 : 128);
 }
 
-template <class C, typename T>
-static void recon_impl(const GemmArgs<T>& g, const float* bias, const uint32_t* X, int64_t ldx, int with_grad,
-                       const float* scal, T* dL, int64_t ldd, T* dLT, int64_t lddt, float* loss_part, float* colpart,
-                       int64_t ldcol, hipStream_t s) {
+template <class C, typename T, bool PP>
+static void recon_impl_k(const GemmArgs<T>& g, const float* bias, const uint32_t* X, int64_t ldx, int with_grad,
+                         const float* scal, T* dL, int64_t ldd, T* dLT, int64_t lddt, float* loss_part, float* colpart,
+                         int64_t ldcol, hipStream_t s) {
   check_gemm(g, C::BM);
   constexpr int lds = std::max<int>(C::LDS, std::max(C::BM * (C::BN + 8), C::BN * (C::BM + 8)) * (int)sizeof(T));
   static_assert(lds <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)k_gemm_recon_loss<C, T>, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
-        hipSuccess)
+    if (hipFuncSetAttribute((const void*)k_gemm_recon_loss<C, T, PP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            lds) != hipSuccess)
       throw Gm2Error("hipFuncSetAttribute(recon)");
     attr = true;
   }
-  hipLaunchKernelGGL((k_gemm_recon_loss<C, T>), dim3((g.Mp / C::BM) * (g.Np / C::BN)), dim3(C::NT), lds, s, g, bias,
-                     X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol);
+  hipLaunchKernelGGL((k_gemm_recon_loss<C, T, PP>), dim3((g.Mp / C::BM) * (g.Np / C::BN)), dim3(C::NT), lds, s, g,
+                     bias, X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol);
+}
+
+template <class C, typename T>
+static void recon_impl(const GemmArgs<T>& g, const float* bias, const uint32_t* X, int64_t ldx, int with_grad,
+                       const float* scal, T* dL, int64_t ldd, T* dLT, int64_t lddt, float* loss_part, float* colpart,
+                       int64_t ldcol, hipStream_t s) {
+  if constexpr (std::is_same_v<C, Big> && sizeof(T) == 2) {
+    if (pp_enabled())
+      return recon_impl_k<C, T, true>(g, bias, X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol,
+                                      s);
+  }
+  recon_impl_k<C, T, false>(g, bias, X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol, s);
 }
 
 // the fp32 parity path stays on the 128-tile (a 256-row fp32 dL image would not fit the LDS)

@@ -32,7 +32,10 @@ if torch.cuda.is_available():
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
 @pytest.mark.parametrize("prec", ["f32", "bf16"])
 @pytest.mark.parametrize("M,N,K,splits", [(128, 128, 64, 1), (200, 300, 192, 1), (256, 1024, 1024, 1),
-                                          (300, 256, 4096, 4), (1000, 130, 320, 1), (2048, 1024, 512, 1)])
+                                          (300, 256, 4096, 4), (1000, 130, 320, 1), (2048, 1024, 512, 1),
+                                          # 256x256 ping-pong tiles: >= 256 tiles (nk = 1, 3), and the
+                                          # long-K plan (big tiles + 8 split-K slices)
+                                          (4000, 4096, 64, 1), (4096, 4000, 192, 1), (512, 512, 8192, -1)])
 def test_gemm(prec, layout, M, N, K, splits):
     """C = P.Q^T with each operand K-major ([rows][K]) or MN-major ([K][rows], read through
     ds_read_b64_tr_b16 / ds_read_b32): nt = both K-major (forward), nn = Q MN-major (input
@@ -50,7 +53,7 @@ def test_gemm(prec, layout, M, N, K, splits):
     pr = native.GM2_BF16 if prec == "bf16" else native.GM2_F32
     Pd, Qd = Ps.to(dt).cuda(), Qs.to(dt).cuda()
     C = torch.full((M, N), float("nan"), device="cuda")
-    slab = torch.empty(splits * M * N + 4, device="cuda") if splits > 1 else None
+    slab = torch.empty(max(splits, 8) * M * N + 4, device="cuda") if splits != 1 else None
     native.gemm(pr, Pd, Ps.shape[1], Qd, Qs.shape[1], C, N, M, N, K, splits, slab, pk, qk)
     ref = (P[:M].double() @ Q[:N].double().T)
     err = (C.cpu().double() - ref).abs().max().item()
