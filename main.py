@@ -7,8 +7,10 @@ Implemented modes, same flags and file layout as the reference:
         [--num-samples N] [--sampling-mode default|focused] [--noise-level s]   run_sampling (:219-446)
 Both route through the gfx950 kernels of libgm2.so (gm2 package); there is no CPU path.
 
-Modes outside the MI355X hot path (explore, preprocess, minimizer, experiment, convert-samples;
-SURVEY.md §2) exit with code 2 and a message. Data files are looked up under the project root as in
+  --mode convert-samples --genes-path masks.npy [--output-file ids.npy]   run_binary_converter (:617-645)
+        (host-side; the consumer of the sampled masks, explore_data/binary_converter.py)
+Modes outside the MI355X hot path (explore, preprocess, minimizer, experiment)
+exit with code 2 and a message. Data files are looked up under the project root as in
 utils/directories.py:13-20 (default: $GM2_PROJECT_ROOT or the current directory; --project-root).
 Return codes follow main.py:647-692: 0 success, 1 failure.
 
@@ -28,7 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "genome-minimizer-2_amd"))
 
 MODES = ["training", "experiment", "minimizer", "explore", "preprocess", "sample", "convert-samples"]
-IMPLEMENTED = ("training", "sample")
+IMPLEMENTED = ("training", "sample", "convert-samples")
 
 
 def parse_arguments(argv=None):
@@ -175,6 +177,28 @@ def run_sampling(args):
     return True
 
 
+def run_binary_converter(args):
+    """main.py:617-645: gene columns from the dataset CSV, masks -> gene-id lists, then the
+    essential-gene fill (explore_data/binary_converter.py)."""
+    import pandas as pd
+    from gm2.binary_converter import check_essential_genes, load_files, masks_to_gene_lists
+    if not args.genes_path:
+        print("✗ --genes-path is required in convert-samples mode (input masks .npy)")
+        return False
+    if not os.path.exists(args.genes_path):
+        print(f"✗ Input masks file not found: {args.genes_path}")
+        return False
+    out_path = args.output_file or "seq_out.npy"
+    paths = data_paths(args.project_root)
+    large = pd.read_csv(paths["Main Dataset"], index_col=0)
+    cols = large.drop(index=["Lineage"], errors="ignore").transpose().columns
+    masks_to_gene_lists(masks_npy_path=args.genes_path, cols=cols, out_ids_npy=out_path)
+    essential_set, id_lists = load_files(paths["Essential Genes"], out_path)
+    filled = check_essential_genes(essential_set, id_lists, out_path)
+    print(f"✓ Binary conversion complete\n- Gene lists: {out_path}\n- Gene lists (essentials filled): {filled}")
+    return True
+
+
 def main(argv=None):
     args = parse_arguments(argv)
     print(f"\nRunning in {args.mode} mode (MI355X / gfx950 build)")
@@ -182,12 +206,14 @@ def main(argv=None):
         print(f"✗ --mode {args.mode} is outside the MI355X hot path of this build (SURVEY.md §2); "
               "use the reference for it")
         return 2
-    if not check_data_availability(args.project_root):
+    if args.mode != "convert-samples" and not check_data_availability(args.project_root):
         print("\n✗ Cannot proceed without required data files")
         return 1
     try:
         if args.mode == "sample":
             return 0 if run_sampling(args) else 1
+        if args.mode == "convert-samples":
+            return 0 if run_binary_converter(args) else 1
         results = run_single_experiment(args)
         if results is None:
             return 1
