@@ -52,10 +52,12 @@ def get_latent_variables(model, data_loader, device=None):
 
 def count_essential_genes(binary_generated_samples, essential_gene_positions):
     """Per sample, how many essential genes are present: a gene counts when ANY of its column
-    positions (< G) is non-zero (extras.py:65-85), vectorised over samples."""
+    positions (< G; negative positions index from the end, as numpy does there) is non-zero after
+    `astype(int)` (extras.py:65-85), vectorised over samples instead of the per-sample loop."""
     b = np.asarray(binary_generated_samples)
     G = b.shape[1]
-    present = b.astype(bool) if b.dtype != bool else b
+    # the reference tests `astype(int) != 0` (truncation: 0.7 counts as absent)
+    present = b if b.dtype == bool else (b != 0 if b.dtype.kind in "iu" else b.astype(int) != 0)
     counts = np.zeros(b.shape[0], dtype=int)
     for _, positions in essential_gene_positions.items():
         cols = [p for p in positions if p < G]

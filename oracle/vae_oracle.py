@@ -450,3 +450,20 @@ def decode_logits64(P, S, z):
         for i in range(3):
             h = _block(P64, S64, f"decoder.{3*i}", f"decoder.{3*i+1}", h, False)
         return F.linear(h, P64["decoder.9.weight"], P64["decoder.9.bias"])
+
+
+# ------------------------------------------------------------------------------------------
+# count_essential_genes (utils/extras.py:49-87): the reference's per-sample, per-gene loop
+# ------------------------------------------------------------------------------------------
+def count_essential_genes_loop(binary_generated_samples, essential_gene_positions):
+    b = np.asarray(binary_generated_samples).astype(int)
+    out = np.zeros(b.shape[0], dtype=int)
+    for i in range(b.shape[0]):
+        n = 0
+        for _, positions in essential_gene_positions.items():
+            for pos in positions:
+                if pos < b.shape[1] and b[i, pos] != 0:
+                    n += 1
+                    break
+        out[i] = n
+    return out

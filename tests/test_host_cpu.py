@@ -169,3 +169,17 @@ def test_steplr():
         lrs.append(s.get_last_lr()[0])
         s.step()
     assert lrs[0] == 1e-3 and lrs[19] == 1e-3 and lrs[20] == 5e-4 and lrs[40] == 2.5e-4
+
+
+def test_count_essential_genes_matches_reference_loop():
+    """Vectorised count_essential_genes == the reference's loop (oracle restatement of
+    extras.py:49-87) on 0/1, uint8, bool and fractional masks, with single, multiple, empty,
+    out-of-range and negative positions."""
+    from gm2.extras import count_essential_genes
+    from oracle import vae_oracle as O
+    rng = np.random.Generator(np.random.PCG64(4))
+    G = 40
+    pos = {"a": [3], "b": [5, 39], "c": [], "d": [41], "e": [41, 7], "f": [-1], "g": [0, 1, 2]}
+    x = (rng.random((25, G)) < 0.3)
+    for m in (x.astype(np.float64), x.astype(np.uint8), x, rng.random((25, G)) * 1.5):
+        np.testing.assert_array_equal(count_essential_genes(m, pos), O.count_essential_genes_loop(m, pos))
