@@ -46,7 +46,7 @@ DEFAULTS = dict(batch=4096, genes=55039, hidden=1024, latent=64, precision="bf16
 
 def pmc_traffic(a, kernel_prefix):
     """HBM bytes per launch of `kernel_prefix` from the newest committed PMC summary
-    (profiles/rNN_pmc_traffic.json, written by tools_pmc.py from separate FETCH_SIZE / WRITE_SIZE
+    (profiles/rNN_pmc_traffic.json, written by tools/pmc.py from separate FETCH_SIZE / WRITE_SIZE
     rocprofv3 passes of this same command). Only valid for the default workload; else None."""
     import glob
     if any(getattr(a, k) != v for k, v in DEFAULTS.items()):
@@ -74,35 +74,95 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sample", action="store_true")
     ap.add_argument("--sample-genomes", type=int, default=262144)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--no-f32-line", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(G, H, L, budget_s):
-    """The oracle (reference algorithm, torch-CPU fp32, autograd) on a bounded sample: v0 preset,
-    one 512-row batch of the same G x H x L model per step, timed for ~budget_s seconds."""
+def cpu_baseline(x_u8, G, H, L, budget_s, batch):
+    """The oracle (reference algorithm: torch-CPU fp32 autograd, the reference's op order) on the
+    box's host cores, SAME workload as the GPU line: v0 preset, batch `batch` rows of the same
+    synthetic pan-genome matrix, fwd + bwd + clip + Adam per step; warm-up step, then as many
+    timed steps as fit `budget_s` (at least one)."""
     sys.path.insert(0, ROOT)
     from oracle import vae_oracle as O
     threads = torch.get_num_threads()
-    B = 512
     torch.manual_seed(0)
     P = O.init_params(G, H, L)
     S = O.init_bn_state(H)
-    rng = np.random.Generator(np.random.PCG64(1))
-    x = torch.tensor((rng.random((B, G), dtype=np.float32) < 0.3).astype(np.float32))
-    ls = O.LossState(O.PRESETS["v0"], 10)
+    g = torch.Generator().manual_seed(7)
+    n_rows = x_u8.shape[0]
+
+    def xb():
+        idx = torch.randperm(n_rows, generator=g)[:batch].numpy()
+        return torch.from_numpy(x_u8[idx].astype(np.float32))
+    ls = O.LossState(O.PRESETS["v0"], 10000)
     opt = O.AdamState()
+    x = xb()
     t0 = time.perf_counter()
-    O.train_step(P, S, ls, opt, x, torch.randn(B, L), 0)  # warm-up
+    O.train_step(P, S, ls, opt, x, torch.randn(batch, L), 0)  # warm-up
     first = time.perf_counter() - t0
-    n = max(1, min(20, int(budget_s / max(first, 1e-3))))
+    n = max(1, min(50, int(budget_s / max(first, 1e-3))))
+    xs = [xb() for _ in range(n)]
     t0 = time.perf_counter()
-    for _ in range(n):
-        O.train_step(P, S, ls, opt, x, torch.randn(B, L), 0)
+    for i in range(n):
+        O.train_step(P, S, ls, opt, xs[i], torch.randn(batch, L), 0)
     dt = time.perf_counter() - t0
-    return {"value": round(B * n / dt, 2), "unit": "strain-vectors/s", "cores": threads, "kind": "port",
+    return {"value": round(batch * n / dt, 2), "unit": "strain-vectors/s", "cores": threads, "kind": "port",
             "sample": f"oracle train_step (torch-CPU fp32 autograd, reference op order), v0 G={G} H={H} L={L}, "
-                      f"{n} steps of 512 rows after 1 warm-up, {dt:.1f}s"}
+                      f"{n} steps of {batch} rows of the same synthetic pan-genome matrix after 1 warm-up step, "
+                      f"{dt:.1f}s on {threads} threads"}
+
+
+def gpu_precision_line(mat, G, H, L, B, prec, steps, dev):
+    """ms/step and strain-vectors/s of the same C2 step in another GEMM precision (the f32 line
+    next to the bf16 headline)."""
+    from gm2 import native
+    from gm2.model import VAE
+    from gm2.trainer import Adam
+    torch.manual_seed(0)
+    model = VAE(G, H, L, device=dev, precision=prec)
+    opt = Adam(model, lr=1e-3)
+    ws = model.workspace(prec, B)
+    grads = torch.zeros_like(model.params)
+    scal = torch.tensor(scalar_table(steps + 1), dtype=torch.float32, device=dev)
+    loss = torch.zeros(steps + 1, native.LOSS_SLOTS, dtype=torch.float64, device=dev)
+    g = torch.Generator().manual_seed(5)
+    rows = torch.randperm(mat.n, generator=g)[:B].to(torch.int32).to(dev)
+
+    def step(i):
+        eps = torch.randn(B, L, device=dev)
+        native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, rows, B, eps), model.params, grads, model.bn,
+                             scal[i], loss[i])
+        native.grad_norm(ws, model.params, grads, scal[i], loss[i])
+        native.adam_step(ws, model.params, grads, opt.exp_avg, opt.exp_avg_sq, scal[i])
+    step(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(1, steps + 1):
+        step(i)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if not np.isfinite(loss.cpu().numpy()[:, :3]).all():
+        raise RuntimeError("non-finite loss in the precision line")
+    del ws, model, opt, grads
+    return {"dtype": "f32" if prec == native.GM2_F32 else "bf16", "ms_per_step": round(dt / steps * 1e3, 3),
+            "value": round(B * steps / dt, 1), "unit": "strain-vectors/s", "steps": steps}
+
+
+def scalar_table(nsteps):
+    """Per-step scalar table of the v0 preset at epoch 0 (beta 0.1, no abundance / L1)."""
+    from gm2 import native
+    tab = np.zeros((nsteps, native.NUM_SCALARS), np.float64)
+    for i in range(nsteps):
+        t = i + 1
+        tab[i, native.S_BETA] = 0.1
+        tab[i, native.S_MAX_NORM] = 1.0
+        tab[i, native.S_NEG_STEP] = -(1e-3 / (1 - 0.9 ** t))
+        tab[i, native.S_BC2_SQRT] = math.sqrt(1 - 0.999 ** t)
+        tab[i, native.S_ONE_MINUS_B1], tab[i, native.S_BETA2] = 1 - 0.9, 0.999
+        tab[i, native.S_ONE_MINUS_B2], tab[i, native.S_ADAM_EPS] = 1 - 0.999, 1e-8
+    return tab
 
 
 def main():
@@ -119,6 +179,7 @@ def main():
 
     from gm2 import native
     from gm2.data import ResidentMatrix, synthetic_pangenome
+    from gm2.ddp import GradSync
     from gm2.model import VAE
     from gm2.trainer import Adam
 
@@ -126,7 +187,8 @@ def main():
     prec = native.GM2_BF16 if a.precision == "bf16" else native.GM2_F32
     x = synthetic_pangenome(a.strains, G, seed=12345 + rank)
     mat = ResidentMatrix(x, device=dev)
-    del x
+    if not (rank == 0 and world == 1 and not a.no_cpu_baseline):
+        del x
     torch.manual_seed(0)  # identical init on every rank
     model = VAE(G, H, L, device=dev, precision=prec)
     opt = Adam(model, lr=1e-3)
@@ -134,27 +196,19 @@ def main():
     grads = torch.zeros_like(model.params)
     nsteps = a.warmup + a.steps
     # per-step scalar table (v0: linear beta over 10000 epochs at epoch 0 -> 0.1; no abundance/L1)
-    tab = np.zeros((nsteps, native.NUM_SCALARS), np.float64)
-    for i in range(nsteps):
-        t = i + 1
-        tab[i, native.S_BETA] = 0.1
-        tab[i, native.S_MAX_NORM] = 1.0
-        tab[i, native.S_NEG_STEP] = -(1e-3 / (1 - 0.9 ** t))
-        tab[i, native.S_BC2_SQRT] = math.sqrt(1 - 0.999 ** t)
-        tab[i, native.S_ONE_MINUS_B1], tab[i, native.S_BETA2] = 1 - 0.9, 0.999
-        tab[i, native.S_ONE_MINUS_B2], tab[i, native.S_ADAM_EPS] = 1 - 0.999, 1e-8
-    scal = torch.tensor(tab, dtype=torch.float32, device=dev)
+    scal = torch.tensor(scalar_table(nsteps), dtype=torch.float32, device=dev)
     g = torch.Generator().manual_seed(100 + rank)
     rows = torch.cat([torch.randperm(a.strains, generator=g)[:B] for _ in range(nsteps)]).to(torch.int32).to(dev)
     loss = torch.zeros(nsteps, native.LOSS_SLOTS, dtype=torch.float64, device=dev)
     torch.cuda.manual_seed(1)
+    sync = GradSync(dist, model, grads) if dist is not None else None
 
     def step(i):
         eps = torch.randn(B, L, device=dev)
         batch = native.make_batch(mat.data, mat.ld, rows[i * B:(i + 1) * B], B, eps)
         native.train_fwd_bwd(ws, batch, model.params, grads, model.bn, scal[i], loss[i])
-        if dist is not None:
-            dist.all_reduce(grads)
+        if sync is not None:
+            sync.after_backward()  # bucketed SUM all-reduce overlapped with the backward
         native.grad_norm(ws, model.params, grads, scal[i], loss[i])
         native.adam_step(ws, model.params, grads, opt.exp_avg, opt.exp_avg_sq, scal[i])
 
@@ -206,10 +260,16 @@ def main():
                      "launch_ms": round(k_avg_ms, 4), "launches": k_n,
                      "flops_per_launch": k_flops},
     }
+    if rank == 0 and world == 1 and not a.no_f32_line:
+        other = native.GM2_F32 if prec == native.GM2_BF16 else native.GM2_BF16
+        out["precision_line"] = gpu_precision_line(mat, G, H, L, B, other, 5, dev)
     if rank == 0 and not a.no_sample:
         out["sample"] = sample_bench(a, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(G, H, L, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(x, G, H, L, a.cpu_seconds, B)
+        # C1 (BASELINE.json configs[0]): the reference's CPU plumbing case, v0 at batch 64
+        c1 = cpu_baseline(x, G, H, L, min(8.0, a.cpu_seconds / 2), 64)
+        out["cpu_baseline_c1"] = {k: c1[k] for k in ("value", "unit", "cores", "kind", "sample")}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

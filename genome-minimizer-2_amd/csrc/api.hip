@@ -2,6 +2,7 @@
 // train / eval / sample hot path. Host-side only; kernels live in gemm.hip and kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -84,7 +85,7 @@ struct Layout {
   // the forward GEMM and as an MN-major operand ([K=out][N=in]) in the backward dX GEMM
   int64_t sE0, sE1, sE2, sHD, sD0, sD1, sD2, sD3;
   int64_t X, XB, Y[6], A[6], save[6], HD, Z, dL, slabs, slab_cap, side_slabs, side_cap, dY[6], DA, dH;
-  int64_t bncoef, bnpart, colpart, colpart_cap, losspart, losspart_cap, klpart, gradpart, clip, total;
+  int64_t bncoef, bnpart, colpart, colpart_cap, losspart, losspart_cap, klpart, gradpart, clip, scal0, total;
 };
 
 Layout make_layout(const gm2_dims* gd, int prec) {
@@ -130,13 +131,14 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.dH = take(Bm * d.L2r * es);      // d(mu | logvar) [Bm][L2r]
   o.bnpart = take((Bm / kBnRowChunk) * H * 8);
   o.bncoef = take(5 * H * 4);
-  o.colpart_cap = std::max<int64_t>({(Bm / kTile) * d.Gp, (Bm / 64) * H, (Bm / 64) * 2 * d.L});
+  o.colpart_cap = std::max<int64_t>({(Bm / 64) * d.Gp, (Bm / 64) * H, (Bm / 64) * 2 * d.L});
   o.colpart = take(o.colpart_cap * 4);
   o.losspart_cap = std::max<int64_t>((d.Gp / kTile) * (Bm / kTile) * 2, Bm / 64);
   o.losspart = take(o.losspart_cap * 4);
   o.klpart = take((Bm / 64) * 4);
   o.gradpart = take(2048 * 2 * 8);
   o.clip = take(64);
+  o.scal0 = take(GM2_NUM_SCALARS * 4);
   o.total = cur;
   return o;
 }
@@ -170,12 +172,16 @@ struct SideRes {
   size_t next = 0;
 };
 
-SideRes* side_res() {
-  static const bool enabled = [] {
+std::atomic<int>& side_flag() {
+  static std::atomic<int> on{[] {
     const char* e = getenv("GM2_SIDE_STREAM");
-    return !(e && e[0] == '0');
-  }();
-  if (!enabled) return nullptr;
+    return (e && e[0] == '0') ? 0 : 1;
+  }()};
+  return on;
+}
+
+SideRes* side_res() {
+  if (!side_flag().load(std::memory_order_relaxed)) return nullptr;
   static std::mutex mu;
   static std::map<int, SideRes> per_dev;
   int dev = 0;
@@ -195,6 +201,37 @@ void order(SideRes* r, hipStream_t from, hipStream_t to) {
   hipEvent_t e = r->ev[r->next++ % r->ev.size()];
   HIP_OK(hipEventRecord(e, from));
   HIP_OK(hipStreamWaitEvent(to, e, 0));
+}
+
+// ---------------------------------------------------------------------------------------------
+// gradient buckets (data-parallel exchange): ranges of the flat gradient buffer in the order the
+// backward finalises them, each with a per-device event recorded when its last gradient is
+// written (gm2_grad_bucket_bounds / gm2_wait_grad_bucket)
+//   0: decoder.9.weight, decoder.9.bias      (output layer: first off the backward)
+//   1: encoder.0.bias .. decoder.7.bias      (every hidden / head / BN tensor)
+//   2: encoder.0.weight                      (input layer: the last weight-gradient GEMM)
+// ---------------------------------------------------------------------------------------------
+struct BucketEvents {
+  hipEvent_t ev[GM2_GRAD_BUCKETS] = {};
+  bool recorded = false;
+};
+
+BucketEvents* bucket_events() {
+  static std::mutex mu;
+  static std::map<int, BucketEvents> per_dev;
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  BucketEvents& b = per_dev[dev];
+  if (!b.ev[0])
+    for (auto& e : b.ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return &b;
+}
+
+void bucket_bounds(const Dims& d, int64_t* lh) {
+  lh[0] = d.off[D9W], lh[1] = d.off[NP];
+  lh[2] = d.off[E0B], lh[3] = d.off[D9W];
+  lh[4] = 0, lh[5] = d.off[E0B];
 }
 
 // GEMM into the fp32 slab scratch (split-K slices summed by the consumer). Returns #slabs.
@@ -284,7 +321,7 @@ TensorTable make_table(const Ctx<T>& c, int kind = 0) {
 // ---------------------------------------------------------------------------------------------
 template <typename T>
 void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, int train, int with_grad,
-             const float* scal, double* loss, float* grads) {
+             const float* scal, double* loss, float* grads, float* probs = nullptr, int64_t ld_probs = 0) {
   const Dims& d = c.d;
   const Layout& l = c.lo;
   const int B = (int)b->n;
@@ -320,8 +357,12 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
     ldin = H;
     Kin = H;
   }
-  // 3) output layer + reconstruction loss (+ dlogits)
   GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, B, (int)d.G, H, Bp, (int)d.Gp, 0};
+  if (probs) {  // 3') VAE.forward: output probabilities p = sigmoid(logits) (model.py:89-90), no loss
+    launch_gemm_mask<T>(g, prm + d.off[D9B], nullptr, 0, probs, ld_probs, c.s);
+    return;
+  }
+  // 3) output layer + reconstruction loss (+ dlogits)
   launch_gemm_recon_loss<T>(g, prm + d.off[D9B], (const uint32_t*)(c.ws + l.XB), d.Bm / 32, with_grad, scal, c.t(l.dL),
                             d.Gp, nullptr, 0, c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
   const int nblk = gemm_recon_grid_blocks<T>(g);
@@ -335,7 +376,8 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
 // and Q (dW[out][in] = sum_b dY[b][out] * in[b][in]), input gradients an MN-major weight
 // (dX[b][in] = sum_out dY[b][out] * W[out][in]); no transposed copy exists anywhere.
 template <typename T>
-void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, const float* scal) {
+void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, const float* scal,
+              const float* dmu_ext = nullptr, const float* dlv_ext = nullptr, int train = 1) {
   const Dims& d = c.d;
   const Layout& l = c.lo;
   const int B = (int)b->n, Bp = (int)round_up(B, kTile);
@@ -348,9 +390,12 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   auto fork = [&] {
     if (sr) order(sr, c.s, w.s);
   };
+  BucketEvents* be = bucket_events();
   // output layer: dW9[g][h] = sum_b dL[b][g] A5[b][h] ; dA5[b][h] = sum_g dL[b][g] W9[g][h]
+  // (its bias gradient was summed in the forward's recon epilogue, before the fork)
   fork();
   gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
+  HIP_OK(hipEventRecord(be->ev[0], w.s));
   int S = gemm_to_slabs<T>(c, c.t(l.dL), Gp, Bp, c.t(l.sD3), H, H, B, H, Gp, H, 1, 0);
   const int64_t shadow_w[6] = {l.sE0, l.sE1, l.sE2, l.sD0, l.sD1, l.sD2};
   for (int i = 5; i >= 0; --i) {
@@ -358,14 +403,18 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     const bool sum = S > 1;
     launch_bn_bwd_partial(c.f(c.slab_off), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
                           prm + d.off[kBlk[i][3]], B, H, c.f(l.bnpart), sum ? c.f(l.DA) : nullptr, c.s);
-    launch_bn_bwd_finalize(c.f(l.bnpart), B, H, c.f(l.save[i]), prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
+    launch_bn_bwd_finalize(c.f(l.bnpart), B, H, train, c.f(l.save[i]), prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
                            gr + d.off[kBlk[i][2]], gr + d.off[kBlk[i][3]], c.f(l.bncoef), c.s);
     launch_bn_bwd_apply2<T>(sum ? c.f(l.DA) : c.f(c.slab_off), c.f(l.Y[i]), H, c.f(l.bncoef), B, Bp, H,
                             c.t(l.dY[i]), c.f(l.colpart), c.s);
     launch_colsum(c.f(l.colpart), Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, c.s);
     const T* dY = c.t(l.dY[i]);
     if (i == 0) {  // input layer: weight gradient only (on the main stream: nothing left to overlap)
+      if (sr) order(sr, w.s, c.s);  // join: every hidden-layer weight gradient is final
+      HIP_OK(hipEventRecord(be->ev[1], c.s));
       gemm_to<T>(c, dY, H, H, c.t(l.X), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 0, 0);
+      HIP_OK(hipEventRecord(be->ev[2], c.s));
+      be->recorded = true;
       break;
     }
     fork();
@@ -373,7 +422,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       gemm_to<T>(w, dY, H, H, c.t(l.Z), Lr, Lr, H, L, Bp, gr + d.off[D0W], nullptr, 0, L, 0, 0);
       S = gemm_to_slabs<T>(c, dY, H, Bp, c.t(l.sD0), Lr, Lr, B, L, H, L, 1, 0);
       launch_reparam_bwd<T>(c.f(c.slab_off), S, (int64_t)Bp * L, L, c.f(l.HD), b->eps, scal, B, Bp, L, c.t(l.dH),
-                            L2r, nullptr, 0, 0, c.f(l.colpart), c.s);
+                            L2r, dmu_ext, dlv_ext, c.f(l.colpart), c.s);
       launch_colsum(c.f(l.colpart), Bp / 64, 2 * L, 2 * L, gr + d.off[MUB], gr + d.off[LVB], L, c.s);
       fork();
       gemm_to<T>(w, c.t(l.dH), L2r, L2r, c.t(l.A[2]), H, H, 2 * L, H, Bp, gr + d.off[MUW], gr + d.off[LVW], L, H, 0,
@@ -384,7 +433,6 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     gemm_to<T>(w, dY, H, H, c.t(l.A[i - 1]), H, H, H, H, Bp, gr + d.off[kBlk[i][0]], nullptr, 0, H, 0, 0);
     S = gemm_to_slabs<T>(c, dY, H, Bp, c.t(shadow_w[i]), H, H, B, H, H, H, 1, 0);
   }
-  if (sr) order(sr, w.s, c.s);  // join
 }
 
 template <typename T>
@@ -593,12 +641,99 @@ int gm2_gemm(int prec, int pk, int qk, const void* P, int64_t ldp, const void* Q
         const int S = launch_gemm_store<T>(g, splits, slab_ws, nullptr, 0, ldc, (int64_t)M * ldc, nullptr,
                                            (hipStream_t)stream);
         // sum the slabs column-block-wise: treat [S][M*ldc] as rows
-        launch_colsum(slab_ws, S, M * ldc, (int)(M * ldc), C, nullptr, 0, (hipStream_t)stream);
+        launch_colsum(slab_ws, S, M * ldc, M * ldc, C, nullptr, 0, (hipStream_t)stream);
       }
     };
     if (prec == GM2_F32) run(float{});
     else if (prec == GM2_BF16) run(bf16_t{});
     else throw Gm2Error("bad precision");
+  });
+}
+
+int gm2_forward(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, float* bn_running,
+                int train, float* probs, int64_t ld_probs, float* mu, float* logvar, void* ws, void* stream) {
+  return guarded([&] {
+    const Layout lo = make_layout(d, prec);
+    if (!probs || ld_probs < lo.d.G) throw Gm2Error("forward: probs required, ld_probs >= G");
+    if (!batch->eps) throw Gm2Error("forward: eps required (model.py:102 draws it)");
+    auto run = [&](auto tag) {
+      using T = decltype(tag);
+      Ctx<T> c(lo, ws, stream);
+      forward<T>(c, batch, params, bn_running, train, 0, nullptr, nullptr, nullptr, probs, ld_probs);
+      const int64_t L = lo.d.L, B = batch->n;
+      if (mu) HIP_OK(hipMemcpy2DAsync(mu, L * 4, c.f(lo.HD), 2 * L * 4, L * 4, B, hipMemcpyDeviceToDevice, c.s));
+      if (logvar)
+        HIP_OK(hipMemcpy2DAsync(logvar, L * 4, c.f(lo.HD) + L, 2 * L * 4, L * 4, B, hipMemcpyDeviceToDevice, c.s));
+    };
+    if (prec == GM2_F32) run(float{});
+    else run(bf16_t{});
+  });
+}
+
+int gm2_backward_outputs(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, int train,
+                         const float* probs, int64_t ld_probs, const float* dprobs, const float* dmu,
+                         const float* dlogvar, float* grads, void* ws, void* stream) {
+  return guarded([&] {
+    const Layout lo = make_layout(d, prec);
+    if (!probs || !dprobs || ld_probs < lo.d.G) throw Gm2Error("backward_outputs: probs / dprobs required");
+    auto run = [&](auto tag) {
+      using T = decltype(tag);
+      Ctx<T> c(lo, ws, stream);
+      const Dims& dd = c.d;
+      const int B = (int)batch->n, Bp = (int)round_up(B, kTile);
+      if (B <= 0 || B > dd.Bm) throw Gm2Error("backward_outputs: rows outside (0, batch_max]");
+      launch_sigmoid_bwd<T>(probs, dprobs, ld_probs, B, Bp, (int)dd.G, (int)dd.Gp, c.t(lo.dL), dd.Gp, c.f(lo.colpart),
+                            c.s);
+      launch_colsum(c.f(lo.colpart), Bp / 64, dd.Gp, dd.G, grads + dd.off[D9B], nullptr, 0, c.s);
+      // the fused loss terms are absent here: beta = 0 in a private scalar block
+      float* scal0 = c.f(lo.scal0);
+      HIP_OK(hipMemsetAsync(scal0, 0, GM2_NUM_SCALARS * 4, c.s));
+      backward<T>(c, batch, params, grads, scal0, dmu, dlogvar, train);
+    };
+    if (prec == GM2_F32) run(float{});
+    else run(bf16_t{});
+  });
+}
+
+int gm2_reparameterize(int64_t n, const float* mu, const float* logvar, const float* eps, float* z,
+                       const float* dz, float* dmu, float* dlogvar, void* stream) {
+  return guarded([&] {
+    if (!mu || !logvar || !eps || (!z && !dz) || (dz && (!dmu || !dlogvar)))
+      throw Gm2Error("reparameterize: bad pointers");
+    launch_reparameterize(n, mu, logvar, eps, z, dz, dmu, dlogvar, (hipStream_t)stream);
+  });
+}
+
+int gm2_grad_bucket_bounds(const gm2_dims* d, int64_t* lo_hi) {
+  return guarded([&] { bucket_bounds(make_dims(d), lo_hi); });
+}
+
+int gm2_wait_grad_bucket(int bucket, void* stream) {
+  return guarded([&] {
+    if (bucket < 0 || bucket >= GM2_GRAD_BUCKETS) throw Gm2Error("bucket %d out of range", bucket);
+    BucketEvents* be = bucket_events();
+    if (!be->recorded) throw Gm2Error("no gm2_train_fwd_bwd has run on this device yet");
+    HIP_OK(hipStreamWaitEvent((hipStream_t)stream, be->ev[bucket], 0));
+  });
+}
+
+int gm2_set_option(int key, int value) {
+  return guarded([&] {
+    switch (key) {
+      case GM2_OPT_GEMM_PP: set_gemm_pp(value); break;
+      case GM2_OPT_SIDE_STREAM: side_flag().store(value ? 1 : 0); break;
+      default: throw Gm2Error("unknown option %d", key);
+    }
+  });
+}
+
+int gm2_get_option(int key, int* value) {
+  return guarded([&] {
+    switch (key) {
+      case GM2_OPT_GEMM_PP: *value = get_gemm_pp(); break;
+      case GM2_OPT_SIDE_STREAM: *value = side_flag().load(); break;
+      default: throw Gm2Error("unknown option %d", key);
+    }
   });
 }
 

@@ -21,7 +21,10 @@
 #include "gm2_common.hpp"
 #include "gm2_kernels.hpp"
 
+#include <atomic>
 #include <cstdlib>
+#include <mutex>
+#include <set>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -627,7 +630,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
         const int m = tl.m0 + wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
         if (m >= g.M) continue;
         const float l = acc[mi][ni][j] + bn;
-        mask[(int64_t)m * ldm + n] = l > kMaskLogitThreshold ? 1 : 0;
+        if (mask) mask[(int64_t)m * ldm + n] = l > kMaskLogitThreshold ? 1 : 0;
         if (probs) probs[(int64_t)m * ldpr + n] = 1.0f / (1.0f + expf(-l));
       }
   }
@@ -721,26 +724,38 @@ static bool use_big(const GemmArgs<T>& g) {
   return plan_gemm(g).tile == 256;
 }
 
-// GM2_GEMM_PP=1 selects the ping-pong main loop for the 256x256 bf16 tiles (experimental until
-// measured on the GPU; the default is the two-stage loop)
-static bool pp_enabled() {
-  static const int on = [] {
+// Main-loop selection for the 256x256 bf16 tiles: the ping-pong loop (default; measured
+// +15-20 % on the long-K GEMMs of the v0 step, profiles/r02_gemm_bench.txt) or the two-stage loop
+// (option GM2_OPT_GEMM_PP = 0, or env GM2_GEMM_PP=0). Read on every launch so a test can switch
+// it in-process (gm2_set_option); both are parity-tested.
+static std::atomic<int>& pp_flag() {
+  static std::atomic<int> on{[] {
     const char* e = std::getenv("GM2_GEMM_PP");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return on != 0;
+    return e && e[0] == '0' ? 0 : 1;
+  }()};
+  return on;
+}
+static bool pp_enabled() { return pp_flag().load(std::memory_order_relaxed) != 0; }
+void set_gemm_pp(int on) { pp_flag().store(on ? 1 : 0, std::memory_order_relaxed); }
+int get_gemm_pp() { return pp_flag().load(std::memory_order_relaxed); }
+
+// hipFuncAttributeMaxDynamicSharedMemorySize is per device: remember (device, kernel) pairs
+static void ensure_lds_attr(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::set<std::pair<int, const void*>> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) throw Gm2Error("hipGetDevice");
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.count({dev, fn})) return;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+    throw Gm2Error("hipFuncSetAttribute(MaxDynamicSharedMemorySize=%d)", bytes);
+  done.insert({dev, fn});
 }
 
 template <class C, typename T, bool AK, bool BK, bool PP>
 static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
                            const float* bias, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)k_gemm_store<C, T, AK, BK, PP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            C::LDS) != hipSuccess)
-      throw Gm2Error("hipFuncSetAttribute(store)");
-    attr = true;
-  }
+  ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP>, C::LDS);
   hipLaunchKernelGGL((k_gemm_store<C, T, AK, BK, PP>), dim3(tiles), dim3(C::NT), C::LDS, s, a, C0, C1 ? C1 : C0,
                      C1 ? msplit : (1 << 30), ldc, slab, bias);
 }
@@ -806,13 +821,7 @@ static void recon_impl_k(const GemmArgs<T>& g, const float* bias, const uint32_t
   check_gemm(g, C::BM);
   constexpr int lds = std::max<int>(C::LDS, std::max(C::BM * (C::BN + 8), C::BN * (C::BM + 8)) * (int)sizeof(T));
   static_assert(lds <= 160 * 1024, "LDS budget");
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)k_gemm_recon_loss<C, T, PP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            lds) != hipSuccess)
-      throw Gm2Error("hipFuncSetAttribute(recon)");
-    attr = true;
-  }
+  ensure_lds_attr((const void*)k_gemm_recon_loss<C, T, PP>, lds);
   hipLaunchKernelGGL((k_gemm_recon_loss<C, T, PP>), dim3((g.Mp / C::BM) * (g.Np / C::BN)), dim3(C::NT), lds, s, g,
                      bias, X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol);
 }
@@ -875,5 +884,7 @@ GM2_INST(bf16_t)
 #undef GM2_INST
 template void launch_gemm_mask<float>(const GemmArgs<float>&, const float*, uint8_t*, int64_t, float*, int64_t,
                                       hipStream_t);
+template void launch_gemm_mask<bf16_t>(const GemmArgs<bf16_t>&, const float*, uint8_t*, int64_t, float*, int64_t,
+                                       hipStream_t);
 
 }  // namespace gm2

@@ -85,6 +85,9 @@ template <typename T>
 int gemm_recon_grid_blocks(const GemmArgs<T>& g);
 template <typename T>
 int gemm_recon_row_tiles(const GemmArgs<T>& g);
+// process-global GEMM main-loop switch (gm2_set_option GM2_OPT_GEMM_PP)
+void set_gemm_pp(int on);
+int get_gemm_pp();
 struct GemmPlan {
   int tile, splits;
 };
@@ -111,27 +114,17 @@ void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* row
 // BN forward: y = sum of S slabs + bias -> Y; per-chunk (mean, M2) partials
 void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, const float* bias, int B, int H,
                            float* Y, float* part, hipStream_t s);
-// BN forward apply (train: batch stats from partials + running-stat update; eval: running stats)
-template <typename T>
-void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
-                         const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,
-                         T* AT, int64_t ldat, hipStream_t s);
 // BN backward: partials of sum(do), sum((y-mean)*do) with do = dA * [bn_out > 0]; optionally
 // writes the summed split-K dA (dsum) so the apply pass reads one slab instead of S
 void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
                            const float* gamma, const float* beta, int B, int H, float* part, float* dsum,
                            hipStream_t s);
-template <typename T>
-void launch_bn_bwd_apply(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
-                         const float* gamma, const float* beta, const float* part, int B, int Bp, int H,
-                         float* dgamma, float* dbeta, T* dY, T* dYT, int64_t ldyt, float* colpart,
-                         hipStream_t s);
 // BatchNorm v2 (finalize once per column, vectorised elementwise passes)
 void launch_bn_fwd_finalize(const float* part, int B, int H, int train, const float* gamma, const float* beta,
                             float* rmean, float* rvar, float* save, float* coef, hipStream_t s);
 template <typename T>
 void launch_bn_fwd_apply2(const float* Y, int64_t ld, const float* coef, int B, int Bp, int H, T* A, hipStream_t s);
-void launch_bn_bwd_finalize(const float* part, int B, int H, const float* save, const float* gamma,
+void launch_bn_bwd_finalize(const float* part, int B, int H, int train, const float* save, const float* gamma,
                             const float* beta, float* dgamma, float* dbeta, float* cf, hipStream_t s);
 template <typename T>
 void launch_bn_bwd_apply2(const float* da, const float* Y, int64_t ld, const float* cf, int B, int Bp, int H, T* dY,
@@ -143,10 +136,17 @@ void launch_reparam(const float* slabs, int S, int64_t slab, int L, const float*
                     float* kl_part, hipStream_t s);
 template <typename T>
 void launch_reparam_bwd(const float* dzslabs, int S, int64_t slab, int64_t ldslab, const float* HD,
-                        const float* eps, const float* scal, int B, int Bp, int L, T* dH, int64_t ldh, T* dHT,
-                        int64_t ldht, int Hrows, float* colpart, hipStream_t s);
+                        const float* eps, const float* scal, int B, int Bp, int L, T* dH, int64_t ldh,
+                        const float* dmu_ext, const float* dlv_ext, float* colpart, hipStream_t s);
+// z = mu + exp(lv/2)*eps over n elements (z != NULL), and/or its backward (dz != NULL -> dmu, dlv)
+void launch_reparameterize(int64_t n, const float* mu, const float* lv, const float* eps, float* z, const float* dz,
+                           float* dmu, float* dlv, hipStream_t s);
+// dl = dp*(1-p)*p -> dL (T) [Bp][ldd] + per-64-row column partial sums [Bp/64][Gp]
+template <typename T>
+void launch_sigmoid_bwd(const float* p, const float* dp, int64_t ldp, int B, int Bp, int G, int Gp, T* dL, int64_t ldd,
+                        float* colpart, hipStream_t s);
 // out[n] = sum_r part[r*ld + n]  (deterministic order)
-void launch_colsum(const float* part, int rows, int64_t ld, int n, float* out0, float* out1, int nsplit,
+void launch_colsum(const float* part, int rows, int64_t ld, int64_t n, float* out0, float* out1, int64_t nsplit,
                    hipStream_t s);
 // C0/C1 (row split at msplit) = sum of S split-K slabs [S][M][N] (slab stride `slab`)
 void launch_slab_sum(const float* slabs, int S, int64_t slab, int M, int N, float* C0, float* C1, int msplit,
@@ -178,16 +178,11 @@ void launch_shadow_sync(const TensorTable& tt, const float* params, hipStream_t 
 template <typename T>
 void launch_adam_fused(const TensorTable& tt, const float* grads, float* params, float* m, float* v, const float* scal,
                        const float* clip, hipStream_t s);
-// transposed shadows from natural shadows (table entries with shadowT; tile0 counts 64x64 tiles)
-template <typename T>
-void launch_shadow_transpose(const TensorTable& tt, hipStream_t s);
 // sum((g + lambda*sign(p))^2) and sum(|p|) over all params -> partials; then finalize
 void launch_grad_stats(const float* params, const float* grads, int64_t n, const float* scal, double* part,
                        int nblocks, hipStream_t s);
 void launch_grad_finalize(const double* part, int nblocks, const float* scal, float* clip_out,
                           double* loss_l1abs, hipStream_t s);
-void launch_adam(const float* grads, float* params, float* m, float* v, int64_t n, const float* scal,
-                 const float* clip, hipStream_t s);
 
 int grad_stats_blocks(int64_t n);
 

@@ -144,66 +144,6 @@ __device__ inline void bn_merge(const float2* __restrict__ part, int B, int H, i
 }
 
 // ---------------------------------------------------------------------------------------------
-// BN forward apply + ReLU: A = relu(y*alpha + beta'), alpha = invstd*gamma, beta' = beta - mean*alpha
-// (the reference's batch_norm transform), A^T via LDS. Tile 64 rows x 64 cols.
-// save[0][c] = mean, save[1][c] = invstd (train) — reused by the backward.
-// ---------------------------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(256) void k_bn_fwd_apply(const float* __restrict__ Y, int64_t ld,
-                                                    const float2* __restrict__ part, int B, int H, int train,
-                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                    float* __restrict__ rmean, float* __restrict__ rvar,
-                                                    float* __restrict__ save, T* __restrict__ A,
-                                                    T* __restrict__ AT, int64_t ldat) {
-  __shared__ float coef[2][64];
-  __shared__ float tile[64][65];
-  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
-  const int t = threadIdx.x;
-  if (t < 64) {
-    const int col = c0 + t;
-    float invstd, meanf;
-    if (train) {
-      double mean, var;
-      bn_merge(part, B, H, col, mean, var);
-      invstd = (float)(1.0 / sqrt(var + kBnEps));
-      meanf = (float)mean;
-      if (blockIdx.y == 0) {
-        save[col] = meanf;
-        save[H + col] = invstd;
-        const double unb = B > 1 ? var * (double)B / (double)(B - 1) : var;
-        rmean[col] = (float)(kBnMomentum * mean + (1.0 - kBnMomentum) * (double)rmean[col]);
-        rvar[col] = (float)(kBnMomentum * unb + (1.0 - kBnMomentum) * (double)rvar[col]);
-      }
-    } else {
-      // eval transform bit-identical to the reference CPU path (pinned in tests): float
-      // invstd = 1/sqrt(rv + eps), alpha = gamma*invstd, beta' = fma(-mean, alpha, beta)
-      meanf = rmean[col];
-      invstd = 1.0f / sqrtf(rvar[col] + (float)kBnEps);
-      if (blockIdx.y == 0 && save) { save[col] = meanf; save[H + col] = invstd; }
-    }
-    const float alpha = invstd * gamma[col];
-    coef[0][t] = alpha;
-    coef[1][t] = fmaf(-meanf, alpha, beta[col]);
-  }
-  __syncthreads();
-  const int c = t & 63;
-  for (int rl = t >> 6; rl < 64; rl += 4) {
-    const int r = r0 + rl;
-    float a = 0.f;
-    if (r < B) a = fmaxf(fmaf(Y[(int64_t)r * ld + c0 + c], coef[0][c], coef[1][c]), 0.f);
-    A[(int64_t)r * ld + c0 + c] = E<T>::cvt(a);
-    tile[c][rl] = a;
-  }
-  __syncthreads();
-  if (AT) {
-    for (int i = t; i < 64 * 64; i += 256) {
-      const int cc = i >> 6, rl = i & 63;
-      AT[(int64_t)(c0 + cc) * ldat + r0 + rl] = E<T>::cvt(tile[cc][rl]);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // BN backward partials: do = dA * [y*alpha+beta' > 0]; sums of do and (y-mean)*do per chunk
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict__ dslabs, int S, int64_t slab,
@@ -237,76 +177,6 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict_
   if (rg == 0)
     part[(int64_t)blockIdx.y * H + col] = make_float2(red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c],
                                                       red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
-}
-
-// BN backward apply (training-mode formula of the reference's native batch_norm backward):
-//   dx = (do - sum(do)/B - (y-mean) * sum((y-mean)*do) * invstd^2 / B) * invstd * gamma
-//   dgamma = sum((y-mean)*do) * invstd ; dbeta = sum(do)
-// Writes dY, dY^T (T) and per-64-row column sums of dx (the preceding Linear's bias gradient).
-template <typename T>
-__global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ dslabs, int S, int64_t slab,
-                                                    const float* __restrict__ Y, int64_t ld,
-                                                    const float* __restrict__ save, const float* __restrict__ gamma,
-                                                    const float* __restrict__ beta, const float2* __restrict__ part,
-                                                    int B, int H, float* __restrict__ dgamma,
-                                                    float* __restrict__ dbeta, T* __restrict__ dY,
-                                                    T* __restrict__ dYT, int64_t ldyt, float* __restrict__ colpart) {
-  __shared__ float cf[5][64];
-  __shared__ float tile[64][65];
-  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
-  const int t = threadIdx.x;
-  if (t < 64) {
-    const int col = c0 + t;
-    double s1 = 0.0, s2 = 0.0;
-    const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
-    for (int ch = 0; ch < nch; ++ch) {
-      const float2 p = part[(int64_t)ch * H + col];
-      s1 += p.x;
-      s2 += p.y;
-    }
-    const float mean = save[col], invstd = save[H + col];
-    const float alpha = invstd * gamma[col];
-    if (blockIdx.y == 0) {
-      dgamma[col] = (float)(s2 * invstd);
-      dbeta[col] = (float)s1;
-    }
-    cf[0][t] = mean;
-    cf[1][t] = alpha;
-    cf[2][t] = fmaf(-mean, alpha, beta[col]);
-    cf[3][t] = (float)(s1 / B);                                 // grad_mean
-    cf[4][t] = (float)(s2 * (double)invstd * invstd / B);      // proj_scale
-  }
-  __syncthreads();
-  const int c = t & 63;
-  const float gs = cf[1][c];  // grad_scale = invstd * gamma
-  float csum = 0.f;
-  for (int rl = t >> 6; rl < 64; rl += 4) {
-    const int r = r0 + rl;
-    float dx = 0.f;
-    if (r < B) {
-      const int64_t o = (int64_t)r * ld + c0 + c;
-      float da = dslabs[o];
-      for (int s = 1; s < S; ++s) da += dslabs[(int64_t)s * slab + o];
-      const float y = Y[o];
-      const float d = fmaf(y, cf[1][c], cf[2][c]) > 0.f ? da : 0.f;
-      dx = (d - cf[3][c] - (y - cf[0][c]) * cf[4][c]) * gs;
-    }
-    csum += dx;
-    dY[(int64_t)r * ld + c0 + c] = E<T>::cvt(dx);
-    tile[c][rl] = dx;
-  }
-  __syncthreads();
-  if (dYT) {
-    for (int i = t; i < 64 * 64; i += 256) {
-      const int cc = i >> 6, rl = i & 63;
-      dYT[(int64_t)(c0 + cc) * ldyt + r0 + rl] = E<T>::cvt(tile[cc][rl]);
-    }
-  }
-  __syncthreads();
-  float* red = &tile[0][0];
-  red[t] = csum;
-  __syncthreads();
-  if (t < 64) colpart[(int64_t)blockIdx.y * H + c0 + t] = red[t] + red[t + 64] + red[t + 128] + red[t + 192];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -348,13 +218,16 @@ __global__ __launch_bounds__(256) void k_reparam(const float* __restrict__ slabs
 }
 
 // backward through reparameterization + beta*KL (autograd of model.py:101-103 and
-// loss_components.py:77): dmu = dz + beta*mu ; dlv = 0.5*dz*eps*std - 0.5*beta*(1 - exp(lv))
+// loss_components.py:77): dmu = dz + beta*mu ; dlv = 0.5*dz*eps*std - 0.5*beta*(1 - exp(lv)).
+// dmu_ext / dlv_ext (optional, [B][L]): upstream gradients of mu / logvar from outside the fused
+// loss (VAE.forward under torch autograd: gm2_backward_outputs), added to the above.
 template <typename T>
 __global__ __launch_bounds__(256) void k_reparam_bwd(const float* __restrict__ dz, int S, int64_t slab,
                                                    int64_t ldslab, const float* __restrict__ HD,
                                                    const float* __restrict__ eps, const float* __restrict__ scal,
-                                                   int B, int L, T* __restrict__ dH, int64_t ldh, T* __restrict__ dHT,
-                                                   int64_t ldht, float* __restrict__ colpart) {
+                                                   int B, int L, T* __restrict__ dH, int64_t ldh,
+                                                   const float* __restrict__ dmu_ext,
+                                                   const float* __restrict__ dlv_ext, float* __restrict__ colpart) {
   __shared__ float acc[2][256];
   const float beta = scal[kScalBeta];
   const int r0 = blockIdx.x * 64;
@@ -374,13 +247,11 @@ __global__ __launch_bounds__(256) void k_reparam_bwd(const float* __restrict__ d
       const float e = eps[(int64_t)r * L + l];
       gmu = d + (0.5f * beta) * (2.0f * mu);
       glv = 0.5f * ((d * e) * sd) + (-0.5f * beta + (0.5f * beta) * expf(lv));
+      if (dmu_ext) gmu += dmu_ext[(int64_t)r * L + l];
+      if (dlv_ext) glv += dlv_ext[(int64_t)r * L + l];
     }
     dH[(int64_t)r * ldh + l] = E<T>::cvt(gmu);
     dH[(int64_t)r * ldh + L + l] = E<T>::cvt(glv);
-    if (dHT) {
-      dHT[(int64_t)l * ldht + r] = E<T>::cvt(gmu);
-      dHT[(int64_t)(L + l) * ldht + r] = E<T>::cvt(glv);
-    }
     smu += gmu;
     slv += glv;
   }
@@ -395,14 +266,45 @@ __global__ __launch_bounds__(256) void k_reparam_bwd(const float* __restrict__ d
   }
 }
 
-__global__ void k_colsum(const float* __restrict__ part, int rows, int64_t ld, int n, float* __restrict__ out0,
-                         float* __restrict__ out1, int nsplit) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n) return;
-  float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += part[(int64_t)r * ld + c];
-  if (c < nsplit) out0[c] = s;
-  else out1[c - nsplit] = s;
+// z = mu + exp(0.5*lv)*eps (model.py:100-104 VAE.reparameterization with the noise given),
+// and its backward (mode 1): dmu = dz, dlv = 0.5*dz*eps*exp(0.5*lv). Elementwise over n*L.
+__global__ __launch_bounds__(256) void k_reparameterize(int64_t n, const float* __restrict__ mu,
+                                                      const float* __restrict__ lv, const float* __restrict__ eps,
+                                                      float* __restrict__ z, const float* __restrict__ dz,
+                                                      float* __restrict__ dmu, float* __restrict__ dlv) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float sd = expf(0.5f * lv[i]);
+    if (z) z[i] = mu[i] + sd * eps[i];
+    if (dz) {
+      const float d = dz[i];
+      dmu[i] = d;
+      dlv[i] = 0.5f * ((d * eps[i]) * sd);
+    }
+  }
+}
+
+// dL/dlogit of the output layer from an upstream dL/dp (autograd of torch.sigmoid, model.py:90):
+// dl = dp * (1 - p) * p, written as T [Bp][ldd] (rows >= B and columns >= G zero) with per-(64-row
+// chunk, column) partial sums for the output bias gradient. Block: 256 columns x 64 rows.
+template <typename T>
+__global__ __launch_bounds__(256) void k_sigmoid_bwd(const float* __restrict__ p, const float* __restrict__ dp,
+                                                   int64_t ldp, int B, int G, int Gp, T* __restrict__ dL,
+                                                   int64_t ldd, float* __restrict__ colpart) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int r0 = blockIdx.y * 64;
+  if (c >= Gp) return;
+  float cs = 0.f;
+  for (int rl = 0; rl < 64; ++rl) {
+    const int r = r0 + rl;
+    float dl = 0.f;
+    if (r < B && c < G) {
+      const float pv = p[(int64_t)r * ldp + c];
+      dl = (dp[(int64_t)r * ldp + c] * (1.0f - pv)) * pv;
+    }
+    cs += dl;
+    dL[(int64_t)r * ldd + c] = E<T>::cvt(dl);
+  }
+  colpart[(int64_t)blockIdx.y * Gp + c] = cs;
 }
 
 __global__ __launch_bounds__(256) void k_reduce_to(const float* __restrict__ part, int n, int stride, int count,
@@ -532,27 +434,6 @@ __global__ __launch_bounds__(256) void k_grad_finalize(const double* __restrict_
   }
 }
 
-__global__ __launch_bounds__(256) void k_adam(const float* __restrict__ g, float* __restrict__ p,
-                                            float* __restrict__ m, float* __restrict__ v, int64_t n,
-                                            const float* __restrict__ scal, const float* __restrict__ clip) {
-  const float lam = scal[kScalLambda], negstep = scal[kScalNegStep], bc2s = scal[kScalBc2Sqrt];
-  const float w1 = scal[kScalOneMinusB1], b2 = scal[kScalBeta2], w2 = scal[kScalOneMinusB2];
-  const float aeps = scal[kScalAdamEps];
-  const float cc = clip[0];
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float pv = p[i];
-    const float gv = (g[i] + lam * sgnf(pv)) * cc;
-    float mv = m[i];
-    mv = mv + w1 * (gv - mv);                    // lerp_(grad, w1), w1 < 0.5 branch
-    float vv = v[i] * b2;
-    vv = vv + w2 * gv * gv;                      // addcmul_(g, g, value=w2)
-    const float denom = sqrtf(vv) / bc2s + aeps;
-    p[i] = pv + negstep * (mv / denom);          // addcdiv_(m, denom, value=-step_size)
-    m[i] = mv;
-    v[i] = vv;
-  }
-}
-
 // fused L1 + clip + Adam over one tensor table entry per block group, writing the fp32 master and
 // the natural-layout GEMM shadow in the same pass (30 B/param of HBM traffic instead of 30 + 6)
 template <typename T>
@@ -625,31 +506,6 @@ __global__ __launch_bounds__(256) void k_adam_fused(TensorTable tt, const float*
         }
       }
     }
-  }
-}
-
-// transposed GEMM shadows from the natural ones (T -> T, 64x64 tiles through LDS)
-template <typename T>
-__global__ __launch_bounds__(256) void k_shadow_transpose(TensorTable tt) {
-  __shared__ float tile[64][65];
-  int ti = 0;
-  while (ti + 1 < tt.n && (int64_t)blockIdx.x >= tt.t[ti + 1].tile0) ++ti;
-  const TensorDesc& d = tt.t[ti];
-  const int64_t local = blockIdx.x - d.tile0;
-  const int64_t tcols = (d.cols + 63) / 64;
-  const int64_t r0 = (local / tcols) * 64, c0 = (local % tcols) * 64;
-  const T* sh = (const T*)d.shadow;
-  T* shT = (T*)d.shadowT;
-  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-    const int rl = i >> 6, cl = i & 63;
-    const int64_t r = r0 + rl, c = c0 + cl;
-    tile[cl][rl] = (r < d.rows && c < d.cols) ? E<T>::ld(sh + (d.srow0 + r) * d.sld + c) : 0.f;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-    const int cl = i >> 6, rl = i & 63;
-    const int64_t r = r0 + rl, c = c0 + cl;
-    if (r < d.rows && c < d.cols) shT[c * d.tld + d.srow0 + r] = E<T>::cvt(tile[cl][rl]);
   }
 }
 
@@ -734,7 +590,9 @@ __global__ __launch_bounds__(256) void k_bn_fwd_apply2(const float* __restrict__
   }
 }
 
-__global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float2* __restrict__ part, int B, int H,
+// train = 0: eval-mode BatchNorm is the affine map y -> (y - rm)*invstd*gamma + beta, whose backward
+// has no batch-coupling terms (grad_mean = proj_scale = 0)
+__global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float2* __restrict__ part, int B, int H, int train,
                                                        const float* __restrict__ save, const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, float* __restrict__ dgamma,
                                                        float* __restrict__ dbeta, float* __restrict__ cf) {
@@ -755,8 +613,8 @@ __global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float2* __restric
   cf[col] = mean;
   cf[H + col] = alpha;
   cf[2 * H + col] = fmaf(-mean, alpha, beta[col]);
-  cf[3 * H + col] = (float)(s1 / B);
-  cf[4 * H + col] = (float)(s2 * (double)invstd * invstd / B);
+  cf[3 * H + col] = train ? (float)(s1 / B) : 0.f;
+  cf[4 * H + col] = train ? (float)(s2 * (double)invstd * invstd / B) : 0.f;
 }
 
 // dx = (do - grad_mean - (y-mean)*proj_scale) * alpha, do = da*[y*alpha+beta' > 0]; rows >= B -> 0.
@@ -805,11 +663,11 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply2(const float* __restrict__
 }
 
 // out[c] = sum_r part[r][c]: 64 columns x 4 row groups per block, fixed order (deterministic)
-__global__ __launch_bounds__(256) void k_colsum2(const float* __restrict__ part, int rows, int64_t ld, int n,
-                                               float* __restrict__ out0, float* __restrict__ out1, int nsplit) {
+__global__ __launch_bounds__(256) void k_colsum2(const float* __restrict__ part, int rows, int64_t ld, int64_t n,
+                                               float* __restrict__ out0, float* __restrict__ out1, int64_t nsplit) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  const int64_t c = (int64_t)blockIdx.x * 64 + cl;
   float s = 0.f;
   if (c < n)
     for (int r = rg; r < rows; r += 4) s += part[(int64_t)r * ld + c];
@@ -846,30 +704,12 @@ void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, 
   GM2_CHECK_LAUNCH();
 }
 
-template <typename T>
-void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
-                         const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A, T* AT,
-                         int64_t ldat, hipStream_t s) {
-  hipLaunchKernelGGL(k_bn_fwd_apply<T>, dim3(H / 64, Bp / 64), dim3(256), 0, s, Y, ld, (const float2*)part, B, H,
-                     train, gamma, beta, rmean, rvar, save, A, AT, ldat);
-  GM2_CHECK_LAUNCH();
-}
-
 void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
                            const float* gamma, const float* beta, int B, int H, float* part, float* dsum,
                            hipStream_t s) {
   const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
   hipLaunchKernelGGL(k_bn_bwd_partial, dim3(H / 64, nch), dim3(256), 0, s, dslabs, S, slab, Y, ld, save, gamma,
                      beta, B, H, (float2*)part, dsum);
-  GM2_CHECK_LAUNCH();
-}
-
-template <typename T>
-void launch_bn_bwd_apply(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
-                         const float* gamma, const float* beta, const float* part, int B, int Bp, int H,
-                         float* dgamma, float* dbeta, T* dY, T* dYT, int64_t ldyt, float* colpart, hipStream_t s) {
-  hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3(H / 64, Bp / 64), dim3(256), 0, s, dslabs, S, slab, Y, ld, save, gamma,
-                     beta, (const float2*)part, B, H, dgamma, dbeta, dY, dYT, ldyt, colpart);
   GM2_CHECK_LAUNCH();
 }
 
@@ -885,18 +725,34 @@ void launch_reparam(const float* slabs, int S, int64_t slab, int L, const float*
 
 template <typename T>
 void launch_reparam_bwd(const float* dzslabs, int S, int64_t slab, int64_t ldslab, const float* HD, const float* eps,
-                        const float* scal, int B, int Bp, int L, T* dH, int64_t ldh, T* dHT, int64_t ldht, int Hrows,
-                        float* colpart, hipStream_t s) {
-  (void)Hrows;
+                        const float* scal, int B, int Bp, int L, T* dH, int64_t ldh, const float* dmu_ext,
+                        const float* dlv_ext, float* colpart, hipStream_t s) {
   if (L > 256 || 256 % L) throw Gm2Error("reparam_bwd: latent_dim must divide 256");
   hipLaunchKernelGGL(k_reparam_bwd<T>, dim3(Bp / 64), dim3(256), 0, s, dzslabs, S, slab, ldslab, HD, eps, scal, B, L,
-                     dH, ldh, dHT, ldht, colpart);
+                     dH, ldh, dmu_ext, dlv_ext, colpart);
   GM2_CHECK_LAUNCH();
 }
 
-void launch_colsum(const float* part, int rows, int64_t ld, int n, float* out0, float* out1, int nsplit,
+void launch_reparameterize(int64_t n, const float* mu, const float* lv, const float* eps, float* z, const float* dz,
+                           float* dmu, float* dlv, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t nb = std::min<int64_t>(4096, (n + 255) / 256);
+  hipLaunchKernelGGL(k_reparameterize, dim3((unsigned)nb), dim3(256), 0, s, n, mu, lv, eps, z, dz, dmu, dlv);
+  GM2_CHECK_LAUNCH();
+}
+
+template <typename T>
+void launch_sigmoid_bwd(const float* p, const float* dp, int64_t ldp, int B, int Bp, int G, int Gp, T* dL, int64_t ldd,
+                        float* colpart, hipStream_t s) {
+  hipLaunchKernelGGL(k_sigmoid_bwd<T>, dim3((Gp + 255) / 256, Bp / 64), dim3(256), 0, s, p, dp, ldp, B, G, Gp, dL, ldd,
+                     colpart);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_colsum(const float* part, int rows, int64_t ld, int64_t n, float* out0, float* out1, int64_t nsplit,
                    hipStream_t s) {
-  hipLaunchKernelGGL(k_colsum2, dim3((n + 63) / 64), dim3(256), 0, s, part, rows, ld, n, out0, out1 ? out1 : out0,
+  if ((n + 63) / 64 > INT32_MAX) throw Gm2Error("colsum: %lld columns", (long long)n);
+  hipLaunchKernelGGL(k_colsum2, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, part, rows, ld, n, out0, out1 ? out1 : out0,
                      out1 ? nsplit : n);
   GM2_CHECK_LAUNCH();
 }
@@ -916,9 +772,9 @@ void launch_bn_fwd_apply2(const float* Y, int64_t ld, const float* coef, int B, 
   GM2_CHECK_LAUNCH();
 }
 
-void launch_bn_bwd_finalize(const float* part, int B, int H, const float* save, const float* gamma,
+void launch_bn_bwd_finalize(const float* part, int B, int H, int train, const float* save, const float* gamma,
                             const float* beta, float* dgamma, float* dbeta, float* cf, hipStream_t s) {
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((H + 255) / 256), dim3(256), 0, s, (const float2*)part, B, H, save, gamma,
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((H + 255) / 256), dim3(256), 0, s, (const float2*)part, B, H, train, save, gamma,
                      beta, dgamma, dbeta, cf);
   GM2_CHECK_LAUNCH();
 }
@@ -956,15 +812,6 @@ void launch_adam_fused(const TensorTable& tt, const float* grads, float* params,
   GM2_CHECK_LAUNCH();
 }
 
-template <typename T>
-void launch_shadow_transpose(const TensorTable& tt, hipStream_t s) {
-  if (tt.n <= 0) return;
-  const TensorDesc& last = tt.t[tt.n - 1];
-  const int64_t tiles = last.tile0 + ((last.rows + 63) / 64) * ((last.cols + 63) / 64);
-  hipLaunchKernelGGL(k_shadow_transpose<T>, dim3((unsigned)tiles), dim3(256), 0, s, tt);
-  GM2_CHECK_LAUNCH();
-}
-
 void launch_slab_sum(const float* slabs, int S, int64_t slab, int M, int N, float* C0, float* C1, int msplit,
                      int64_t ldc, hipStream_t s) {
   if (slab % 4) throw Gm2Error("slab_sum: slab %% 4");
@@ -988,33 +835,22 @@ void launch_grad_finalize(const double* part, int nblocks, const float* scal, fl
   GM2_CHECK_LAUNCH();
 }
 
-void launch_adam(const float* grads, float* params, float* m, float* v, int64_t n, const float* scal,
-                 const float* clip, hipStream_t s) {
-  const int nb = (int)std::min<int64_t>(8192, (n + 255) / 256);
-  hipLaunchKernelGGL(k_adam, dim3(nb), dim3(256), 0, s, grads, params, m, v, n, scal, clip);
-  GM2_CHECK_LAUNCH();
-}
-
 #define GM2_INST(T)                                                                                             \
   template void launch_gather_rows<T>(const uint8_t*, int64_t, const int32_t*, int, int, T*, int64_t, int, T*,  \
                                       int64_t, int, uint32_t*, int64_t, hipStream_t);                           \
-  template void launch_bn_fwd_apply<T>(const float*, int64_t, const float*, int, int, int, int, const float*,   \
-                                       const float*, float*, float*, float*, T*, T*, int64_t, hipStream_t);     \
-  template void launch_bn_bwd_apply<T>(const float*, int, int64_t, const float*, int64_t, const float*,         \
-                                       const float*, const float*, const float*, int, int, int, float*, float*, \
-                                       T*, T*, int64_t, float*, hipStream_t);                                   \
   template void launch_reparam<T>(const float*, int, int64_t, int, const float*, const float*, const float*,   \
                                   int, int, float*, T*, int64_t, T*, int64_t, int, float*, hipStream_t);        \
   template void launch_reparam_bwd<T>(const float*, int, int64_t, int64_t, const float*, const float*,         \
-                                      const float*, int, int, int, T*, int64_t, T*, int64_t, int, float*,       \
-                                      hipStream_t);                                                             \
+                                      const float*, int, int, int, T*, int64_t, const float*, const float*,     \
+                                      float*, hipStream_t);                                                     \
+  template void launch_sigmoid_bwd<T>(const float*, const float*, int64_t, int, int, int, int, T*, int64_t,     \
+                                      float*, hipStream_t);                                                     \
   template void launch_shadow_sync<T>(const TensorTable&, const float*, hipStream_t);                          \
   template void launch_bn_fwd_apply2<T>(const float*, int64_t, const float*, int, int, int, T*, hipStream_t);  \
   template void launch_bn_bwd_apply2<T>(const float*, const float*, int64_t, const float*, int, int, int, T*,    \
                                         float*, hipStream_t);                                                  \
   template void launch_adam_fused<T>(const TensorTable&, const float*, float*, float*, float*, const float*,    \
-                                     const float*, hipStream_t);                                                \
-  template void launch_shadow_transpose<T>(const TensorTable&, hipStream_t);
+                                     const float*, hipStream_t);
 GM2_INST(float)
 GM2_INST(bf16_t)
 #undef GM2_INST

@@ -1,0 +1,118 @@
+"""Data-parallel strain-row training: one process per GPU, torch.distributed (RCCL under the "nccl"
+backend on ROCm; gloo for CPU / single-GPU tests). The reference is single-device (main.py:37);
+SURVEY.md §8e defines the sharding this module implements.
+
+Semantics:
+  * every rank draws the same global batch (same seeds) and runs the contiguous row share
+    `rank_slice` of it through the fused step;
+  * the gradient buffer is SUM-all-reduced in GM2_GRAD_BUCKETS contiguous buckets, each started on a
+    communication stream as soon as libgm2 has finalised it (gm2_wait_grad_bucket: a device-side
+    wait on the bucket's event), so the output-layer bucket's exchange runs under the rest of the
+    backward; L1, clip statistics and Adam then run on the reduced gradient, identically on every
+    rank (the losses are sum-reductions, so the reduced gradient is the global-batch gradient
+    except that train-mode BatchNorm normalises with each rank's own shard statistics, the
+    standard non-synchronised DDP BatchNorm);
+  * the per-batch loss sums stay on the device and are reduced once per epoch;
+  * BatchNorm running statistics are averaged over ranks at the end of every training epoch, so
+    validation, sampling and the saved checkpoint see one set of statistics on every rank. The
+    running-stat update is linear in the batch statistics, so one average per epoch equals the
+    average of per-step averages (up to fp32 rounding).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import native
+
+
+def get_dist():
+    """torch.distributed when a process group of more than one rank is initialised, else None."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist
+    return None
+
+
+def rank_world(dist=None):
+    dist = dist if dist is not None else get_dist()
+    return (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
+
+
+def rank_slice(n, rank, world):
+    """Contiguous share [lo, hi) of a global batch of n rows for `rank` of `world`."""
+    return (n * rank) // world, (n * (rank + 1)) // world
+
+
+class GradSync:
+    """Bucketed SUM all-reduce of the flat gradient buffer, overlapped with the backward."""
+
+    def __init__(self, dist, model, grads):
+        self.dist = dist
+        self.grads = grads
+        self.bounds = native.grad_bucket_bounds(native.dims(model.input_dim, model.hidden_dim,
+                                                            model.latent_dim, 1))
+        self.stream = torch.cuda.Stream(device=grads.device)
+
+    def after_backward(self, ran=True):
+        """Enqueue the bucket all-reduces behind the backward just launched (ran=True), or behind
+        whatever the current stream holds (ran=False: this rank contributed zeros)."""
+        cur = torch.cuda.current_stream(self.grads.device)
+        with torch.cuda.stream(self.stream):
+            if not ran:
+                self.stream.wait_stream(cur)
+            for b, (lo, hi) in enumerate(self.bounds):
+                if ran:
+                    native.wait_grad_bucket(b, self.stream)
+                self.dist.all_reduce(self.grads[lo:hi])
+        cur.wait_stream(self.stream)
+
+
+def reduce_loss_rows(dist, rec):
+    """SUM over ranks of the per-rank loss sums [BCE, sum p, KL] of every batch row of the epoch's
+    loss record (rec [nb][GM2_LOSS_SLOTS] fp64; slots 3-4 are post-reduction values already
+    identical on every rank). One contiguous exchange per epoch."""
+    part = rec[:, :3].contiguous()
+    dist.all_reduce(part)
+    rec[:, :3].copy_(part)
+
+
+def average_running_stats(dist, bn):
+    """Mean over ranks of the BatchNorm running statistics ([6][2][H] fp32, contiguous)."""
+    dist.all_reduce(bn)
+    bn.mul_(1.0 / dist.get_world_size())
+
+
+def broadcast_model(dist, model, src=0):
+    """Every rank starts from rank `src`'s parameters and statistics (the reference's init draws
+    from the unseeded global generator, so ranks would otherwise differ)."""
+    dist.broadcast(model.params, src)
+    dist.broadcast(model.bn, src)
+    model.touch()
+
+
+def shared_seed(dist, src=0):
+    """A seed drawn on rank `src` and broadcast, for identical host RNG streams on every rank."""
+    t = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
+    if dist.get_backend() == "nccl":
+        t = t.cuda()
+    dist.broadcast(t, src)
+    return int(t.item())
+
+
+def init_from_env(backend=None):
+    """torchrun entry (main.py): bind this process to LOCAL_RANK's GPU and initialise the process
+    group BEFORE any other GPU work. No-op for a single process. Returns the dist module or None."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    backend = backend or os.environ.get("GM2_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    return dist

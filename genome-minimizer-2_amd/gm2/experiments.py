@@ -18,6 +18,7 @@ import torch
 from . import native
 from .custom_config import ExperimentConfig
 from .data import ResidentMatrix, StrainLoader, load_and_validate_data, split_indices
+from .ddp import broadcast_model, get_dist, rank_world, shared_seed
 from .model import VAE
 from .trainer import Adam, StepLR, v0, v1, v2, v3
 
@@ -88,6 +89,8 @@ class IntegratedExperimentRunner:
         self.logger.info(f"Using device: {self.device}")
 
     def display_config(self):
+        if rank_world()[0] != 0:
+            return
         lines = ["=" * 80, "EXPERIMENT CONFIGURATION", "=" * 80,
                  f"Generated on: {datetime.now().strftime('%Y-%m-%d %H:%M:%S')}", ""]
         cats = {"Model Parameters": ["hidden_dim", "latent_dim"],
@@ -107,6 +110,10 @@ class IntegratedExperimentRunner:
         Path(self.figure_dir, f"{self.config.experiment_name}_config.txt").write_text(text)
 
     def prep_data(self):
+        dist = get_dist()
+        if dist:
+            # one host RNG stream on every rank: same loader permutations and eps draws
+            torch.manual_seed(shared_seed(dist))
         _, merged, _ = load_and_validate_data(self.dataset_csv, self.phylogroups_csv)
         data = merged.iloc[:, :-1].values
         self.phylogroups = merged["Phylogroup"].values
@@ -128,6 +135,9 @@ class IntegratedExperimentRunner:
         self.model = VAE(self.input_dim, c.hidden_dim, c.latent_dim, device=self.device, precision=self.precision)
         self.optimizer = Adam(self.model, lr=c.learning_rate)
         self.scheduler = StepLR(self.optimizer, step_size=c.scheduler_step_size, gamma=c.scheduler_gamma)
+        dist = get_dist()
+        if dist:
+            broadcast_model(dist, self.model)
         self.logger.info(f"Model parameters - Total: {self.model.n_params:,}, Trainable: {self.model.n_params:,}")
 
     def train_model(self, **kw):
@@ -139,7 +149,7 @@ class IntegratedExperimentRunner:
         self.logger.info(f"Training completed after {ep} epochs")
         self.logger.info(f"Final train loss: {tr[-1]:.4f}")
         self.logger.info(f"Final validation loss: {va[-1]:.4f}")
-        if c.save_model:
+        if c.save_model and rank_world()[0] == 0:
             path = os.path.join(self.model_dir, f"saved_VAE_{c.trainer_version}.pt")
             torch.save(self.model.state_dict(), path)
             self.results["model_path"] = path

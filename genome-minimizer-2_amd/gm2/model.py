@@ -187,8 +187,11 @@ class VAE:
         return ws
 
     def shadows_current(self, prec):
-        """Called after an in-kernel optimizer step that refreshed the shadows itself."""
-        self._shadow_stamp[prec] = self._version
+        """Called after an in-kernel optimizer step that updated the fp32 master AND refreshed the
+        `prec` shadows itself: the parameters changed (new version), only that workspace is current."""
+        self._version += 1
+        if prec in self._workspaces:
+            self._shadow_stamp[prec] = self._version
 
     # ---------------------------------------------------------------------- compute API
     def decode(self, z):

@@ -26,8 +26,9 @@ S_ONE_MINUS_B1, S_BETA2, S_ONE_MINUS_B2, S_ADAM_EPS = 6, 7, 8, 9
 EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_offsets",
            "gm2_workspace_size", "gm2_workspace_init", "gm2_sync_shadows", "gm2_train_fwd_bwd",
            "gm2_grad_norm", "gm2_adam_step", "gm2_eval_forward", "gm2_decode_mask", "gm2_encode",
-           "gm2_gemm", "gm2_timing_begin", "gm2_timing_end"]
+           "gm2_gemm", "gm2_grad_bucket_bounds", "gm2_wait_grad_bucket", "gm2_set_option", "gm2_get_option", "gm2_timing_begin", "gm2_timing_end"]
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
+OPT_GEMM_PP, OPT_SIDE_STREAM = 1, 2
 
 
 class Dims(C.Structure):
@@ -67,6 +68,10 @@ def lib():
         "gm2_decode_mask": (C.c_int, [dp, vp, vp, vp, i64, vp, i64, vp, i64, vp, vp]),
         "gm2_encode": (C.c_int, [dp, i32, C.POINTER(Batch), vp, vp, vp, vp, vp, vp]),
         "gm2_gemm": (C.c_int, [i32, i32, i32, vp, i64, vp, i64, vp, i64, i64, i64, i64, i32, vp, vp]),
+        "gm2_grad_bucket_bounds": (C.c_int, [dp, C.POINTER(C.c_int64)]),
+        "gm2_wait_grad_bucket": (C.c_int, [i32, vp]),
+        "gm2_set_option": (C.c_int, [i32, i32]),
+        "gm2_get_option": (C.c_int, [i32, C.POINTER(C.c_int)]),
         "gm2_timing_begin": (C.c_int, [i32]),
         "gm2_timing_end": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     }
@@ -167,6 +172,33 @@ def encode(ws: Workspace, batch: Batch, params, bn, mu, logvar):
 def gemm(prec, P, ldp, Q, ldq, Cout, ldc, M, N, K, splits=1, slab=None, p_kmajor=True, q_kmajor=True):
     check(lib().gm2_gemm(prec, int(p_kmajor), int(q_kmajor), ptr(P), ldp, ptr(Q), ldq, ptr(Cout), ldc, M, N, K,
                          splits, ptr(slab), stream()), "gm2_gemm")
+
+
+GRAD_BUCKETS = 3
+
+
+def grad_bucket_bounds(d: Dims):
+    """[(lo, hi)] element ranges of the flat gradient buffer, in backward completion order."""
+    lh = (C.c_int64 * (2 * GRAD_BUCKETS))()
+    check(lib().gm2_grad_bucket_bounds(C.byref(d), lh), "gm2_grad_bucket_bounds")
+    return [(lh[2 * i], lh[2 * i + 1]) for i in range(GRAD_BUCKETS)]
+
+
+def wait_grad_bucket(bucket: int, stream_obj):
+    """Make `stream_obj` (a torch.cuda.Stream) wait until gradient bucket `bucket` of the last
+    train_fwd_bwd on this device is final (device-side wait)."""
+    check(lib().gm2_wait_grad_bucket(int(bucket), C.c_void_p(stream_obj.cuda_stream)), "gm2_wait_grad_bucket")
+
+
+def set_option(key: int, value: int):
+    """Process-global tuning switch (gm2.h GM2_OPT_*)."""
+    check(lib().gm2_set_option(int(key), int(value)), "gm2_set_option")
+
+
+def get_option(key: int) -> int:
+    v = C.c_int()
+    check(lib().gm2_get_option(int(key), C.byref(v)), "gm2_get_option")
+    return v.value
 
 
 def timing_begin(classes: int):

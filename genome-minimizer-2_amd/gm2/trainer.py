@@ -8,11 +8,11 @@ backward launch sequence, the clip statistics and one fused L1+clip+Adam pass, a
 with the per-component batch losses kept on the device and read ONCE per epoch (the reference
 syncs with .item() per component per batch, trainer.py:52-55).
 
-Data parallel: with torch.distributed initialised (one process per GPU, RCCL), each rank runs its
-contiguous slice of every global batch; gradients are SUM-all-reduced before the clip statistics
-(reduction='sum' losses, so the sum over ranks is the global-batch gradient); the L1 term and the
-clip are applied once, after the reduction, identically on every rank. BatchNorm statistics are
-per rank (standard DDP).
+Data parallel (gm2/ddp.py): with torch.distributed initialised (one process per GPU,
+RCCL), each rank runs its contiguous slice of every global batch; the gradient buffer is
+SUM-all-reduced in buckets overlapped with the backward, before the clip statistics; the L1 term
+and the clip are applied once, after the reduction, identically on every rank. BatchNorm batch
+statistics are per rank (standard DDP); running statistics are averaged over ranks every epoch.
 """
 from __future__ import annotations
 
@@ -25,6 +25,7 @@ import torch
 
 from . import native
 from .data import StrainLoader, as_strain_loader
+from .ddp import GradSync, average_running_stats, get_dist, rank_slice, rank_world, reduce_loss_rows
 from .loss_components import (BUILTIN, GeneAbundanceLoss, KLDivergenceLoss, L1RegularizationLoss, LossComponent,
                               ReconstructionLoss)
 
@@ -149,28 +150,6 @@ class EarlyStopping:
         return self.epochs_no_improve >= self.patience
 
 
-def _dist():
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        return dist
-    return None
-
-
-def rank_slice(n, rank, world):
-    """Contiguous share [lo, hi) of a global batch of n rows for `rank` of `world` (SURVEY.md §8e:
-    one shuffled global permutation, identical on every rank, split contiguously)."""
-    return (n * rank) // world, (n * (rank + 1)) // world
-
-
-def reduce_batch(dist, grads, rec_row):
-    """The one data-path exchange of a DDP step: SUM of the per-rank gradients (the losses are
-    sum-reductions, so the sum over row shards is the full-batch gradient) and of the per-rank
-    loss sums [BCE, sum p, KL] of the loss record. L1, clipping and Adam follow on the reduced
-    values, identically on every rank."""
-    dist.all_reduce(grads)
-    dist.all_reduce(rec_row[:3])
-
-
 class VAETrainer:
     """trainer.py:84-189 on libgm2. `eps_rng`: 'device' draws the reparameterization noise with
     torch's generator on the model's device (what the reference does on a GPU: randn_like on a
@@ -189,6 +168,7 @@ class VAETrainer:
         self.scal = torch.zeros(native.NUM_SCALARS, dtype=torch.float32, device=self.device)
         self.grads = torch.zeros_like(model.params)
         self.last_grad_norm = None
+        self._sync = None
 
     def setup_loss_components(self, loss_components: List[LossComponent]):
         self.loss_tracker = LossTracker(loss_components)
@@ -229,10 +209,10 @@ class VAETrainer:
     def _bump_bn(self):
         self.model.num_batches_tracked = [n + 1 for n in self.model.num_batches_tracked]
 
-    def _rank_slice(self, n):
-        dist = _dist()
-        world, rank = (dist.get_world_size(), dist.get_rank()) if dist else (1, 0)
-        return rank_slice(n, rank, world)
+    def _grad_sync(self, dist):
+        if self._sync is None or self._sync.dist is not dist:
+            self._sync = GradSync(dist, self.model, self.grads)
+        return self._sync
 
     def _epoch_values(self, raw, pers, n_rows):
         epoch_losses = None
@@ -248,13 +228,13 @@ class VAETrainer:
 
     # ------------------------------------------------------------------------------ epochs
     def train_epoch(self, train_loader, epoch: int) -> Dict[str, float]:
-        """trainer.py:104-131. Per batch: fused fwd+bwd -> (all-reduce) -> clip stats -> Adam."""
+        """trainer.py:104-131. Per batch: fused fwd+bwd -> (bucketed all-reduce) -> clip stats -> Adam."""
         model = self.model
         model.train()
         loader = as_strain_loader(train_loader, self.device)
         mat = loader.matrix
-        dist = _dist()
-        world = dist.get_world_size() if dist else 1
+        dist = get_dist()
+        rank, world = rank_world(dist)
         batches = list(loader)   # draws the loader's seeds / permutation (reference order)
         for rows in batches:
             if rows.shape[0] == 1:
@@ -269,20 +249,30 @@ class VAETrainer:
         scal = self._upload(srows)
         ws = model.workspace(model.precision, (loader.batch_size + world - 1) // world)
         rec = torch.zeros(max(nb, 1), native.LOSS_SLOTS, dtype=torch.float64, device=self.device)
+        sync = self._grad_sync(dist) if dist else None
         for bi, rows in enumerate(batches):
             n = rows.shape[0]
-            lo, hi = self._rank_slice(n)
+            lo, hi = rank_slice(n, rank, world)
             eps = self._eps(n)[lo:hi].contiguous()
-            batch = native.make_batch(mat.data, mat.ld, rows[lo:hi], hi - lo, eps)
-            native.train_fwd_bwd(ws, batch, model.params, self.grads, model.bn, scal[bi], rec[bi])
-            if dist:
-                reduce_batch(dist, self.grads, rec[bi])
+            ran = hi - lo >= 2
+            if ran:
+                batch = native.make_batch(mat.data, mat.ld, rows[lo:hi], hi - lo, eps)
+                native.train_fwd_bwd(ws, batch, model.params, self.grads, model.bn, scal[bi], rec[bi])
+            else:
+                # DDP only: fewer than 2 of this global batch's rows landed on this rank; train-mode
+                # BatchNorm cannot run on them, so this rank contributes a zero gradient
+                self.grads.zero_()
+            if sync:
+                sync.after_backward(ran)
             native.grad_norm(ws, model.params, self.grads, scal[bi], rec[bi])
             native.adam_step(ws, model.params, self.grads, self.optimizer.exp_avg, self.optimizer.exp_avg_sq,
                              scal[bi])
             self.optimizer.step_count += 1
             model.shadows_current(model.precision)
             self._bump_bn()
+        if dist:
+            reduce_loss_rows(dist, rec)
+            average_running_stats(dist, model.bn)
         raw = rec.cpu().numpy()  # the epoch's one device->host sync
         if nb:
             self.last_grad_norm = float(raw[nb - 1, 4])
@@ -294,8 +284,8 @@ class VAETrainer:
         model.eval()
         loader = as_strain_loader(val_loader, self.device)
         mat = loader.matrix
-        dist = _dist()
-        world = dist.get_world_size() if dist else 1
+        dist = get_dist()
+        rank, world = rank_world(dist)
         batches = list(loader)
         nb = len(batches)
         pers, srows = [], []
@@ -308,7 +298,7 @@ class VAETrainer:
         rec = torch.zeros(max(nb, 1), native.LOSS_SLOTS, dtype=torch.float64, device=self.device)
         for bi, rows in enumerate(batches):
             n = rows.shape[0]
-            lo, hi = self._rank_slice(n)
+            lo, hi = rank_slice(n, rank, world)
             eps = self._eps(n)[lo:hi].contiguous()
             if hi > lo:
                 batch = native.make_batch(mat.data, mat.ld, rows[lo:hi], hi - lo, eps)
@@ -318,7 +308,7 @@ class VAETrainer:
             native.grad_norm(ws, model.params, self.grads, scal[0], rec[0])
             rec[1:, 3] = rec[0, 3]
         if dist:
-            dist.all_reduce(rec[:, :3])
+            reduce_loss_rows(dist, rec)
         raw = rec.cpu().numpy()
         return self._epoch_values(raw, pers, len(loader.dataset))
 
@@ -332,13 +322,14 @@ class VAETrainer:
             val_losses = self.validate_epoch(val_loader, epoch)
             self.loss_tracker.update_epoch_losses(val_losses, is_training=False)
             self.scheduler.step()
-            if (epoch + 1) % self.config.print_every == 0:
+            if (epoch + 1) % self.config.print_every == 0 and rank_world()[0] == 0:
                 print(f"Epoch {epoch + 1}:")
                 print(f"  Learning Rate: {self.scheduler.get_last_lr()[0]}")
                 print(f"  Train Loss: {train_losses['total']}")
                 print(f"  Validation Loss: {val_losses['total']}")
             if self.early_stopping.should_stop(val_losses["total"]):
-                print(f"Early stopping triggered after {epoch + 1} epochs")
+                if rank_world()[0] == 0:
+                    print(f"Early stopping triggered after {epoch + 1} epochs")
                 break
         return (self.loss_tracker.train_losses["total"], self.loss_tracker.val_losses["total"], epoch + 1)
 

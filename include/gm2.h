@@ -104,6 +104,17 @@ int gm2_train_fwd_bwd(const gm2_dims* d, int precision, const gm2_batch* batch, 
                       float* grads, float* bn_running, const float* scalars, double* loss, void* ws,
                       void* stream);
 
+/* Data-parallel gradient exchange. The flat gradient buffer is cut into
+ * GM2_GRAD_BUCKETS contiguous ranges in the order gm2_train_fwd_bwd finalises them:
+ *   0 = decoder.9.{weight,bias}, 1 = encoder.0.bias .. decoder.7.bias, 2 = encoder.0.weight.
+ * gm2_grad_bucket_bounds writes [lo, hi) element offsets per bucket (lo_hi[2*GM2_GRAD_BUCKETS]).
+ * gm2_wait_grad_bucket makes `stream` wait (device-side, no host sync) until that bucket of the
+ * most recent gm2_train_fwd_bwd on the current device is written, so a caller can start the
+ * all-reduce of bucket b on a communication stream while the rest of the backward still runs. */
+#define GM2_GRAD_BUCKETS 3
+int gm2_grad_bucket_bounds(const gm2_dims* d, int64_t* lo_hi);
+int gm2_wait_grad_bucket(int bucket, void* stream);
+
 /* L1 term + clip_grad_norm_ statistics (trainer.py:119; loss_components.py:167-184): computes
  * ||g + lambda*sign(theta)||_2 (loss slot [4]), sum|theta| (slot [3]) and the clip coefficient
  * min(1, max_norm/(norm+1e-6)) kept in the workspace for gm2_adam_step. */
@@ -132,6 +143,28 @@ int gm2_decode_mask(const gm2_dims* d, const float* params, const float* bn_runn
 int gm2_encode(const gm2_dims* d, int precision, const gm2_batch* batch, const float* params,
                const float* bn_running, float* mu, float* logvar, void* ws, void* stream);
 
+/* VAE.forward (model.py:109-113) as `model(x)`: encoder (BatchNorm in train mode — batch
+ * statistics + running-stat update — when `train`, else running stats), reparameterisation with
+ * the given batch->eps, decoder, probs fp32 [n][ld_probs] = sigmoid(logits); mu / logvar fp32 [n][L]
+ * (either may be NULL). The workspace keeps the activations for gm2_backward_outputs. */
+int gm2_forward(const gm2_dims* d, int precision, const gm2_batch* batch, const float* params, float* bn_running,
+                int train, float* probs, int64_t ld_probs, float* mu, float* logvar, void* ws, void* stream);
+
+/* Backward of the most recent gm2_forward on this workspace (same batch, same `train` mode) given
+ * upstream gradients dL/dprobs [n][ld_probs], dL/dmu and dL/dlogvar [n][L] (either may be NULL) —
+ * what torch autograd hands back to VAE.forward when a custom LossComponent is trained
+ * (trainer.py:349-352 with_custom_loss). Overwrites `grads` (flat, parameter order) with dL/dtheta
+ * through the whole VAE (train = 0: eval-mode BatchNorm, an affine map). */
+int gm2_backward_outputs(const gm2_dims* d, int precision, const gm2_batch* batch, const float* params, int train,
+                         const float* probs, int64_t ld_probs, const float* dprobs, const float* dmu,
+                         const float* dlogvar, float* grads, void* ws, void* stream);
+
+/* VAE.reparameterization (model.py:100-104) with the noise given: z = mu + exp(0.5*logvar)*eps over
+ * n elements; with dz != NULL also (or only, z = NULL) its backward dmu = dz,
+ * dlogvar = 0.5*dz*eps*exp(0.5*logvar). */
+int gm2_reparameterize(int64_t n, const float* mu, const float* logvar, const float* eps, float* z,
+                       const float* dz, float* dmu, float* dlogvar, void* stream);
+
 /* Raw GEMM primitive, exposed for kernel-level tests: C[M][ldc] (fp32) = sum_k P(m,k) Q(n,k).
  * p_kmajor / q_kmajor = 1: the operand is stored [rows][ld] with K contiguous (P(m,k) = P[m*ld+k]);
  * 0: stored [K][ld] with M (N) contiguous (P(m,k) = P[k*ld+m]). Elements of `precision` type;
@@ -148,6 +181,16 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  * own stream; gm2_timing_end synchronises those events and returns their summed duration and the
  * launch count. Classes: GM2_KC_RECON_LOSS (decoder output layer GEMM + fused BCE / dlogits
  * epilogue), GM2_KC_GEMM_STORE (every other GEMM), GM2_KC_MASK (sampling output layer GEMM). */
+/* Process-global tuning switches (no effect on results' semantics; both paths are parity-tested):
+ *   GM2_OPT_GEMM_PP     1 = ping-pong (4-phase, staggered wave groups) main loop for the 256x256
+ *                       bf16 GEMM tiles (default), 0 = two-stage loop. Initial value from env
+ *                       GM2_GEMM_PP (0 disables).
+ *   GM2_OPT_SIDE_STREAM 1 = weight-gradient GEMMs on a forked side stream (default), 0 = all on
+ *                       the caller's stream. Initial value from env GM2_SIDE_STREAM. */
+enum { GM2_OPT_GEMM_PP = 1, GM2_OPT_SIDE_STREAM = 2 };
+int gm2_set_option(int key, int value);
+int gm2_get_option(int key, int* value);
+
 enum { GM2_KC_RECON_LOSS = 1, GM2_KC_GEMM_STORE = 2, GM2_KC_MASK = 4 };
 int gm2_timing_begin(int kernel_classes);
 int gm2_timing_end(double* total_ms, int64_t* launches);

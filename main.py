@@ -14,6 +14,11 @@ exit with code 2 and a message. Data files are looked up under the project root 
 utils/directories.py:13-20 (default: $GM2_PROJECT_ROOT or the current directory; --project-root).
 Return codes follow main.py:647-692: 0 success, 1 failure.
 
+Multi-GPU (no reference equivalent; the reference is single-device, main.py:37):
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 main.py --mode training ...
+runs strain-row data parallelism over RCCL (gm2/ddp.py): every rank trains its share of each batch,
+rank 0 prints and saves the checkpoint. Other modes run on rank 0 only.
+
 Additions (no reference equivalent): --precision bf16|f32 for the training GEMMs (sampling always
 decodes in exact fp32), --mask-dtype float64|uint8 for the saved masks (the reference writes float64
 via `.astype(float)`, main.py:369-371 / extras.py:200-201; uint8 keeps 1e6-genome runs in memory),
@@ -201,6 +206,25 @@ def run_binary_converter(args):
 
 def main(argv=None):
     args = parse_arguments(argv)
+    dist = None
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # torchrun: one process per GPU; bind the device and join the process group before any
+        # other GPU work (strain-row data parallelism)
+        if args.mode != "training":
+            if int(os.environ.get("RANK", "0")) != 0:
+                return 0
+            print(f"--mode {args.mode} does not shard; running it on rank 0 only")
+        else:
+            from gm2.ddp import init_from_env
+            dist = init_from_env()
+    try:
+        return _main(args)
+    finally:
+        if dist is not None:
+            dist.destroy_process_group()
+
+
+def _main(args):
     print(f"\nRunning in {args.mode} mode (MI355X / gfx950 build)")
     if args.mode not in IMPLEMENTED:
         print(f"✗ --mode {args.mode} is outside the MI355X hot path of this build (SURVEY.md §2); "

@@ -1,8 +1,12 @@
-"""World-size-2 data-parallel step on CPU (gloo): the host side of the DDP path of gm2.trainer
-(rank_slice + reduce_batch, then clip + Adam on the reduced gradient) with the oracle standing in
-for the per-rank fused kernels. Checks that the shards partition every batch, that the reduced
-gradient and loss sums equal the sum of the per-shard values, and that both ranks end the step with
-bit-identical parameters (the property that lets every rank keep a full replica)."""
+"""World-size-2 data-parallel step on CPU (gloo): the host side of the DDP path (gm2/ddp.py:
+rank_slice, the gradient SUM, the per-epoch loss-record reduction, running-statistics averaging,
+then clip + Adam on the reduced gradient) with the oracle standing in for the per-rank fused
+kernels. Checks that the shards partition every batch, that the reduced gradient and loss sums equal
+the sum of the per-shard values for EVERY batch row of a multi-batch record (the round-1 strided
+view bug reduced the wrong elements), that slots 3-4 are left alone, that the running statistics
+end equal on both ranks, and that both ranks end the step with bit-identical parameters.
+The GPU path of the same code (bucketed, backward-overlapped all-reduce through libgm2's bucket
+events, VAETrainer epochs) is tests/test_gpu_ddp.py."""
 import os
 import socket
 
@@ -11,7 +15,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from gm2.trainer import rank_slice, reduce_batch
+from gm2.ddp import average_running_stats, rank_slice, reduce_loss_rows
 from oracle import vae_oracle as O
 
 G, H, L, B = 40, 16, 4, 27
@@ -52,7 +56,16 @@ def _worker(rank, world, port, out_dir):
     g, rec = _shard_step(P, S, x, eps, lo, hi)
     names = list(P.keys())
     flat = torch.cat([g[n].reshape(-1) for n in names])
-    reduce_batch(dist, flat, rec)
+    dist.all_reduce(flat)
+    # a 3-batch epoch record: row b holds this rank's sums scaled by (b+1); slots 3-4 are
+    # post-reduction values (identical on every rank) and must not be summed
+    recs = torch.stack([rec * (b + 1) for b in range(3)])
+    recs[:, 3] = 11.0
+    recs[:, 4] = 7.0
+    reduce_loss_rows(dist, recs)
+    # per-rank running statistics -> their mean
+    bn = torch.full((6, 2, H), float(rank + 1))
+    average_running_stats(dist, bn)
     # unflatten, clip on the reduced gradient, Adam: identical on every rank
     red, off = {}, 0
     for n in names:
@@ -62,8 +75,8 @@ def _worker(rank, world, port, out_dir):
     O.clip_grads(red, 1.0)
     O.adam_step(P, red, O.AdamState())
     params = torch.cat([P[n].reshape(-1) for n in names])
-    np.savez(os.path.join(out_dir, f"r{rank}.npz"), grad=flat.numpy(), rec=rec.numpy(), params=params.numpy(),
-             lo=lo, hi=hi)
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), grad=flat.numpy(), rec=recs.numpy(), params=params.numpy(),
+             bn=bn.numpy(), lo=lo, hi=hi)
     dist.destroy_process_group()
 
 
@@ -92,7 +105,12 @@ def test_two_rank_step(tmp_path):
         exp_g = exp_g + torch.cat([g[n].reshape(-1) for n in names]).numpy()
         exp_rec = exp_rec + rec.numpy()
     np.testing.assert_allclose(r0["grad"], exp_g, rtol=1e-6, atol=1e-7)
-    np.testing.assert_allclose(r0["rec"][:3], exp_rec[:3], rtol=1e-12)
+    for b in range(3):
+        for r in (r0, r1):
+            np.testing.assert_allclose(r["rec"][b, :3], (b + 1) * exp_rec[:3], rtol=1e-12)
+            assert r["rec"][b, 3] == 11.0 and r["rec"][b, 4] == 7.0
+    np.testing.assert_array_equal(r0["bn"], np.full((6, 2, H), 1.5, np.float32))
+    np.testing.assert_array_equal(r1["bn"], r0["bn"])
 
 
 @pytest.mark.parametrize("world", [2])

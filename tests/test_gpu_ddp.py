@@ -1,0 +1,175 @@
+"""Data-parallel VAETrainer on the GPU: world size 2 (gloo, two processes on the one MI355X, each
+running libgm2) driving the real `train_epoch` / `validate_epoch` of gm2.trainer, with the
+bucketed backward-overlapped gradient all-reduce of gm2.ddp.GradSync (bucket events from
+gm2_wait_grad_bucket), against the oracle's per-shard math:
+
+  * the reduced data gradient of a step == sum over the two row shards of the oracle's explicit
+    gradient, each shard normalised with its OWN BatchNorm batch statistics;
+    f32 path: rel 1e-4 per tensor (pre-BN Linear biases: absolute, they are rounding noise);
+  * the epoch's training loss components == the oracle's per-shard sums (rel 1e-5);
+  * running statistics == mean over ranks of the per-shard momentum updates, equal on both ranks;
+  * parameters bit-identical on both ranks after the step (replicas stay in lock step);
+  * a 3-batch validation epoch (64 + 64 + 22 rows, each split over the ranks) == the oracle's
+    eval-mode losses of the same rows with the GPU's own final parameters (rel 1e-5), i.e. every
+    batch row of the loss record is reduced (the round-1 strided-view bug summed the wrong ones).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from gpu_helpers import perturb_bn, synth_x
+from oracle import vae_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+G, H, L = 700, 128, 16
+N_TRAIN, N_VAL, BS = 64, 150, 64
+SEED = 1234
+BETA_KW = dict(scheduler_type="cosine", min_beta=0.1, max_beta=1.0, T=10)
+GAMMA_KW = dict(gamma_start=1.0, gamma_end=0.1, weight=1.0)
+LAM = 0.01
+N_EPOCHS = 10
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _state():
+    torch.manual_seed(SEED)
+    P = O.init_params(G, H, L)
+    S = O.init_bn_state(H)
+    return perturb_bn(P, S, 77)
+
+
+def _data():
+    return synth_x(N_TRAIN, G, 3), synth_x(N_VAL, G, 4)
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gm2 import native
+    from gm2.data import ResidentMatrix, StrainLoader
+    from gm2.loss_components import GeneAbundanceLoss, KLDivergenceLoss, L1RegularizationLoss, ReconstructionLoss
+    from gm2.model import VAE
+    from gm2.trainer import Adam, StepLR, TrainingConfig, VAETrainer
+
+    P, S = _state()
+    m = VAE(G, H, L, precision=native.GM2_F32, init=False)
+    m.load_state_dict({**P, **S})
+    opt = Adam(m, lr=1e-3)
+    sch = StepLR(opt, 20, 0.5)
+    tr = VAETrainer(m, opt, sch, TrainingConfig(n_epochs=N_EPOCHS, max_norm=1.0, lambda_l1=LAM), eps_rng="cpu")
+    tr.setup_loss_components([ReconstructionLoss(), KLDivergenceLoss(**BETA_KW), GeneAbundanceLoss(**GAMMA_KW),
+                              L1RegularizationLoss(LAM)])
+    xt, xv = _data()
+    torch.manual_seed(SEED + 1)  # identical host RNG on both ranks: loader seeds and eps draws
+    tl = StrainLoader(ResidentMatrix(xt), None, BS, shuffle=True)
+    vl = StrainLoader(ResidentMatrix(xv), None, BS, shuffle=False)
+    tr_losses = tr.train_epoch(tl, 0)
+    torch.cuda.synchronize()
+    out = dict(grads=tr.grads.cpu().numpy(), params=m.params.cpu().numpy(), bn=m.bn.cpu().numpy(),
+               tr=np.array([tr_losses[k] for k in sorted(tr_losses)]))
+    va_losses = tr.validate_epoch(vl, 0)
+    out["va"] = np.array([va_losses[k] for k in sorted(va_losses)])
+    out["keys"] = np.array(sorted(va_losses))
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), **out)
+    dist.destroy_process_group()
+
+
+def _shard_sums(P, S, x, eps, train):
+    recon, mu, lv = O.forward(P, S, x, eps, train=train)
+    bce = torch.nn.functional.binary_cross_entropy(recon, x, reduction="sum").double().item()
+    return bce, recon.sum().double().item(), torch.sum(1 + lv - mu.pow(2) - lv.exp()).double().item()
+
+
+def test_two_rank_trainer_epoch(tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = np.load(tmp_path / "r0.npz"), np.load(tmp_path / "r1.npz")
+    np.testing.assert_array_equal(r0["params"], r1["params"])
+    np.testing.assert_array_equal(r0["bn"], r1["bn"])
+    np.testing.assert_array_equal(r0["grads"], r1["grads"])
+    np.testing.assert_array_equal(r0["va"], r1["va"])
+
+    # ---- oracle: replay the trainer's host RNG use (loader base seed + sampler seed + randperm,
+    # then one eps draw per batch) and the per-shard math
+    P, S = _state()
+    xt, xv = _data()
+    torch.manual_seed(SEED + 1)
+    torch.empty((), dtype=torch.int64).random_()
+    perm = O.loader_perm(N_TRAIN)
+    x = torch.tensor(xt[perm.numpy()], dtype=torch.float32)
+    eps = torch.randn(N_TRAIN, L)
+    ls = O.LossState(O.Preset("t", "cosine", 0.1, 1.0, T=10, gamma_start=1.0, gamma_end=0.1, lambda_l1=LAM),
+                     N_EPOCHS)
+    beta = ls.beta(0)
+    gamma = ls.gamma(0)
+    grads, sums, bn_new = None, np.zeros(3), {k: 0.0 for k in S if "running" in k}
+    for lo, hi in ((0, N_TRAIN // 2), (N_TRAIN // 2, N_TRAIN)):
+        g = O.manual_grads(P, S, x[lo:hi], eps[lo:hi], beta, gamma, 0.0)
+        grads = g if grads is None else {k: grads[k] + g[k] for k in g}
+        S2 = {k: v.clone() for k, v in S.items()}
+        sums += np.array(_shard_sums(P, S2, x[lo:hi], eps[lo:hi], True))
+        for k in bn_new:
+            bn_new[k] = bn_new[k] + S2[k] / 2
+    # gradient per tensor (the libgm2 layout is model.parameters() order)
+    off = np.cumsum([0] + [int(np.prod(s)) for _, s in O.param_specs(G, H, L)])
+    fails = []
+    for i, (name, _) in enumerate(O.param_specs(G, H, L)):
+        got = r0["grads"][off[i]:off[i + 1]]
+        ref = grads[name].reshape(-1).numpy()
+        parts = name.split(".")
+        if parts[0] in ("encoder", "decoder") and parts[1] in ("0", "3", "6") and parts[2] == "bias":
+            scale = float(np.abs(grads[name.replace("bias", "weight")].numpy()).max())
+            if np.abs(got).max() > 1e-3 * scale:
+                fails.append(f"{name}: |g| {np.abs(got).max():.3g} vs weight scale {scale:.3g}")
+            continue
+        e = float(np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-30))
+        if e > 1e-4:
+            fails.append(f"{name}: rel err {e:.3g}")
+    assert not fails, "\n".join(fails)
+    # running statistics: mean of the two shards' momentum updates
+    for i, b in enumerate(O.BNS):
+        np.testing.assert_allclose(r0["bn"][i, 0], bn_new[b + ".running_mean"].numpy(), rtol=2e-5, atol=2e-6)
+        np.testing.assert_allclose(r0["bn"][i, 1], bn_new[b + ".running_var"].numpy(), rtol=2e-5, atol=2e-6)
+    # training losses of the epoch (one batch): components from the summed shard values
+    keys = list(r0["keys"])
+    tr = dict(zip(keys, r0["tr"]))
+    l1 = sum(v.abs().sum().item() for v in P.values())
+    exp = {"reconstruction": sums[0] / N_TRAIN, "gene_abundance": np.float32(gamma) * sums[1] / N_TRAIN,
+           "kl_divergence": np.float32(beta) * (-0.5 * sums[2]) / N_TRAIN,
+           "l1_regularization": LAM * l1 / N_TRAIN}
+    for k, v in exp.items():
+        assert abs(tr[k] - v) <= 1e-5 * abs(v) + 1e-7, (k, tr[k], v)
+
+    # ---- validation epoch with the GPU's own final parameters and averaged running statistics
+    Pf = O.unflatten(r0["params"], G, H, L)
+    Sf = {k: v.clone() for k, v in S.items()}
+    for i, b in enumerate(O.BNS):
+        Sf[b + ".running_mean"] = torch.tensor(r0["bn"][i, 0])
+        Sf[b + ".running_var"] = torch.tensor(r0["bn"][i, 1])
+    torch.empty((), dtype=torch.int64).random_()  # the val loader's base seed
+    xv_t = torch.tensor(xv, dtype=torch.float32)
+    vs = np.zeros(3)
+    betas, n_b = [], 0
+    for s0 in range(0, N_VAL, BS):
+        xb = xv_t[s0:s0 + BS]
+        eb = torch.randn(xb.shape[0], L)
+        betas.append(ls.beta(0))
+        bce, ps, kl = _shard_sums(Pf, Sf, xb, eb, False)
+        vs += [bce, np.float32(gamma) * ps, np.float32(betas[-1]) * (-0.5 * kl)]
+        n_b += 1
+    va = dict(zip(keys, r0["va"]))
+    assert n_b == 3
+    for k, v in zip(["reconstruction", "gene_abundance", "kl_divergence"], vs):
+        assert abs(va[k] - v / N_VAL) <= 1e-5 * abs(v / N_VAL) + 1e-7, (k, va[k], v / N_VAL)

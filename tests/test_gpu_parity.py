@@ -29,6 +29,15 @@ if torch.cuda.is_available():
     from gm2.data import ResidentMatrix
 
 
+@pytest.fixture(params=[0, 1], ids=["loop2", "pingpong"])
+def gemm_pp(request):
+    """Both main loops of the 256x256 bf16 tiles (gm2_set_option GM2_OPT_GEMM_PP)."""
+    old = native.get_option(native.OPT_GEMM_PP)
+    native.set_option(native.OPT_GEMM_PP, request.param)
+    yield request.param
+    native.set_option(native.OPT_GEMM_PP, old)
+
+
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
 @pytest.mark.parametrize("prec", ["f32", "bf16"])
 @pytest.mark.parametrize("M,N,K,splits", [(128, 128, 64, 1), (200, 300, 192, 1), (256, 1024, 1024, 1),
@@ -36,7 +45,7 @@ if torch.cuda.is_available():
                                           # 256x256 ping-pong tiles: >= 256 tiles (nk = 1, 3), and the
                                           # long-K plan (big tiles + 8 split-K slices)
                                           (4000, 4096, 64, 1), (4096, 4000, 192, 1), (512, 512, 8192, -1)])
-def test_gemm(prec, layout, M, N, K, splits):
+def test_gemm(prec, layout, M, N, K, splits, gemm_pp):
     """C = P.Q^T with each operand K-major ([rows][K]) or MN-major ([K][rows], read through
     ds_read_b64_tr_b16 / ds_read_b32): nt = both K-major (forward), nn = Q MN-major (input
     gradients), tn = both MN-major (weight gradients). fp32 accumulation of exact products."""
@@ -60,6 +69,39 @@ def test_gemm(prec, layout, M, N, K, splits):
     scale = (P[:M].double().abs() @ Q[:N].double().abs().T).max().item()
     assert torch.isfinite(C).all()
     assert err <= 2e-6 * scale, (err, scale)
+
+
+# The GEMMs of the v0 C2 step (B=4096, G=55,039 -> Gp=55,040, H=1024) at their real sizes, through
+# gm2_gemm with the hot path's own tile / split plan (splits=-1); fp64 reference computed on the
+# device from the same bf16 operands. (55040, 1024, 4096, tn) is the shape that faulted in the
+# round-1 microbenchmark (gpurun_out/gemm_g1.log); (55039, ...) is the unpadded hot-path M.
+@pytest.mark.parametrize("name,layout,M,N,K", [("dW9", "tn", 55040, 1024, 4096), ("dW9u", "tn", 55039, 1024, 4096),
+                                               ("dWe0", "tn", 1024, 55040, 4096), ("enc0", "nt", 4096, 1024, 55040),
+                                               ("dA5", "nn", 4096, 1024, 55040), ("hid", "nt", 4096, 1024, 1024),
+                                               ("hid_dX", "nn", 4096, 1024, 1024), ("hid_dW", "tn", 1024, 1024, 4096)])
+def test_gemm_hot_shapes(name, layout, M, N, K, gemm_pp):
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    Mp, Np = -(-M // 128) * 128, -(-N // 128) * 128
+    pk, qk = {"nt": (True, True), "nn": (True, False), "tn": (False, False)}[layout]
+    Ps = (torch.rand((Mp, K) if pk else (K, Mp), generator=g, device=dev) * 2 - 1).bfloat16()
+    Qs = (torch.rand((Np, K) if qk else (K, Np), generator=g, device=dev) * 2 - 1).bfloat16()
+    if pk:
+        Ps[M:] = 0
+    else:
+        Ps[:, M:] = 0
+    C = torch.full((M, N), float("nan"), device=dev)
+    slab = torch.empty(8 * M * N + 4, device=dev)
+    native.gemm(native.GM2_BF16, Ps, Ps.shape[1], Qs, Qs.shape[1], C, N, M, N, K, -1, slab, pk, qk)
+    Pm = (Ps if pk else Ps.t())[:M].double()
+    Qm = (Qs if qk else Qs.t())[:N].double()
+    ref = Pm @ Qm.t()
+    torch.cuda.synchronize()
+    assert torch.isfinite(C).all()
+    err = (C.double() - ref).abs().max().item()
+    scale = (Pm.abs() @ Qm.abs().t()).max().item()
+    assert err <= 2e-6 * scale, (name, err, scale)
+    del Ps, Qs, C, slab, ref
 
 
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
@@ -128,8 +170,10 @@ def _prebn_bias(name):
 
 @pytest.mark.parametrize("prec", ["f32", "bf16"])
 @pytest.mark.parametrize("G,H,L,B,wg,lam", [(300, 128, 16, 200, 0.0, 0.0), (517, 256, 32, 130, 0.55, 0.01),
-                                            (1000, 128, 64, 64, 1.2, 0.01)])
-def test_train_step_vs_oracle(prec, G, H, L, B, wg, lam):
+                                            (1000, 128, 64, 64, 1.2, 0.01),
+                                            # >= 128 256x256 output tiles: the big-tile recon kernel
+                                            (8192, 256, 32, 1024, 0.55, 0.01)])
+def test_train_step_vs_oracle(prec, G, H, L, B, wg, lam, gemm_pp):
     """One fused fwd+bwd (+clip+L1+Adam) against the oracle's explicit gradients and its
     autograd-driven step (trainer.py:109-120 semantics)."""
     P, S = perturb_bn(*oracle_state(G, H, L, G + B), seed=9)

@@ -11,7 +11,7 @@ rc=$?; echo "gemm tests rc=$rc" >> gpurun_out/gemm_tests_$TAG.log
 timeout -k 10 900 python3 -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/gpu_tests_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/gpu_tests_$TAG.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python3 tools_gemm_bench.py 20 > gpurun_out/gemm_$TAG.log 2>&1
+timeout -k 10 300 python3 tools/gemm_bench.py 20 > gpurun_out/gemm_$TAG.log 2>&1
 rc=$?; echo "gemm bench rc=$rc" >> gpurun_out/gemm_$TAG.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/bench_$TAG.log 2>&1

@@ -4,7 +4,7 @@
 MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE
 reports half the bytes of a wide coalesced streaming read, so it is doubled here. Values are the
 median over the launches of each (kernel, grid) pair. Usage:
-    python3 tools_pmc.py gpurun_out/pmc_fetch_TAG gpurun_out/pmc_write_TAG profiles/rNN_pmc_traffic.json
+    python3 tools/pmc.py gpurun_out/pmc_fetch_TAG gpurun_out/pmc_write_TAG profiles/rNN_pmc_traffic.json
 """
 import collections
 import csv
