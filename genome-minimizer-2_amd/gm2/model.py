@@ -194,8 +194,54 @@ class VAE:
             self._shadow_stamp[prec] = self._version
 
     # ---------------------------------------------------------------------- compute API
+    # ------------------------------------------------------------- reference module surface
+    def requires_grad_(self, flag=True):
+        """Let torch autograd track the flat parameter buffer (VAE.forward's backward then writes
+        dL/dtheta into self.params.grad, parameter views included)."""
+        self.params.requires_grad_(flag)
+        return self
+
+    def zero_grad(self, set_to_none=True):
+        self.params.grad = None
+
+    def reparameterization(self, mean, logvar):
+        """z = mean + exp(0.5*logvar) * randn_like(std) (model.py:100-104), on libgm2's kernel,
+        differentiable (torch autograd) in mean and logvar."""
+        eps = torch.randn_like(logvar)
+        return _Reparam.apply(mean, logvar, eps)
+
+    def forward(self, x, eps=None):
+        """(x_hat, mean, logvar) = model(x) (model.py:109-113) through libgm2: encoder with
+        BatchNorm in the module's train/eval mode (train mode updates the running statistics),
+        reparameterisation (eps ~ N(0, I) drawn on the device like randn_like, unless given),
+        decoder, sigmoid. x: a 0/1 tensor [B, G] (any dtype), a ResidentMatrix, or a
+        (ResidentMatrix, int32 row-index tensor) pair. Differentiable under torch autograd in the
+        parameters (self.params, after requires_grad_()) through gm2_backward_outputs, so
+        arbitrary LossComponents can be trained on it (trainer.py:349-352)."""
+        from .data import ResidentMatrix
+        if isinstance(x, tuple):
+            mat, rows = x
+        else:
+            mat, rows = (x if isinstance(x, ResidentMatrix) else ResidentMatrix(x, device=self.device)), None
+        n = int(rows.shape[0]) if rows is not None else mat.n
+        if self.training and n < 2:
+            raise ValueError(f"Expected more than 1 value per channel when training, got input size [1, {self.hidden_dim}]")
+        if eps is None:
+            eps = torch.randn(n, self.latent_dim, device=self.device)
+        eps = eps.to(self.device, torch.float32).contiguous()
+        out = _Forward.apply(self.params, self, mat, rows, n, eps)
+        if self.training:
+            self.num_batches_tracked = [k + 1 for k in self.num_batches_tracked]
+        return out
+
+    __call__ = forward
+
     def decode(self, z):
-        """p = sigmoid(decoder(z)) in eval mode, exact fp32 (model.py:106-107)."""
+        """p = sigmoid(decoder(z)) (model.py:106-107), exact fp32. Eval mode (running statistics):
+        every reference call site decodes a loaded, eval()'d model (extras.py:185-198)."""
+        if self.training:
+            raise RuntimeError("VAE.decode on this build runs eval-mode BatchNorm; call model.eval() first "
+                               "(train-mode decoding runs inside model(x))")
         _, p = self.decode_mask(z, want_probs=True)
         return p
 
@@ -214,7 +260,8 @@ class VAE:
         return mask, probs
 
     def encode(self, x):
-        """(mean, logvar) of the eval-mode encoder (model.py:95-98) for a 0/1 matrix x [B, G]."""
+        """(mean, logvar) of the eval-mode encoder (model.py:95-98) for a 0/1 matrix x [B, G]
+        (every reference call site encodes an eval()'d model: extras.py:205-228)."""
         from .data import ResidentMatrix
         m = x if isinstance(x, ResidentMatrix) else ResidentMatrix(x, device=self.device)
         B = m.n
@@ -227,3 +274,58 @@ class VAE:
     def __repr__(self):
         return (f"VAE(input_dim={self.input_dim}, hidden_dim={self.hidden_dim}, latent_dim={self.latent_dim}, "
                 f"device={self.device}, precision={'fp32' if self.precision == native.GM2_F32 else 'bf16'})")
+
+
+class _Forward(torch.autograd.Function):
+    """model(x) on libgm2 with a libgm2 backward (gm2_forward / gm2_backward_outputs). The
+    workspace keeps the forward's activations; a later forward on the same model invalidates them
+    (the backward checks a token and raises)."""
+
+    @staticmethod
+    def forward(ctx, params, model, mat, rows, n, eps):
+        dev = model.device
+        G, L = model.input_dim, model.latent_dim
+        ws = model.workspace(model.precision, n)
+        probs = torch.empty(n, G, device=dev)
+        mu = torch.empty(n, L, device=dev)
+        lv = torch.empty(n, L, device=dev)
+        batch = native.make_batch(mat.data, mat.ld, rows, n, eps)
+        native.forward(ws, batch, params.detach(), model.bn, int(model.training), probs, G, mu, lv)
+        model._fwd_token = getattr(model, "_fwd_token", 0) + 1
+        ctx.model, ctx.mat, ctx.rows, ctx.n, ctx.token, ctx.train = model, mat, rows, n, model._fwd_token, model.training
+        ctx.save_for_backward(probs, eps)
+        return probs, mu, lv
+
+    @staticmethod
+    def backward(ctx, dprobs, dmu, dlv):
+        m = ctx.model
+        if m._fwd_token != ctx.token:
+            raise RuntimeError("VAE.forward activations were overwritten by a later forward of the same model; "
+                               "call backward before the next forward")
+        probs, eps = ctx.saved_tensors
+        if dprobs is None:
+            dprobs = torch.zeros_like(probs)
+        grads = torch.empty_like(m.params)
+        ws = m.workspace(m.precision, ctx.n)
+        batch = native.make_batch(ctx.mat.data, ctx.mat.ld, ctx.rows, ctx.n, eps)
+        native.backward_outputs(ws, batch, m.params.detach(), int(ctx.train), probs, m.input_dim,
+                                dprobs.contiguous(), None if dmu is None else dmu.contiguous(),
+                                None if dlv is None else dlv.contiguous(), grads)
+        return grads, None, None, None, None, None
+
+
+class _Reparam(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mean, logvar, eps):
+        mean, logvar, eps = (t.contiguous().float() for t in (mean, logvar, eps))
+        z = torch.empty_like(mean)
+        native.reparameterize(mean.numel(), mean, logvar, eps, z)
+        ctx.save_for_backward(mean, logvar, eps)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        mean, logvar, eps = ctx.saved_tensors
+        dmu, dlv = torch.empty_like(mean), torch.empty_like(mean)
+        native.reparameterize(mean.numel(), mean, logvar, eps, None, dz.contiguous(), dmu, dlv)
+        return dmu, dlv, None

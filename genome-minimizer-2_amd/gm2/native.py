@@ -25,7 +25,8 @@ S_ONE_MINUS_B1, S_BETA2, S_ONE_MINUS_B2, S_ADAM_EPS = 6, 7, 8, 9
 
 EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_offsets",
            "gm2_workspace_size", "gm2_workspace_init", "gm2_sync_shadows", "gm2_train_fwd_bwd",
-           "gm2_grad_norm", "gm2_adam_step", "gm2_eval_forward", "gm2_decode_mask", "gm2_encode",
+           "gm2_grad_norm", "gm2_adam_step", "gm2_eval_forward", "gm2_decode_mask", "gm2_encode", "gm2_forward", "gm2_backward_outputs",
+           "gm2_reparameterize",
            "gm2_gemm", "gm2_grad_bucket_bounds", "gm2_wait_grad_bucket", "gm2_set_option", "gm2_get_option", "gm2_timing_begin", "gm2_timing_end"]
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
 OPT_GEMM_PP, OPT_SIDE_STREAM = 1, 2
@@ -67,6 +68,9 @@ def lib():
         "gm2_eval_forward": (C.c_int, [dp, i32, C.POINTER(Batch), vp, vp, vp, vp, vp, vp]),
         "gm2_decode_mask": (C.c_int, [dp, vp, vp, vp, i64, vp, i64, vp, i64, vp, vp]),
         "gm2_encode": (C.c_int, [dp, i32, C.POINTER(Batch), vp, vp, vp, vp, vp, vp]),
+        "gm2_forward": (C.c_int, [dp, i32, C.POINTER(Batch), vp, vp, i32, vp, i64, vp, vp, vp, vp]),
+        "gm2_backward_outputs": (C.c_int, [dp, i32, C.POINTER(Batch), vp, i32, vp, i64, vp, vp, vp, vp, vp, vp]),
+        "gm2_reparameterize": (C.c_int, [i64, vp, vp, vp, vp, vp, vp, vp, vp]),
         "gm2_gemm": (C.c_int, [i32, i32, i32, vp, i64, vp, i64, vp, i64, i64, i64, i64, i32, vp, vp]),
         "gm2_grad_bucket_bounds": (C.c_int, [dp, C.POINTER(C.c_int64)]),
         "gm2_wait_grad_bucket": (C.c_int, [i32, vp]),
@@ -167,6 +171,22 @@ def decode_mask(ws: Workspace, params, bn, z, n, mask, ld_mask, probs=None, ld_p
 def encode(ws: Workspace, batch: Batch, params, bn, mu, logvar):
     check(lib().gm2_encode(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), ptr(bn), ptr(mu), ptr(logvar),
                            ws.ptr, stream()), "gm2_encode")
+
+
+def forward(ws: Workspace, batch: Batch, params, bn, train, probs, ld_probs, mu=None, logvar=None):
+    check(lib().gm2_forward(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), ptr(bn), int(train), ptr(probs),
+                            int(ld_probs), ptr(mu), ptr(logvar), ws.ptr, stream()), "gm2_forward")
+
+
+def backward_outputs(ws: Workspace, batch: Batch, params, train, probs, ld_probs, dprobs, dmu, dlogvar, grads):
+    check(lib().gm2_backward_outputs(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), int(train), ptr(probs),
+                                     int(ld_probs), ptr(dprobs), ptr(dmu), ptr(dlogvar), ptr(grads), ws.ptr,
+                                     stream()), "gm2_backward_outputs")
+
+
+def reparameterize(n, mu, logvar, eps, z, dz=None, dmu=None, dlogvar=None):
+    check(lib().gm2_reparameterize(int(n), ptr(mu), ptr(logvar), ptr(eps), ptr(z), ptr(dz), ptr(dmu), ptr(dlogvar),
+                                   stream()), "gm2_reparameterize")
 
 
 def gemm(prec, P, ldp, Q, ldq, Cout, ldc, M, N, K, splits=1, slab=None, p_kmajor=True, q_kmajor=True):

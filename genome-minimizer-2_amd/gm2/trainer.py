@@ -26,8 +26,8 @@ import torch
 from . import native
 from .data import StrainLoader, as_strain_loader
 from .ddp import GradSync, average_running_stats, get_dist, rank_slice, rank_world, reduce_loss_rows
-from .loss_components import (BUILTIN, GeneAbundanceLoss, KLDivergenceLoss, L1RegularizationLoss, LossComponent,
-                              ReconstructionLoss)
+from .loss_components import (GeneAbundanceLoss, KLDivergenceLoss, L1RegularizationLoss, LossComponent,
+                              ReconstructionLoss, fused_supported)
 
 
 @dataclass
@@ -85,19 +85,16 @@ class StepLR:
         return [self.optimizer.param_groups[0]["lr"]]
 
 
+def _dist_world():
+    return rank_world()[1]
+
+
 class LossTracker:
     """trainer.py:34-62 (per-epoch lists of epoch-averaged component losses)."""
 
     def __init__(self, loss_components: List[LossComponent]):
-        for c in loss_components:
-            if not isinstance(c, BUILTIN):
-                raise NotImplementedError(
-                    f"loss component {type(c).__name__} is not one of the fused built-ins "
-                    "(Reconstruction, KLDivergence, GeneAbundance, L1Regularization)")
-        names = [type(c) for c in loss_components]
-        if ReconstructionLoss not in names:
-            raise NotImplementedError("the fused path always evaluates the reconstruction term; include it")
         self.loss_components = loss_components
+        self.fused = fused_supported(loss_components)
         self.train_losses = {c.get_name(): [] for c in loss_components}
         self.val_losses = {c.get_name(): [] for c in loss_components}
         self.train_losses["total"] = []
@@ -125,6 +122,17 @@ class LossTracker:
             total = np.float32(total + v)
         out["total"] = float(total)
         return out
+
+    def compute_total_loss(self, recon_x, data, mu, logvar, model, epoch, batch_idx, is_training=True):
+        """trainer.py:44-56 (the autograd path): components in list order, each .item()'d."""
+        individual = {}
+        total = torch.tensor(0.0, device=recon_x.device)
+        for c in self.loss_components:
+            loss = c.compute_loss(recon_x, data, mu, logvar, model, epoch, batch_idx)
+            individual[c.get_name()] = loss.item()
+            total += loss
+        individual["total"] = total.item()
+        return total, individual
 
     def update_epoch_losses(self, epoch_losses: Dict[str, float], is_training=True):
         d = self.train_losses if is_training else self.val_losses
@@ -227,8 +235,61 @@ class VAETrainer:
         return {k: v / n_rows for k, v in epoch_losses.items()}
 
     # ------------------------------------------------------------------------------ epochs
+    # ------------------------------------------------ autograd path (non-fused loss compositions)
+    def _gather(self, mat, rows):
+        """data = batch[0].to(float) (trainer.py:110): the batch's rows as fp32 [n, G] on the device."""
+        return mat.data.index_select(0, rows.long())[:, :self.model.input_dim].float()
+
+    def _epoch_autograd(self, loader, epoch, training):
+        """trainer.py:104-156 with model(data) = libgm2's forward (VAE.forward), the components'
+        compute_loss in torch, total.backward() through gm2_backward_outputs, then libgm2's clip
+        statistics and Adam on the autograd gradient (L1 et al. are already in it)."""
+        model = self.model
+        if _dist_world() > 1:
+            raise NotImplementedError("data-parallel training runs the fused loss path only (built-in components)")
+        model.train(training)
+        mat = loader.matrix
+        batches = list(loader)
+        totals = {name: 0.0 for name in (self.loss_tracker.train_losses if training else self.loss_tracker.val_losses)}
+        ws = model.workspace(model.precision, loader.batch_size)
+        rec = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device=self.device)
+        model.requires_grad_(training)
+        try:
+            for bi, rows in enumerate(batches):
+                data = self._gather(mat, rows)
+                eps = self._eps(rows.shape[0])
+                if training:
+                    model.zero_grad()
+                    recon, mu, lv = model((mat, rows), eps=eps)
+                    total, parts = self.loss_tracker.compute_total_loss(recon, data, mu, lv, model, epoch, bi)
+                    total.backward()
+                    grads = model.params.grad
+                    sc = self._scalar_row({"beta": 0.0, "wgamma": 0.0, "lambda": 0.0}, self.optimizer.step_count + 1)
+                    scal = torch.from_numpy(sc).to(self.device)
+                    native.grad_norm(ws, model.params.detach(), grads, scal, rec)
+                    native.adam_step(ws, model.params.detach(), grads, self.optimizer.exp_avg,
+                                     self.optimizer.exp_avg_sq, scal)
+                    self.optimizer.step_count += 1
+                    model.shadows_current(model.precision)
+                else:
+                    with torch.no_grad():
+                        recon, mu, lv = model((mat, rows), eps=eps)
+                        _, parts = self.loss_tracker.compute_total_loss(recon, data, mu, lv, model, epoch, bi,
+                                                                        is_training=False)
+                for k, v in parts.items():
+                    totals[k] += v
+        finally:
+            model.requires_grad_(False)
+            model.zero_grad()
+        if training and batches:
+            self.last_grad_norm = float(rec[4].item())
+        n = len(loader.dataset)
+        return {k: v / n for k, v in totals.items()}
+
     def train_epoch(self, train_loader, epoch: int) -> Dict[str, float]:
         """trainer.py:104-131. Per batch: fused fwd+bwd -> (bucketed all-reduce) -> clip stats -> Adam."""
+        if not self.loss_tracker.fused:
+            return self._epoch_autograd(as_strain_loader(train_loader, self.device), epoch, True)
         model = self.model
         model.train()
         loader = as_strain_loader(train_loader, self.device)
@@ -280,6 +341,8 @@ class VAETrainer:
 
     def validate_epoch(self, val_loader, epoch: int) -> Dict[str, float]:
         """trainer.py:133-156: eval-mode forward + the same loss components (KL counter advances)."""
+        if not self.loss_tracker.fused:
+            return self._epoch_autograd(as_strain_loader(val_loader, self.device), epoch, False)
         model = self.model
         model.eval()
         loader = as_strain_loader(val_loader, self.device)

@@ -1,0 +1,100 @@
+"""`--mode sample` paths against the oracle:
+
+  * sample_from_model (extras.py:192-203) with N > one decode chunk, so the chunked path of
+    VAE.decode_mask runs and chunk boundaries are crossed (default 65,536-row chunks, and a
+    smaller chunk that leaves a ragged last chunk);
+  * focused sampling (main.py:351-370 as main.focused_samples): 100 default samples, the fewest-
+    genes sample, its output-space nearest neighbour, z* + sigma * N(0, I) decoded;
+  * sample -> train one epoch -> sample on the same model: the second sampling decodes with the
+    trained weights (the fp32 decode shadows are re-derived after the bf16 optimizer steps).
+Bar: masks bit-exact to the oracle's fp32 decode outside the fp64 rounding band of each logit
+(|logit64| <= 1e-3: counted, reported, not asserted), probabilities rel 2e-5.
+"""
+import numpy as np
+import pytest
+import torch
+
+from gpu_helpers import oracle_state, perturb_bn, synth_x, to_model
+from oracle import vae_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from gm2 import native
+
+
+def _masks_ok(mask, P, S, z):
+    ref = (O.sample_decode(P, S, z).numpy() > 0.5)
+    l64 = O.decode_logits64(P, S, z).numpy()
+    band = np.abs(l64) <= 1e-3
+    bad = int(((np.asarray(mask).astype(bool) != ref) & ~band).sum())
+    print(f"{int(band.sum())} band elements, {bad} mismatches outside the band")
+    return bad
+
+
+@pytest.mark.parametrize("N,chunk", [(70001, 65536), (70001, 30000)])
+def test_sample_from_model_chunked(N, chunk):
+    from gm2.extras import sample_from_model
+    G, H, L = 257, 128, 16
+    P, S = perturb_bn(*oracle_state(G, H, L, 40), seed=41)
+    P["decoder.9.bias"] = torch.linspace(-1.5, 1.0, G)
+    m = to_model(P, S, G, H, L, native.GM2_F32)
+    m.eval()
+    torch.manual_seed(123)
+    binary, probs, z = sample_from_model(m, L, N, torch.device("cuda"), chunk=chunk)
+    assert binary.shape == (N, G) and binary.dtype == np.float64 and z.shape == (N, L)
+    zc = z.cpu()
+    assert _masks_ok(binary, P, S, zc) == 0
+    np.testing.assert_allclose(probs, O.sample_decode(P, S, zc).numpy(), rtol=2e-5, atol=2e-6)
+    # z is the reference draw: torch.randn(N, L, device) from the seeded generator
+    torch.manual_seed(123)
+    np.testing.assert_array_equal(zc.numpy(), torch.randn(N, L, device="cuda").cpu().numpy())
+
+
+def test_focused_sampling_matches_oracle():
+    import main as cli
+    G, H, L, N, sigma = 300, 128, 16, 500, 0.1
+    P, S = perturb_bn(*oracle_state(G, H, L, 50), seed=51)
+    P["decoder.9.bias"] = torch.linspace(-2.0, 0.5, G)
+    m = to_model(P, S, G, H, L, native.GM2_F32)
+    m.eval()
+    dev = torch.device("cuda")
+    torch.manual_seed(7)
+    mask, z = cli.focused_samples(m, L, N, sigma, dev)
+    # oracle: replay the two device draws, then the reference's selection and noise
+    torch.manual_seed(7)
+    z_temp = torch.randn(100, L, device=dev).cpu()
+    noise = torch.randn(N, L, device=dev).cpu() * sigma
+    p_temp = O.sample_decode(P, S, z_temp).numpy()
+    b_temp = (p_temp > 0.5).astype(float)
+    i_min = np.argmin(b_temp.sum(axis=1))
+    closest = np.argmin(np.linalg.norm(p_temp - p_temp[i_min], axis=1))
+    z_ref = z_temp[closest].unsqueeze(0) + noise
+    np.testing.assert_allclose(z.cpu().numpy(), z_ref.numpy(), rtol=0, atol=1e-6)
+    assert _masks_ok(mask.cpu().numpy(), P, S, z_ref) == 0
+
+
+def test_sample_train_sample_uses_trained_weights():
+    """decoding after training must use the updated weights, also when the fp32
+    (sampling) workspace existed before a bf16 training epoch."""
+    from gm2.data import ResidentMatrix, StrainLoader
+    from gm2.trainer import Adam, StepLR, create_v0_trainer
+    G, H, L = 300, 128, 16
+    P, S = oracle_state(G, H, L, 60)
+    m = to_model(P, S, G, H, L, native.GM2_BF16)
+    z = torch.randn(64, L)
+    m.eval()
+    before, _ = m.decode_mask(z)
+    opt = Adam(m, lr=1e-2)
+    tr = create_v0_trainer(m, opt, StepLR(opt), 2, 1.0, 0.1, 1.0)
+    x = synth_x(128, G, 61)
+    tr.train_epoch(StrainLoader(ResidentMatrix(x), None, 64, shuffle=True), 0)
+    m.eval()
+    after, p_after = m.decode_mask(z, want_probs=True)
+    Pn = O.unflatten(m.params.cpu().numpy(), G, H, L)
+    Sn = {k: v.clone() for k, v in S.items()}
+    for i, b in enumerate(O.BNS):
+        Sn[b + ".running_mean"] = m.bn[i, 0].cpu()
+        Sn[b + ".running_var"] = m.bn[i, 1].cpu()
+    np.testing.assert_allclose(p_after.cpu().numpy(), O.sample_decode(Pn, Sn, z).numpy(), rtol=2e-5, atol=2e-6)
+    assert not torch.equal(before, after)
