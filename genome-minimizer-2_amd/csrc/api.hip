@@ -111,7 +111,7 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.sD2 = take(H * H * es);
   o.sD3 = take(d.Gp * H * es);       // [Gp][H]
   o.X = take(Bm * d.Gp * es);        // gathered strain rows [Bm][Gp]
-  o.XB = take(d.Gp * (Bm / 32) * 4); // bit-packed X^T target [Gp][Bm/32]
+  o.XB = take(Bm * (d.Gp / 32) * 4); // row-major bit-packed target [Bm][Gp/32]
   for (int i = 0; i < 6; ++i) {
     o.Y[i] = take(Bm * H * 4);       // pre-BN fp32
     o.A[i] = take(Bm * H * es);      // post-ReLU
@@ -331,8 +331,8 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   const int Bp = (int)round_up(B, kTile);
   const int H = (int)d.H, L = (int)d.L;
   // 1) strain rows -> X [Bp][Gp] (T) + bit-packed target
-  launch_gather_rows<T>(b->data, b->ld_data, b->rows, B, (int)d.G, c.t(l.X), d.Gp, (int)d.Gp, nullptr, 0, Bp,
-                        (uint32_t*)(c.ws + l.XB), d.Bm / 32, c.s);
+  launch_gather_rows<T>(b->data, b->ld_data, b->rows, B, (int)d.G, c.t(l.X), d.Gp, (int)d.Gp, Bp,
+                        (uint32_t*)(c.ws + l.XB), d.Gp / 32, c.s);
   // 2) encoder blocks, heads + reparameterisation, decoder blocks (all NT GEMMs)
   const T* in = c.t(l.X);
   int64_t ldin = d.Gp;
@@ -357,14 +357,15 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
     ldin = H;
     Kin = H;
   }
-  GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, B, (int)d.G, H, Bp, (int)d.Gp, 0};
   if (probs) {  // 3') VAE.forward: output probabilities p = sigmoid(logits) (model.py:89-90), no loss
+    GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, B, (int)d.G, H, Bp, (int)d.Gp, 0};
     launch_gemm_mask<T>(g, prm + d.off[D9B], nullptr, 0, probs, ld_probs, c.s);
     return;
   }
-  // 3) output layer + reconstruction loss (+ dlogits)
-  launch_gemm_recon_loss<T>(g, prm + d.off[D9B], (const uint32_t*)(c.ws + l.XB), d.Bm / 32, with_grad, scal, c.t(l.dL),
-                            d.Gp, nullptr, 0, c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
+  // 3) output layer + reconstruction loss (+ dlogits), computed as logit^T: genes x strains
+  GemmArgs<T> g{c.t(l.sD3), H, c.t(l.A[5]), H, (int)d.G, B, H, (int)d.Gp, Bp, 0};
+  launch_gemm_recon_loss<T>(g, prm + d.off[D9B], (const uint32_t*)(c.ws + l.XB), d.Gp / 32, with_grad, scal, c.t(l.dL),
+                            d.Gp, c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
   const int nblk = gemm_recon_grid_blocks<T>(g);
   launch_reduce_to(c.f(l.losspart), nblk, 2, 2, loss + 0, c.s);
   launch_reduce_to(c.f(l.klpart), Bp / 64, 1, 1, loss + 2, c.s);
@@ -597,8 +598,8 @@ int gm2_encode(const gm2_dims* d, int prec, const gm2_batch* batch, const float*
       const int B = (int)b.n, Bp = (int)round_up(B, kTile), H = (int)dd.H, L = (int)dd.L;
       if (B <= 0 || B > dd.Bm) throw Gm2Error("encode rows outside (0, batch_max]");
       float* bn = const_cast<float*>(bn_running);
-      launch_gather_rows<T>(b.data, b.ld_data, b.rows, B, (int)dd.G, c.t(lo.X), dd.Gp, (int)dd.Gp, nullptr, 0, Bp,
-                            nullptr, 0, c.s);
+      launch_gather_rows<T>(b.data, b.ld_data, b.rows, B, (int)dd.G, c.t(lo.X), dd.Gp, (int)dd.Gp, Bp, nullptr, 0,
+                            c.s);
       const T* in = c.t(lo.X);
       int64_t ldin = dd.Gp;
       int Kin = (int)dd.Gp;
@@ -722,6 +723,10 @@ int gm2_set_option(int key, int value) {
     switch (key) {
       case GM2_OPT_GEMM_PP: set_gemm_pp(value); break;
       case GM2_OPT_SIDE_STREAM: side_flag().store(value ? 1 : 0); break;
+      case GM2_OPT_RECON_TILE:
+        if (value != 0 && value != 128 && value != 256) throw Gm2Error("recon tile %d: 0, 128 or 256", value);
+        set_recon_tile(value);
+        break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });
@@ -732,6 +737,7 @@ int gm2_get_option(int key, int* value) {
     switch (key) {
       case GM2_OPT_GEMM_PP: *value = get_gemm_pp(); break;
       case GM2_OPT_SIDE_STREAM: *value = side_flag().load(); break;
+      case GM2_OPT_RECON_TILE: *value = get_recon_tile(); break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });

@@ -436,31 +436,126 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
 
 // ---------------------------------------------------------------------------------------------
 // Epilogue 2: decoder output layer + reconstruction loss (loss_components.py:49-50 BCE(sum),
-// :111-115 gene abundance) and, in training, dL/dlogit exactly as autograd composes
-// Sigmoid->BCE: dp = (p-x)/max((1-p)p, 1e-12) + w*gamma ; dl = dp*(1-p)*p.
+// :111-115 gene abundance) and, in training, dL/dlogit as autograd composes Sigmoid->BCE:
+//   dp = (p-x)/max((1-p)p, 1e-12) + w*gamma ; dl = dp*(1-p)*p.
 // (sign(colsum p) == 1 wherever p > 0, and dl == 0 wherever p == 0: no batch-wide pass needed.)
-// FAST (bf16 training path): v_exp / v_rcp / v_log hardware approximations (~1 ulp) and
-// log(1-p) for log1p(-p); exact libm forms on the fp32 parity path.
-// Writes dL [m][ldd] (row-major, staged through LDS for full-line stores) and dL^T [n][lddt]
-// (4 consecutive m per lane), zero outside the valid M x N box; per-tile BCE and sum(p) into
-// loss_part[tile*2 + {0,1}]; per-(m-tile, n) column sums of dl into colpart.
+// The tile is computed TRANSPOSED: P = the output weight W9 [Gp][H] (rows = genes), Q = the last
+// hidden activations A5 [Bp][H] (rows = strains), so acc holds logit^T and each lane owns FOUR
+// CONSECUTIVE GENES of one strain row: 8-byte bf16 (16-byte f32) LDS image writes, one 32-bit word
+// of the row-major target bits, a float4 of the bias.
+// FAST (bf16 training path): hardware exp / rcp / log (~1 ulp), log(1-p) for log1p(-p), and the
+// (p-x)/max(q,1e-12)*q product folded to (p-x) where q >= 1e-12 (the same value up to one
+// rounding); the fp32 parity path keeps the reference's exact formula order.
+// Writes dL [strain][ldd] (row-major, through an LDS image for full-line stores), zero outside the
+// valid G x B box; per-tile BCE and sum(p) into loss_part[tile*2 + {0,1}]; per-(strain tile, gene)
+// sums of dl into colpart (the output bias gradient).
 // ---------------------------------------------------------------------------------------------
+// The loss epilogue's element loop. No per-element guards: padded genes (g >= G) have a zero
+// weight row and a zero bias, so their logit is exactly 0 and their BCE / sum(p) contributions are
+// exact constants the kernel subtracts per tile; padded strains are masked by `smask` inside the
+// accumulating FMAs. Padded dL entries are harmless: every consumer multiplies them by
+// zero-padded operands (W9 shadow rows >= G, A5 rows >= B) or never reads them.
+//
+// FAST (bf16 training) element math, select-free: with ns = (x ? -1 : +1) built from the target
+// bit by integer ops, t = sigmoid(-ns*l) is the BCE argument (p for x = 1, 1-p for x = 0), and
+//   -log t (clamped at 100) ; p - x = ns*(1-t) ; p(1-p) = t(1-t) ; p = [x == 0] - ns*t,
+// so sum(p) = (number of x == 0 targets) + sum(-ns*t). Hardware exp2 / rcp / log2 (~1 ulp), BCE
+// summed in log2 units (scaled by ln 2 once per tile), and (p-x)/max(q,1e-12)*q folded to
+// (p-x)*min(q*1e12, 1): the reference's value up to rounding.
+// Exact (fp32 parity) path: the reference's formula order, p computed first.
+template <class C, typename T, bool FAST>
+__device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], const uint32_t* __restrict__ xrow,
+                                           int64_t ldxb, const float* bias_s, int N, int n0, int wm, int wn, int q,
+                                           int c, float wgam, bool with_grad, T* img, float& bce, float& psum) {
+  constexpr int PR = C::BM + 8;
+  constexpr int XW = C::WTM / 32;  // target words of this wave's gene span per strain row
+  static_assert(XW == 4 || XW == 2, "wave gene span");
+  // strain-major order: one strain column (16 lanes x 4 genes x FM slices) at a time, so only
+  // that strain's target words and one LDS row base are live (the image offsets of the FM slices
+  // are immediates)
+#pragma unroll
+  for (int ni = 0; ni < C::FN; ++ni) {
+    const int sl = wn * C::WTN + ni * 16 + c;  // strain (tile-local)
+    const bool sok = n0 + sl < N;
+    const float sm = sok ? 1.0f : 0.0f;
+    uint32_t xw[XW];
+    const uint32_t* xp = xrow + (int64_t)(n0 + sl) * ldxb;
+    if (sok) {
+      if constexpr (XW == 4) {
+        const uint4 v = *(const uint4*)xp;
+        xw[0] = v.x; xw[1] = v.y; xw[2] = v.z; xw[3] = v.w;
+      } else {
+        const uint2 v = *(const uint2*)xp;
+        xw[0] = v.x; xw[1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < XW; ++k) xw[k] = 0u;
+    }
+    T* irow = img + sl * PR + wm * C::WTM + 4 * q;
+#pragma unroll
+    for (int mi = 0; mi < C::FM; ++mi) {
+      // the tile's bias slice sits in LDS (zero beyond G)
+      const float4 b4 = *(const float4*)(bias_s + wm * C::WTM + mi * 16 + 4 * q);
+      const float bn[4] = {b4.x, b4.y, b4.z, b4.w};
+      const uint32_t xb = xw[mi >> 1] >> ((mi & 1) * 16 + 4 * q);
+      float dl4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float l = acc[mi][ni][j] + bn[j];
+        if constexpr (FAST) {
+          const uint32_t sb = (xb << (31 - j)) & 0x80000000u;     // sign bit set iff x = 1
+          const float ns = __uint_as_float(sb | 0x3F800000u);      // x ? -1 : +1
+          const float t = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(__uint_as_float(__float_as_uint(l) ^ sb) * 1.4426950408889634f));
+          const float omt = 1.0f - t;
+          bce = fmaf(sm, fminf(-__builtin_amdgcn_logf(t), 144.26950408889634f), bce);  // min(-ln t,100)/ln 2
+          psum = fmaf(-ns * sm, t, psum);
+          const float qq = t * omt;
+          dl4[j] = fmaf(ns * omt, fminf(qq * 1e12f, 1.0f), wgam * qq);
+        } else {
+          const bool x = (xb >> j) & 1u;
+          const float p = 1.0f / (1.0f + expf(-l));
+          bce = fmaf(sm, x ? -fmaxf(logf(p), -100.f) : -fmaxf(log1pf(-p), -100.f), bce);
+          psum = fmaf(sm, p, psum);
+          const float omp = 1.0f - p;
+          const float dp = (p - (x ? 1.0f : 0.0f)) / fmaxf(omp * p, 1e-12f) + wgam;
+          dl4[j] = dp * omp * p;
+        }
+      }
+      if (with_grad) {
+        if constexpr (sizeof(T) == 2) {
+          uint2 pk;
+          pk.x = (uint32_t)f2bf(dl4[0]) | ((uint32_t)f2bf(dl4[1]) << 16);
+          pk.y = (uint32_t)f2bf(dl4[2]) | ((uint32_t)f2bf(dl4[3]) << 16);
+          *(uint2*)(irow + mi * 16) = pk;
+        } else {
+          *(f32x4*)(irow + mi * 16) = f32x4{dl4[0], dl4[1], dl4[2], dl4[3]};
+        }
+      }
+    }
+    if constexpr (FAST) {
+      // sum(p) = #(x == 0 targets of the valid strains) + sum(-ns*t): the q == 0 lanes count
+      // their strain's zero bits over the wave's WTM genes (q = 1..3 lanes hold the same words)
+      if (q == 0) {
+        int ones = 0;
+#pragma unroll
+        for (int k = 0; k < XW; ++k) ones += __builtin_popcount(xw[k]);
+        psum = fmaf(sm, (float)(C::WTM - ones), psum);
+      }
+    }
+  }
+}
+
+// BCE / sum(p) of one padded gene (logit exactly 0, target 0): p = 1/2, BCE = -log(1/2)
 template <bool FAST>
-__device__ __forceinline__ void recon_elem(float l, float x, float wgam, float& e, float& p, float& dl) {
+__device__ __forceinline__ void recon_pad_const(float& e0, float& p0) {
   if constexpr (FAST) {
-    const float ex = __builtin_amdgcn_exp2f(-l * 1.4426950408889634f);
-    p = __builtin_amdgcn_rcpf(1.0f + ex);
-    const float omp = 1.0f - p;
-    const float t = x != 0.f ? p : omp;
-    e = -fmaxf(__builtin_amdgcn_logf(t) * 0.6931471805599453f, -100.f);
-    const float dp = (p - x) * __builtin_amdgcn_rcpf(fmaxf(omp * p, 1e-12f)) + wgam;
-    dl = dp * omp * p;
+    const float t = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(0.f));
+    e0 = fminf(-__builtin_amdgcn_logf(t), 144.26950408889634f) * 0.6931471805599453f;
+    p0 = t;
   } else {
-    p = 1.0f / (1.0f + expf(-l));
-    e = x != 0.f ? -fmaxf(logf(p), -100.f) : -fmaxf(log1pf(-p), -100.f);
-    const float omp = 1.0f - p;
-    const float dp = (p - x) / fmaxf(omp * p, 1e-12f) + wgam;
-    dl = dp * omp * p;
+    p0 = 1.0f / (1.0f + expf(-0.f));
+    e0 = -fmaxf(log1pf(-p0), -100.f);
   }
 }
 
@@ -468,141 +563,99 @@ template <class C, typename T, bool PP>
 __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const float* __restrict__ bias,
                                                          const uint32_t* __restrict__ xbits, int64_t ldxb,
                                                          int with_grad, const float* __restrict__ scal,
-                                                         T* __restrict__ dL, int64_t ldd, T* __restrict__ dLT,
-                                                         int64_t lddt, float* __restrict__ loss_part,
-                                                         float* __restrict__ colpart, int64_t ldcol) {
+                                                         T* __restrict__ dL, int64_t ldd,
+                                                         float* __restrict__ loss_part, float* __restrict__ colpart,
+                                                         int64_t ldcol) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool FAST = sizeof(T) == 2;
-  constexpr int XW = C::WTM / 32;  // target words per lane per column (bit-packed X^T)
   const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
-  const TileXY tl = tile_of<C>(tm, tn);
+  const TileXY tl = tile_of<C>(tm, tn);  // m = genes, n = strains
+  // LDS: [0, image / staging) | per-row-group dl sums | BCE, sum(p) slots | bias slice
+  constexpr int EPC = 16 / sizeof(T);
+  constexpr int PR = C::BM + 8;
+  constexpr int CPR = C::BM / EPC;      // 16-byte chunks per image row
+  constexpr int RG = C::NT / CPR;       // row groups of the store pass
+  constexpr int IMG = std::max<int>(C::LDS, C::BN * PR * (int)sizeof(T));
+  float* colred = (float*)(smem + IMG);  // [RG][BM]
+  float* red = colred + RG * C::BM;     // [2][32]
+  float* bias_s = red + 64;             // [BM]
+  for (int i = threadIdx.x; i < C::BM; i += C::NT) bias_s[i] = tl.m0 + i < g.M ? bias[tl.m0 + i] : 0.f;
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP)
     mainloop_pp<true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   else
     mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
-  const int q = lane >> 4;
+  const int q = lane >> 4, c = lane & 15;
   const float wgam = scal[kScalWGamma];
   float bce = 0.f, psum = 0.f;
-  float csum[C::FN];
-  // phase 1: loss terms and dl in registers (dl overwrites the accumulator)
-#pragma unroll
-  for (int ni = 0; ni < C::FN; ++ni) {
-    csum[ni] = 0.f;
-    const int n = tl.n0 + wn * C::WTN + ni * 16 + (lane & 15);
-    const bool nok = n < g.N;
-    const float bn = nok ? bias[n] : 0.f;
-    uint32_t xw[XW];
-    const uint32_t* xp = xbits + (int64_t)n * ldxb + (tl.m0 + wm * C::WTM) / 32;
-    if constexpr (XW == 4) {
-      const uint4 v = *(const uint4*)xp;
-      xw[0] = v.x; xw[1] = v.y; xw[2] = v.z; xw[3] = v.w;
-    } else {
-      const uint2 v = *(const uint2*)xp;
-      xw[0] = v.x; xw[1] = v.y;
-    }
-#pragma unroll
-    for (int mi = 0; mi < C::FM; ++mi) {
-      const int mb = tl.m0 + wm * C::WTM + mi * 16 + 4 * q;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float dl = 0.f;
-        if (nok && mb + j < g.M) {
-          const float x = (float)((xw[mi >> 1] >> ((mi & 1) * 16 + 4 * q + j)) & 1u);
-          float e, p;
-          recon_elem<FAST>(acc[mi][ni][j] + bn, x, wgam, e, p, dl);
-          bce += e;
-          psum += p;
-          csum[ni] += dl;
-        }
-        acc[mi][ni][j] = dl;
-      }
-    }
-  }
-  constexpr int EPC = 16 / sizeof(T);
-  if (with_grad && dLT) {
-    // phase 2 (optional): dL^T [n][m] through an LDS image [BN][BM+8] (each lane owns 4
-    // consecutive m of one n: one 8/16-byte LDS write), then full-row coalesced stores
-    {
-      constexpr int PT = C::BM + 8;
-      T* img = (T*)smem;
-#pragma unroll
-      for (int mi = 0; mi < C::FM; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < C::FN; ++ni) {
-          const int nl = wn * C::WTN + ni * 16 + (lane & 15);
-          const int ml = wm * C::WTM + mi * 16 + 4 * q;
-          if constexpr (sizeof(T) == 2) {
-            uint2 pk;
-            pk.x = (uint32_t)f2bf(acc[mi][ni][0]) | ((uint32_t)f2bf(acc[mi][ni][1]) << 16);
-            pk.y = (uint32_t)f2bf(acc[mi][ni][2]) | ((uint32_t)f2bf(acc[mi][ni][3]) << 16);
-            *(uint2*)(img + nl * PT + ml) = pk;
-          } else {
-            *(f32x4*)(img + nl * PT + ml) = acc[mi][ni];
-          }
-        }
-      __syncthreads();
-      constexpr int CPR = C::BM / EPC;
-      for (int i = threadIdx.x; i < C::BN * CPR; i += C::NT) {
-        const int r = i / CPR, cch = i % CPR;
-        *(uint4*)(dLT + (int64_t)(tl.n0 + r) * lddt + tl.m0 + cch * EPC) = *(const uint4*)(img + r * PT + cch * EPC);
-      }
-      __syncthreads();
-    }
-  }
+  T* img = (T*)smem;  // LDS image [BN strains][BM genes + 8] of T
+  recon_tile<C, T, FAST>(acc, xbits + ((tl.m0 + wm * C::WTM) >> 5), ldxb, bias_s, g.N, tl.n0, wm, wn, q, c, wgam,
+                         with_grad, img, bce, psum);
+  if constexpr (FAST) bce *= 0.6931471805599453f;
   if (with_grad) {
-    // phase 3: dL [m][n] through an LDS image [BM][BN+8], full-row coalesced stores
-    {
-      constexpr int PR = C::BN + 8;
-      T* img = (T*)smem;
+    __syncthreads();
+    // dL rows (strains) of BM genes: full 16-byte stores along each row. Thread i keeps one chunk
+    // column (EPC genes) over rows i/CPR, +RG, ...: the same pass sums that chunk's dl over the
+    // valid strains for the output bias gradient (the rounded values the dW9 GEMM reads).
+    const int cch = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
+    float cs[EPC];
 #pragma unroll
-      for (int mi = 0; mi < C::FM; ++mi)
+    for (int e = 0; e < EPC; ++e) cs[e] = 0.f;
+    for (int r = r0; r < C::BN; r += RG) {
+      const uint4 v = *(const uint4*)(img + r * PR + cch * EPC);
+      *(uint4*)(dL + (int64_t)(tl.n0 + r) * ldd + tl.m0 + cch * EPC) = v;
+      if (tl.n0 + r < g.N) {
+        if constexpr (sizeof(T) == 2) {
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int ni = 0; ni < C::FN; ++ni) {
-          const int nl = wn * C::WTN + ni * 16 + (lane & 15);
-          const int ml = wm * C::WTM + mi * 16 + 4 * q;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) img[(ml + j) * PR + nl] = E<T>::cvt(acc[mi][ni][j]);
+          for (int e = 0; e < 4; ++e) {
+            cs[2 * e] += __uint_as_float(w[e] << 16);
+            cs[2 * e + 1] += __uint_as_float(w[e] & 0xFFFF0000u);
+          }
+        } else {
+          cs[0] += __uint_as_float(v.x); cs[1] += __uint_as_float(v.y);
+          cs[2] += __uint_as_float(v.z); cs[3] += __uint_as_float(v.w);
         }
-      __syncthreads();
-      constexpr int CPR = C::BN / EPC;
-      for (int i = threadIdx.x; i < C::BM * CPR; i += C::NT) {
-        const int r = i / CPR, cch = i % CPR;
-        *(uint4*)(dL + (int64_t)(tl.m0 + r) * ldd + tl.n0 + cch * EPC) = *(const uint4*)(img + r * PR + cch * EPC);
       }
     }
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) colred[r0 * C::BM + cch * EPC + e] = cs[e];
   }
-  __syncthreads();
-  // block reductions (reuse LDS): BCE and sum(p) -> loss_part[tile]; column sums of dl
-  float* red = (float*)smem;          // [2][32]
-  float* colred = (float*)smem + 64;  // [WGM][BN]
   bce = wave_sum(bce);
   psum = wave_sum(psum);
   if (lane == 0) { red[wid] = bce; red[32 + wid] = psum; }
-#pragma unroll
-  for (int ni = 0; ni < C::FN; ++ni) {
-    float v = csum[ni];
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (lane < 16) colred[wm * C::BN + wn * C::WTN + ni * 16 + lane] = v;
-  }
   __syncthreads();
   if (threadIdx.x == 0) {
     float a = 0.f, b = 0.f;
     for (int w = 0; w < C::NT / 64; ++w) { a += red[w]; b += red[32 + w]; }
+    // padded genes of an edge tile: logit exactly 0 -> p = 1/2, x = 0, BCE = -log(1/2) each
+    const int pad_g = max(0, tl.m0 + C::BM - g.M), val_s = min(C::BN, g.N - tl.n0);
+    if (pad_g > 0) {
+      float e0, p0;
+      recon_pad_const<FAST>(e0, p0);
+      a -= (float)pad_g * (float)val_s * e0;
+      b -= (float)pad_g * (float)val_s * p0;
+    }
     loss_part[tl.t * 2 + 0] = a;
     loss_part[tl.t * 2 + 1] = b;
   }
   if (with_grad) {
-    for (int c = threadIdx.x; c < C::BN; c += C::NT) {
-      const int n = tl.n0 + c;
+    for (int cc = threadIdx.x; cc < C::BM; cc += C::NT) {
+      const int gg = tl.m0 + cc;
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < C::WGM; ++w) v += colred[w * C::BN + c];
-      if (n < g.N) colpart[(int64_t)(tl.m0 / C::BM) * ldcol + n] = v;
+      for (int w = 0; w < RG; ++w) v += colred[w * C::BM + cc];
+      if (gg < g.M) colpart[(int64_t)(tl.n0 / C::BN) * ldcol + gg] = v;
     }
   }
+}
+
+template <class C, typename T>
+constexpr int recon_lds_bytes() {
+  constexpr int img = std::max<int>(C::LDS, C::BN * (C::BM + 8) * (int)sizeof(T));
+  constexpr int rg = C::NT / (C::BM / (16 / (int)sizeof(T)));
+  return img + (rg * C::BM + 64 + C::BM) * 4;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -810,53 +863,65 @@ int gemm_recon_grid_blocks(const GemmArgs<T>& g) {
 }
 
 template <typename T>
-int gemm_recon_row_tiles(const GemmArgs<T>& g) {
-  return g.Mp / (recon_big(g) ? 256 : 128);
+int gemm_recon_row_tiles(const GemmArgs<T>& g) {  // strain tiles (rows of colpart)
+  return g.Np / (recon_big(g) ? 256 : 128);
 }
 
 template <class C, typename T, bool PP>
 static void recon_impl_k(const GemmArgs<T>& g, const float* bias, const uint32_t* X, int64_t ldx, int with_grad,
-                         const float* scal, T* dL, int64_t ldd, T* dLT, int64_t lddt, float* loss_part, float* colpart,
-                         int64_t ldcol, hipStream_t s) {
+                         const float* scal, T* dL, int64_t ldd, float* loss_part, float* colpart, int64_t ldcol,
+                         hipStream_t s) {
   check_gemm(g, C::BM);
-  constexpr int lds = std::max<int>(C::LDS, std::max(C::BM * (C::BN + 8), C::BN * (C::BM + 8)) * (int)sizeof(T));
+  if (ldx * 32 < g.Mp || (ldx & 3)) throw Gm2Error("recon: target bit rows too short");
+  constexpr int lds = recon_lds_bytes<C, T>();
   static_assert(lds <= 160 * 1024, "LDS budget");
   ensure_lds_attr((const void*)k_gemm_recon_loss<C, T, PP>, lds);
   hipLaunchKernelGGL((k_gemm_recon_loss<C, T, PP>), dim3((g.Mp / C::BM) * (g.Np / C::BN)), dim3(C::NT), lds, s, g,
-                     bias, X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol);
+                     bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol);
 }
 
 template <class C, typename T>
 static void recon_impl(const GemmArgs<T>& g, const float* bias, const uint32_t* X, int64_t ldx, int with_grad,
-                       const float* scal, T* dL, int64_t ldd, T* dLT, int64_t lddt, float* loss_part, float* colpart,
-                       int64_t ldcol, hipStream_t s) {
+                       const float* scal, T* dL, int64_t ldd, float* loss_part, float* colpart, int64_t ldcol,
+                       hipStream_t s) {
   if constexpr (std::is_same_v<C, Big> && sizeof(T) == 2) {
     if (pp_enabled())
-      return recon_impl_k<C, T, true>(g, bias, X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol,
-                                      s);
+      return recon_impl_k<C, T, true>(g, bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol, s);
   }
-  recon_impl_k<C, T, false>(g, bias, X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol, s);
+  recon_impl_k<C, T, false>(g, bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol, s);
 }
 
-// the fp32 parity path stays on the 128-tile (a 256-row fp32 dL image would not fit the LDS)
+// the fp32 parity path stays on the 128-tile (a 256-row fp32 dL image would not fit the LDS).
+// GM2_OPT_RECON_TILE: 0 = plan (256 when it fills the chip), 128 / 256 = force (A/B measurements)
+static std::atomic<int>& recon_tile_flag() {
+  static std::atomic<int> v{0};
+  return v;
+}
+void set_recon_tile(int t) { recon_tile_flag().store(t); }
+int get_recon_tile() { return recon_tile_flag().load(); }
+
 template <typename T>
 static bool recon_big(const GemmArgs<T>& g) {
-  return sizeof(T) == 2 && g.Mp % 256 == 0 && g.Np % 256 == 0 && (g.Mp / 256) * (g.Np / 256) >= 128;
+  const int force = recon_tile_flag().load(std::memory_order_relaxed);
+  const bool ok = sizeof(T) == 2 && g.Mp % 256 == 0 && g.Np % 256 == 0;
+  if (force == 128) return false;
+  if (force == 256) return ok;
+  return ok && (g.Mp / 256) * (g.Np / 256) >= 128;
 }
 
 template <typename T>
 void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const uint32_t* X, int64_t ldx, int with_grad,
-                            const float* scal, T* dL, int64_t ldd, T* dLT, int64_t lddt, float* loss_part,
-                            float* colpart, int64_t ldcol, hipStream_t s) {
+                            const float* scal, T* dL, int64_t ldd, float* loss_part, float* colpart, int64_t ldcol,
+                            hipStream_t s) {
   TimedLaunch tl(kKcReconLoss, s);
   bool done = false;
   if constexpr (sizeof(T) == 2) {
     if (recon_big(g)) {
-      recon_impl<Big, T>(g, bias, X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol, s);
+      recon_impl<Big, T>(g, bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol, s);
       done = true;
     }
   }
-  if (!done) recon_impl<Small, T>(g, bias, X, ldx, with_grad, scal, dL, ldd, dLT, lddt, loss_part, colpart, ldcol, s);
+  if (!done) recon_impl<Small, T>(g, bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol, s);
   GM2_CHECK_LAUNCH();
 }
 
@@ -877,8 +942,7 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
   template int gemm_recon_row_tiles<T>(const GemmArgs<T>&);                                                     \
   template GemmPlan plan_gemm<T>(const GemmArgs<T>&);                                                          \
   template void launch_gemm_recon_loss<T>(const GemmArgs<T>&, const float*, const uint32_t*, int64_t, int,        \
-                                          const float*,                                                         \
-                                          T*, int64_t, T*, int64_t, float*, float*, int64_t, hipStream_t);
+                                          const float*, T*, int64_t, float*, float*, int64_t, hipStream_t);
 GM2_INST(float)
 GM2_INST(bf16_t)
 #undef GM2_INST

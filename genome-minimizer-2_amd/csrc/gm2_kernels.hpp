@@ -88,15 +88,19 @@ int gemm_recon_row_tiles(const GemmArgs<T>& g);
 // process-global GEMM main-loop switch (gm2_set_option GM2_OPT_GEMM_PP)
 void set_gemm_pp(int on);
 int get_gemm_pp();
+void set_recon_tile(int t);
+int get_recon_tile();
 struct GemmPlan {
   int tile, splits;
 };
 template <typename T>
 GemmPlan plan_gemm(const GemmArgs<T>& g);
+// output layer GEMM computed transposed (P = W9 shadow [Gp][H], M = genes; Q = A5 [Bp][H], N =
+// strains) + fused loss epilogue; xbits = row-major target bits [Bp][ldxb words]; dL [strain][ldd]
 template <typename T>
 void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const uint32_t* xbits, int64_t ldxb, int with_grad,
-                            const float* scal, T* dL, int64_t ldd, T* dLT, int64_t lddt, float* loss_part,
-                            float* colpart, int64_t ldcol, hipStream_t s);
+                            const float* scal, T* dL, int64_t ldd, float* loss_part, float* colpart, int64_t ldcol,
+                            hipStream_t s);
 template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs,
                       int64_t ldpr, hipStream_t s);
@@ -104,12 +108,12 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
 // ---- kernels.hip ----
 constexpr int kBnRowChunk = 128;  // rows per BatchNorm partial-statistics chunk
 
-// gather strain rows of the resident u8 matrix into X [Bp][ldx] and X^T [ldxt rows][Bp] (T), plus
-// the bit-packed target X^T bits [Gp][ldxb words] (bit b%32 of word b/32 = X[b][g]) that the
-// reconstruction-loss epilogue reads; zero-fills columns >= G and rows >= B up to the padded extents
+// gather strain rows of the resident u8 matrix into X [Bp][ldx] (T), plus the row-major bit-packed
+// target [Bp][ldxb words] (bit g%32 of word g/32 of row b = X[b][g]) that the reconstruction-loss
+// epilogue reads; zero-fills columns >= G and rows >= B up to the padded extents
 template <typename T>
 void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* rows, int B, int G, T* X, int64_t ldx,
-                        int Gp, T* XT, int64_t ldxt, int Bp, uint32_t* xbits, int64_t ldxb, hipStream_t s);
+                        int Gp, int Bp, uint32_t* xbits, int64_t ldxb, hipStream_t s);
 
 // BN forward: y = sum of S slabs + bias -> Y; per-chunk (mean, M2) partials
 void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, const float* bias, int B, int H,

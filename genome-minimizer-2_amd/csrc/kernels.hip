@@ -13,18 +13,20 @@ constexpr double kBnEps = 1e-5;       // nn.BatchNorm1d default eps
 constexpr double kBnMomentum = 0.1;   // nn.BatchNorm1d default momentum
 
 // ---------------------------------------------------------------------------------------------
-// gather: X[r][c] = data[rows[r]][c] (u8 0/1 -> T), X^T via an LDS transpose. Tile 64 x 128.
+// gather: X[r][c] = data[rows[r]][c] (u8 0/1 -> T) and the row-major target bits of the loss
+// epilogue (bit c%32 of word c/32 of row r). Tile 64 rows x 128 columns, 256 threads: each
+// thread loads 16 bytes of one row (4 rows per pass), expands them to 16 T, and ballots its row's
+// bytes into bits: the 8 lanes of a row hold 128 columns, one ballot per byte index gives bit i of
+// every 16-column chunk of 8 rows, re-assembled per lane into its 16-bit slice of the row's words.
 // ---------------------------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data, int64_t ld_data,
                                               const int32_t* __restrict__ rows, int B, int G, T* __restrict__ X,
-                                              int64_t ldx, T* __restrict__ XT, int64_t ldxt,
-                                              uint32_t* __restrict__ xbits, int64_t ldxb) {
-  __shared__ uint8_t tile[128][68];  // [column][row] bytes (pitch 68: conflict-light column reads)
+                                              int64_t ldx, uint32_t* __restrict__ xbits, int64_t ldxb) {
   const int c0 = blockIdx.x * 128, r0 = blockIdx.y * 64;
   const int t = threadIdx.x;
   const int ch = t & 7;  // 16-column chunk
-#pragma unroll
+#pragma unroll 2
   for (int pass = 0; pass < 2; ++pass) {
     const int rl = pass * 32 + (t >> 3);
     const int r = r0 + rl;
@@ -35,10 +37,11 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data
     }
     uint8_t b[16];
     *(uint4*)b = v;
+    uint32_t bits = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       if (c0 + ch * 16 + i >= G) b[i] = 0;
-      tile[ch * 16 + i][rl] = b[i];
+      bits |= (b[i] ? 1u : 0u) << i;
     }
     // 16 elements -> 2 (bf16) or 4 (fp32) 16-byte stores
     T* dst = X + (int64_t)r * ldx + c0 + ch * 16;
@@ -53,26 +56,12 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data
       for (int i = 0; i < 4; ++i)
         *(float4*)(dst + 4 * i) = make_float4((float)b[4 * i], (float)b[4 * i + 1], (float)b[4 * i + 2], (float)b[4 * i + 3]);
     }
-  }
-  __syncthreads();
-  if (XT) {  // optional explicit transpose (unused by the current schedule)
-    for (int i = t; i < 128 * 64; i += 256) {
-      const int c = i >> 6, rl = i & 63;
-      XT[(int64_t)(c0 + c) * ldxt + r0 + rl] = E<T>::cvt((float)tile[c][rl]);
+    if (xbits) {
+      // lanes ch = 0..7 of this row hold 16-bit pieces of the row's four 32-bit words; even
+      // lanes combine with their odd neighbour and write one word each
+      const uint32_t hi = __shfl_down(bits, 1, 8);
+      if ((ch & 1) == 0) xbits[(int64_t)r * ldxb + (c0 >> 5) + (ch >> 1)] = bits | (hi << 16);
     }
-  }
-  // bit-packed X^T by ballot: wave w, lane = row; 32 columns per wave, one ballot per column
-  if (xbits) {
-    const int w = t >> 6, lane = t & 63;
-    uint64_t mine = 0;
-#pragma unroll 4
-    for (int k = 0; k < 32; ++k) {
-      const uint64_t m = __ballot(tile[w * 32 + k][lane] != 0);
-      if (lane == k) mine = m;
-    }
-    if (lane < 32)
-      *(uint2*)(xbits + (int64_t)(c0 + w * 32 + lane) * ldxb + (r0 >> 5)) =
-          make_uint2((uint32_t)mine, (uint32_t)(mine >> 32));
   }
 }
 
@@ -687,11 +676,11 @@ __global__ __launch_bounds__(256) void k_colsum2(const float* __restrict__ part,
 // ------------------------------------------------------------------------------------------------
 template <typename T>
 void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* rows, int B, int G, T* X, int64_t ldx,
-                        int Gp, T* XT, int64_t ldxt, int Bp, uint32_t* xbits, int64_t ldxb, hipStream_t s) {
-  if (Gp % 128 || Bp % 64 || ld_data % 16 || ld_data < Gp || ((uintptr_t)data & 15))
+                        int Gp, int Bp, uint32_t* xbits, int64_t ldxb, hipStream_t s) {
+  if (Gp % 128 || Bp % 64 || ld_data % 16 || ld_data < Gp || ((uintptr_t)data & 15) || (xbits && ldxb * 32 < Gp))
     throw Gm2Error("gather: bad layout (Gp=%d Bp=%d ld=%lld)", Gp, Bp, (long long)ld_data);
-  hipLaunchKernelGGL(k_gather<T>, dim3(Gp / 128, Bp / 64), dim3(256), 0, s, data, ld_data, rows, B, G, X, ldx, XT,
-                     ldxt, xbits, ldxb);
+  hipLaunchKernelGGL(k_gather<T>, dim3(Gp / 128, Bp / 64), dim3(256), 0, s, data, ld_data, rows, B, G, X, ldx, xbits,
+                     ldxb);
   GM2_CHECK_LAUNCH();
 }
 
@@ -836,8 +825,8 @@ void launch_grad_finalize(const double* part, int nblocks, const float* scal, fl
 }
 
 #define GM2_INST(T)                                                                                             \
-  template void launch_gather_rows<T>(const uint8_t*, int64_t, const int32_t*, int, int, T*, int64_t, int, T*,  \
-                                      int64_t, int, uint32_t*, int64_t, hipStream_t);                           \
+  template void launch_gather_rows<T>(const uint8_t*, int64_t, const int32_t*, int, int, T*, int64_t, int, int,  \
+                                      uint32_t*, int64_t, hipStream_t);                                         \
   template void launch_reparam<T>(const float*, int, int64_t, int, const float*, const float*, const float*,   \
                                   int, int, float*, T*, int64_t, T*, int64_t, int, float*, hipStream_t);        \
   template void launch_reparam_bwd<T>(const float*, int, int64_t, int64_t, const float*, const float*,         \

@@ -186,8 +186,9 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       bf16 GEMM tiles (default), 0 = two-stage loop. Initial value from env
  *                       GM2_GEMM_PP (0 disables).
  *   GM2_OPT_SIDE_STREAM 1 = weight-gradient GEMMs on a forked side stream (default), 0 = all on
- *                       the caller's stream. Initial value from env GM2_SIDE_STREAM. */
-enum { GM2_OPT_GEMM_PP = 1, GM2_OPT_SIDE_STREAM = 2 };
+ *                       the caller's stream. Initial value from env GM2_SIDE_STREAM.
+ *   GM2_OPT_RECON_TILE  output-layer loss GEMM tile: 0 = plan (default), 128 or 256 = force. */
+enum { GM2_OPT_GEMM_PP = 1, GM2_OPT_SIDE_STREAM = 2, GM2_OPT_RECON_TILE = 3 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);
 

@@ -428,6 +428,91 @@ def manual_grads(P, S, x, eps, beta, wgamma, lambda_l1):
     return {n: G[n] for n in P}
 
 
+def manual_grads_emulated(P, S, x, eps, beta, wgamma, operand_round=None, dtype=torch.float64):
+    """manual_grads' math (the reference's autograd chain, model.py:95-113 + loss_components.py:
+    49-115) evaluated in `dtype` (fp64 by default: an exact-arithmetic reference on any device),
+    with `operand_round` applied to exactly the tensors libgm2's bf16 path stores as GEMM operands
+    (weights, post-ReLU activations, z, dL/dlogit, every BatchNorm input gradient dY and the head
+    gradient d(mu|logvar)). operand_round=None: no rounding (the exact reference for the fp32 path);
+    operand_round=bf16 rounding: the bf16 path's arithmetic, so a GPU-vs-emulation difference is
+    accumulation order only. Returns (grads, loss sums [BCE, sum p, KL raw])."""
+    r = operand_round if operand_round is not None else (lambda t: t)
+    dt = dtype
+    Pd = {k: v.to(dt) for k, v in P.items()}
+    Wr = {k: r(v).to(dt) if v.dim() == 2 else v.to(dt) for k, v in P.items()}
+    x = x.to(dt)
+    eps = eps.to(dt)
+    B = x.shape[0]
+    cache = []
+
+    def blk(lin, bn, a_rounded):
+        y = a_rounded @ Wr[lin + ".weight"].t() + Pd[lin + ".bias"]
+        mean = y.mean(0)
+        var = ((y - mean) ** 2).mean(0)
+        invstd = 1.0 / torch.sqrt(var + BN_EPS)
+        xhat = (y - mean) * invstd
+        o = xhat * Pd[bn + ".weight"] + Pd[bn + ".bias"]
+        a = torch.relu(o)
+        cache.append((lin, bn, a_rounded, xhat, invstd, o))
+        return r(a).to(dt)
+    h = x
+    for i in range(3):
+        h = blk(f"encoder.{3*i}", f"encoder.{3*i+1}", h)
+    h2 = h
+    mu = h2 @ Wr["mean_layer.weight"].t() + Pd["mean_layer.bias"]
+    lv = h2 @ Wr["logvar_layer.weight"].t() + Pd["logvar_layer.bias"]
+    std = torch.exp(0.5 * lv)
+    z = mu + std * eps
+    h = r(z).to(dt)
+    for i in range(3):
+        h = blk(f"decoder.{3*i}", f"decoder.{3*i+1}", h)
+    a5 = h
+    logit = a5 @ Wr["decoder.9.weight"].t() + Pd["decoder.9.bias"]
+    p = torch.sigmoid(logit)
+    bce = -(x * torch.clamp(torch.log(p), min=-100) + (1 - x) * torch.clamp(torch.log1p(-p), min=-100)).sum()
+    sums = [bce.item(), p.sum().item(), torch.sum(1 + lv - mu.pow(2) - lv.exp()).item()]
+    G = {}
+    dp = (p - x) / torch.clamp((1 - p) * p, min=1e-12) + wgamma
+    dl = r(dp * (1 - p) * p).to(dt)
+    del logit, dp
+    G["decoder.9.weight"] = dl.t() @ a5
+    G["decoder.9.bias"] = dl.sum(0)
+    da = dl @ Wr["decoder.9.weight"]
+    del dl, p
+
+    def blk_bwd(entry, da):
+        lin, bn, a, xhat, invstd, o = entry
+        do = da * (o > 0).to(dt)
+        sdo = do.sum(0)
+        sdx = (do * xhat).sum(0)
+        G[bn + ".weight"] = sdx
+        G[bn + ".bias"] = sdo
+        dy = Pd[bn + ".weight"] * invstd / B * (B * do - sdo - xhat * sdx)
+        G[lin + ".bias"] = dy.sum(0)
+        dyr = r(dy).to(dt)
+        G[lin + ".weight"] = dyr.t() @ a
+        return dyr @ Wr[lin + ".weight"]
+    for e in reversed(cache[3:]):
+        da = blk_bwd(e, da)
+    dz = da
+    dmu = dz + beta * mu
+    dlv = dz * eps * std * 0.5 - 0.5 * beta * (1 - torch.exp(lv))
+    G["mean_layer.bias"] = dmu.sum(0)
+    G["logvar_layer.bias"] = dlv.sum(0)
+    dmur, dlvr = r(dmu).to(dt), r(dlv).to(dt)
+    G["mean_layer.weight"] = dmur.t() @ h2
+    G["logvar_layer.weight"] = dlvr.t() @ h2
+    da = dmur @ Wr["mean_layer.weight"] + dlvr @ Wr["logvar_layer.weight"]
+    for e in reversed(cache[:3]):
+        da = blk_bwd(e, da)
+    return {n: G[n] for n in P}, sums
+
+
+def bf16_round(t):
+    """Round to bf16 (RNE) and back: what libgm2's bf16 path stores for a GEMM operand."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
 # ------------------------------------------------------------------------------------------
 # sampling (extras.py:192-203; main.py:351-370)
 # ------------------------------------------------------------------------------------------
