@@ -15,10 +15,11 @@ from oracle import vae_oracle as O
 
 pytestmark = pytest.mark.gpu
 
+from gm2.loss_components import LossComponent
+
 if torch.cuda.is_available():
     from gm2 import native
     from gm2.data import ResidentMatrix, StrainLoader
-    from gm2.loss_components import KLDivergenceLoss, LossComponent, ReconstructionLoss
     from gm2.trainer import Adam, StepLR, VAETrainerBuilder
 
 G, H, L, B = 640, 128, 16, 96
