@@ -321,7 +321,8 @@ TensorTable make_table(const Ctx<T>& c, int kind = 0) {
 // ---------------------------------------------------------------------------------------------
 template <typename T>
 void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, int train, int with_grad,
-             const float* scal, double* loss, float* grads, float* probs = nullptr, int64_t ld_probs = 0) {
+             const float* scal, double* loss, float* grads, float* probs = nullptr, int64_t ld_probs = 0,
+             int* counts = nullptr, float thr = 0.5f) {
   const Dims& d = c.d;
   const Layout& l = c.lo;
   const int B = (int)b->n;
@@ -357,9 +358,11 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
     ldin = H;
     Kin = H;
   }
-  if (probs) {  // 3') VAE.forward: output probabilities p = sigmoid(logits) (model.py:89-90), no loss
+  if (probs || counts) {  // 3') VAE.forward: p = sigmoid(logits) (model.py:89-90) and / or the
+                          // per-strain (TP, FP, FN) of (p > thr) vs the strain's genes; no loss
     GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, B, (int)d.G, H, Bp, (int)d.Gp, 0};
-    launch_gemm_mask<T>(g, prm + d.off[D9B], nullptr, 0, probs, ld_probs, c.s);
+    launch_gemm_mask<T>(g, prm + d.off[D9B], nullptr, 0, probs, ld_probs, c.s, nullptr, 0, counts,
+                        (const uint32_t*)(c.ws + l.XB), d.Gp / 32, thr);
     return;
   }
   // 3) output layer + reconstruction loss (+ dlogits), computed as logit^T: genes x strains
@@ -438,7 +441,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
 
 template <typename T>
 void decode_chain(const Ctx<T>& c, const float* prm, float* bn, int n, uint8_t* mask, int64_t ldm, float* probs,
-                  int64_t ldpr) {
+                  int64_t ldpr, uint8_t* bits = nullptr, int64_t ldb = 0) {
   const Dims& d = c.d;
   const Layout& l = c.lo;
   const int Bp = (int)round_up(n, kTile), H = (int)d.H;
@@ -461,7 +464,7 @@ void decode_chain(const Ctx<T>& c, const float* prm, float* bn, int n, uint8_t* 
     ldw = H;
   }
   GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, n, (int)d.G, H, Bp, (int)d.Gp, 0};
-  launch_gemm_mask<T>(g, prm + d.off[D9B], mask, ldm, probs, ldpr, c.s);
+  launch_gemm_mask<T>(g, prm + d.off[D9B], mask, ldm, probs, ldpr, c.s, bits, ldb);
 }
 
 template <typename T>
@@ -583,6 +586,67 @@ int gm2_decode_mask(const gm2_dims* d, const float* params, const float* bn_runn
     // z [n][L] -> Z [Bm][Lp] (pad columns stay zero from workspace init)
     HIP_OK(hipMemcpy2DAsync(c.f(lo.Z), lo.d.Lr * 4, z, lo.d.L * 4, lo.d.L * 4, n, hipMemcpyDeviceToDevice, c.s));
     decode_chain<float>(c, params, const_cast<float*>(bn_running), (int)n, mask, ld_mask, probs, ld_probs);
+  });
+}
+
+int64_t gm2_packed_row_bytes(int64_t G) { return round_up(G, kTile) / 8; }
+
+int gm2_mask_count_groups(const uint8_t* bits, int64_t n, int64_t ld_bits, const int32_t* group_offsets,
+                          int64_t n_groups, const int32_t* positions, int32_t* counts, void* stream) {
+  return guarded([&] {
+    if (n < 0 || n_groups < 0 || (n && (!bits || !counts)) || (n_groups && (!group_offsets || !positions)))
+      throw Gm2Error("mask_count_groups: bad arguments");
+    if (n_groups == 0) {
+      HIP_OK(hipMemsetAsync(counts, 0, (size_t)n * 4, (hipStream_t)stream));
+      return;
+    }
+    launch_count_groups(bits, n, ld_bits, group_offsets, n_groups, positions, counts, (hipStream_t)stream);
+  });
+}
+
+int gm2_mask_row_offsets(const uint8_t* bits, int64_t n, int64_t ld_bits, const uint8_t* keep_bits, int64_t* offsets,
+                         void* stream) {
+  return guarded([&] {
+    if (n < 0 || !offsets || (n && !bits) || (ld_bits & 15)) throw Gm2Error("mask_row_offsets: bad arguments");
+    launch_row_offsets(bits, n, ld_bits, keep_bits, offsets, (hipStream_t)stream);
+  });
+}
+
+int gm2_mask_compact(const uint8_t* bits, int64_t n, int64_t ld_bits, const uint8_t* keep_bits, const int64_t* offsets,
+                     int32_t* indices, void* stream) {
+  return guarded([&] {
+    if (n < 0 || (n && (!bits || !offsets)) || (ld_bits & 15)) throw Gm2Error("mask_compact: bad arguments");
+    launch_compact(bits, n, ld_bits, keep_bits, offsets, indices, (hipStream_t)stream);
+  });
+}
+
+int gm2_decode_bits(const gm2_dims* d, const float* params, const float* bn_running, const float* z, int64_t n,
+                    uint8_t* bits, int64_t ld_bits, float* probs, int64_t ld_probs, void* ws, void* stream) {
+  return guarded([&] {
+    const Layout lo = make_layout(d, GM2_F32);
+    if (n <= 0 || n > lo.d.Bm) throw Gm2Error("decode rows %lld outside (0, batch_max]", (long long)n);
+    if (ld_bits < gm2_packed_row_bytes(lo.d.G) || (probs && ld_probs < lo.d.G)) throw Gm2Error("decode_bits: ld too small");
+    Ctx<float> c(lo, ws, stream);
+    HIP_OK(hipMemcpy2DAsync(c.f(lo.Z), lo.d.Lr * 4, z, lo.d.L * 4, lo.d.L * 4, n, hipMemcpyDeviceToDevice, c.s));
+    decode_chain<float>(c, params, const_cast<float*>(bn_running), (int)n, nullptr, 0, probs, ld_probs, bits, ld_bits);
+  });
+}
+
+int gm2_recon_counts(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, const float* bn_running,
+                     float threshold, int32_t* counts, void* ws, void* stream) {
+  return guarded([&] {
+    const Layout lo = make_layout(d, prec);
+    if (!batch->eps) throw Gm2Error("recon_counts: eps required (model(x) samples z)");
+    if (!counts) throw Gm2Error("recon_counts: counts required");
+    HIP_OK(hipMemsetAsync(counts, 0, (size_t)batch->n * 3 * 4, (hipStream_t)stream));
+    float* bn = const_cast<float*>(bn_running);  // eval mode never writes running stats
+    auto run = [&](auto tag) {
+      using T = decltype(tag);
+      Ctx<T> c(lo, ws, stream);
+      forward<T>(c, batch, params, bn, 0, 0, nullptr, nullptr, nullptr, nullptr, 0, counts, threshold);
+    };
+    if (prec == GM2_F32) run(float{});
+    else run(bf16_t{});
   });
 }
 

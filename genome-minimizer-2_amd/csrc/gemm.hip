@@ -659,33 +659,106 @@ constexpr int recon_lds_bytes() {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Epilogue 3: sampling output layer. mask = logit > 0x33C00000 (== sigmoid_fp32 > 0.5,
-// extras.py:200-201); optional probabilities p = sigmoid(logit) (extras.py:198).
+// Epilogue 3: sampling / evaluation output layer. pred = sigmoid_fp32(logit) > thr: for thr = 0.5
+// (the reference's extras.py:200-201 `> 0.5`) as logit > 0x33C00000, else p > thr with
+// p = 1 / (1 + exp(-logit)) in fp32. The tile's predictions go through an LDS u8 image and leave as
+//   * mask  u8 [m][ldm] (full-row byte runs; 16-byte stores when ldm allows), and/or
+//   * bits  [m][ldb] bytes, numpy packbits(bitorder='little') rows: bit (n & 7) of byte n / 8, and/or
+//   * counts int32 [m][3] += (TP, FP, FN) against the row-major target bits (metrics.py:19-64), and/or
+//   * probs fp32 [m][ldpr] = p (extras.py:198).
 // ---------------------------------------------------------------------------------------------
+struct MaskOut {
+  uint8_t* mask; int64_t ldm;
+  uint8_t* bits; int64_t ldb;
+  float* probs; int64_t ldpr;
+  int* counts; const uint32_t* xbits; int64_t ldxb;
+  float thr;
+};
+
 template <class C, typename T>
-__global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float* __restrict__ bias,
-                                                   uint8_t* __restrict__ mask, int64_t ldm, float* __restrict__ probs,
-                                                   int64_t ldpr) {
+__global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float* __restrict__ bias, MaskOut o) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
   f32x4 acc[C::FM][C::FN];
   mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
+  constexpr int PI = C::BN + 16;  // u8 image pitch
+  uint8_t* img = (uint8_t*)smem;  // [BM][PI] (mainloop staging is free after its last barrier)
+  const bool half = o.thr == 0.5f;
 #pragma unroll
   for (int ni = 0; ni < C::FN; ++ni) {
-    const int n = tl.n0 + wn * C::WTN + ni * 16 + (lane & 15);
-    if (n >= g.N) continue;
-    const float bn = bias[n];
+    const int nl = wn * C::WTN + ni * 16 + (lane & 15);
+    const int n = tl.n0 + nl;
+    const float bn = n < g.N ? bias[n] : 0.f;
 #pragma unroll
     for (int mi = 0; mi < C::FM; ++mi)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int m = tl.m0 + wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
-        if (m >= g.M) continue;
+        const int ml = wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
+        const int m = tl.m0 + ml;
         const float l = acc[mi][ni][j] + bn;
-        if (mask) mask[(int64_t)m * ldm + n] = l > kMaskLogitThreshold ? 1 : 0;
-        if (probs) probs[(int64_t)m * ldpr + n] = 1.0f / (1.0f + expf(-l));
+        float p = 0.f;
+        if (o.probs || !half) p = 1.0f / (1.0f + expf(-l));
+        const bool pred = n < g.N && (half ? l > kMaskLogitThreshold : p > o.thr);
+        img[ml * PI + nl] = pred ? 1 : 0;
+        if (o.probs && m < g.M && n < g.N) o.probs[(int64_t)m * o.ldpr + n] = p;
       }
+  }
+  __syncthreads();
+  const int rows = min(C::BM, g.M - tl.m0);
+  if (o.mask) {
+    // one row per 8 threads' 16-byte pieces (or byte runs when the rows are not 16-B aligned)
+    const bool vec = (o.ldm & 15) == 0 && (((uintptr_t)o.mask) & 15) == 0 && tl.n0 + C::BN <= g.N;
+    if (vec) {
+      constexpr int CPR = C::BN / 16;
+      for (int i = threadIdx.x; i < rows * CPR; i += C::NT) {
+        const int r = i / CPR, cc = i % CPR;
+        *(uint4*)(o.mask + (int64_t)(tl.m0 + r) * o.ldm + tl.n0 + cc * 16) = *(const uint4*)(img + r * PI + cc * 16);
+      }
+    } else {
+      const int cols = min(C::BN, g.N - tl.n0);
+      for (int i = threadIdx.x; i < rows * C::BN; i += C::NT) {
+        const int r = i / C::BN, cc = i % C::BN;
+        if (cc < cols) o.mask[(int64_t)(tl.m0 + r) * o.ldm + tl.n0 + cc] = img[r * PI + cc];
+      }
+    }
+  }
+  if (o.bits) {
+    // 8 image bytes -> one packed byte; BN / 8 bytes per row, written 16 at a time
+    constexpr int BPR = C::BN / 8;
+    static_assert(BPR % 16 == 0, "packed row piece");
+    for (int i = threadIdx.x; i < rows * (BPR / 16); i += C::NT) {
+      const int r = i / (BPR / 16), cc = i % (BPR / 16);
+      uint32_t w[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const uint2 e = *(const uint2*)(img + r * PI + cc * 128 + (k * 4 + b) * 8);
+          const uint32_t lo = e.x * 0x10204080u, hi = e.y * 0x10204080u;  // gather byte LSBs
+          v |= (((lo >> 28) | ((hi >> 28) << 4)) & 0xFFu) << (8 * b);
+        }
+        w[k] = v;
+      }
+      *(uint4*)(o.bits + (int64_t)(tl.m0 + r) * o.ldb + tl.n0 / 8 + cc * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+  if (o.counts) {
+    // per-row TP / FP / FN of this tile against the target bits; integer atomics (exact)
+    constexpr int WPR = C::BN / 32;  // target words per tile row
+    for (int i = threadIdx.x; i < rows * WPR; i += C::NT) {
+      const int r = i / WPR, k = i % WPR;
+      uint32_t pw = 0;
+#pragma unroll
+      for (int b = 0; b < 32; ++b) pw |= (uint32_t)img[r * PI + k * 32 + b] << b;
+      const uint32_t xw = o.xbits[(int64_t)(tl.m0 + r) * o.ldxb + (tl.n0 >> 5) + k];
+      int* cr = o.counts + (int64_t)(tl.m0 + r) * 3;
+      const int tp = __builtin_popcount(pw & xw), fp = __builtin_popcount(pw & ~xw), fn = __builtin_popcount(~pw & xw);
+      if (tp) atomicAdd(cr + 0, tp);
+      if (fp) atomicAdd(cr + 1, fp);
+      if (fn) atomicAdd(cr + 2, fn);
+    }
   }
 }
 
@@ -927,11 +1000,16 @@ void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const uint3
 
 template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs, int64_t ldpr,
-                      hipStream_t s) {
+                      hipStream_t s, uint8_t* bits, int64_t ldb, int* counts, const uint32_t* xbits, int64_t ldxb,
+                      float thr) {
   check_gemm(g, 128);
+  if (bits && ((ldb & 15) || (((uintptr_t)bits) & 15) || ldb * 8 < g.Np))
+    throw Gm2Error("mask bits: row pitch %lld must be a multiple of 16 bytes covering the padded genes", (long long)ldb);
+  if (counts && (!xbits || ldxb * 32 < g.Np)) throw Gm2Error("mask counts: target bits required");
+  MaskOut o{mask, ldm, bits, ldb, probs, ldpr, counts, xbits, ldxb, thr};
   TimedLaunch tl(kKcMask, s);
   hipLaunchKernelGGL((k_gemm_mask<Small, T>), dim3((g.Mp / 128) * (g.Np / 128)), dim3(Small::NT), Small::LDS, s, g,
-                     bias, mask, ldm, probs, ldpr);
+                     bias, o);
   GM2_CHECK_LAUNCH();
 }
 
@@ -947,8 +1025,8 @@ GM2_INST(float)
 GM2_INST(bf16_t)
 #undef GM2_INST
 template void launch_gemm_mask<float>(const GemmArgs<float>&, const float*, uint8_t*, int64_t, float*, int64_t,
-                                      hipStream_t);
+                                      hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float);
 template void launch_gemm_mask<bf16_t>(const GemmArgs<bf16_t>&, const float*, uint8_t*, int64_t, float*, int64_t,
-                                       hipStream_t);
+                                       hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float);
 
 }  // namespace gm2

@@ -101,9 +101,11 @@ template <typename T>
 void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const uint32_t* xbits, int64_t ldxb, int with_grad,
                             const float* scal, T* dL, int64_t ldd, float* loss_part, float* colpart, int64_t ldcol,
                             hipStream_t s);
+// output layer + threshold (sampling / metrics): u8 mask, packed bits, probs, per-row (TP, FP, FN)
 template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs,
-                      int64_t ldpr, hipStream_t s);
+                      int64_t ldpr, hipStream_t s, uint8_t* bits = nullptr, int64_t ldb = 0, int* counts = nullptr,
+                      const uint32_t* xbits = nullptr, int64_t ldxb = 0, float thr = 0.5f);
 
 // ---- kernels.hip ----
 constexpr int kBnRowChunk = 128;  // rows per BatchNorm partial-statistics chunk
@@ -157,6 +159,14 @@ void launch_slab_sum(const float* slabs, int S, int64_t slab, int M, int N, floa
                      int64_t ldc, hipStream_t s);
 // out[i] = sum of partial buffers in double, fixed order (loss record slots)
 void launch_reduce_to(const float* part, int n, int stride, int count, double* out, hipStream_t s);
+
+// ---- masks.hip: consumers of the packed sampled masks ----
+void launch_count_groups(const uint8_t* bits, int64_t n, int64_t ldb, const int32_t* goff, int64_t ngroups,
+                         const int32_t* pos, int32_t* counts, hipStream_t s);
+void launch_row_offsets(const uint8_t* bits, int64_t n, int64_t ldb, const uint8_t* keep, int64_t* offsets,
+                        hipStream_t s);
+void launch_compact(const uint8_t* bits, int64_t n, int64_t ldb, const uint8_t* keep, const int64_t* offsets,
+                    int32_t* idx, hipStream_t s);
 
 // parameter tensor table for the multi-tensor optimizer / shadow kernels
 struct TensorDesc {

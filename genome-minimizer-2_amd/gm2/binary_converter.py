@@ -2,10 +2,13 @@
 explore_data/binary_converter.py (load_files :11-17, masks_to_gene_lists :19-76,
 check_essential_genes :78-121) with the same files, names, ordering and errors.
 
-The reference thresholds and compacts one Python row at a time; here a 2-D mask array is
-thresholded in one vectorised pass and each row compacted with one `nonzero`. Outputs are the same
-object arrays (`np.array(list_of_lists, dtype=object)`, so equal-length rows become a 2-D object
-array exactly as there).
+The reference thresholds and compacts one Python row at a time. Here a 2-D mask array is
+thresholded in one vectorised pass (the same float64 `>= threshold`) and, on a GPU box, packed 8 genes
+per byte, uploaded and compacted on the device (gm2.masks: gm2_mask_row_offsets + gm2_mask_compact,
+a row-popcount scan and a wave-parallel bit compaction) into a CSR of column indices that the host
+turns into name lists; without a GPU the same CSR comes from numpy. Outputs are the same object
+arrays (`np.array(list_of_lists, dtype=object)`, so equal-length rows become a 2-D object array
+exactly as there).
 """
 from __future__ import annotations
 
@@ -48,6 +51,24 @@ def _threshold_rows(masks, P, threshold):
     return np.stack(rows, axis=0) if rows else np.zeros((0, P), dtype=bool)
 
 
+def gene_index_csr(M):
+    """(row offsets, ascending column indices) of a boolean [N, P] mask: on the device when one is
+    visible (packed upload + gm2 compaction), else numpy."""
+    import torch
+    if M.shape[0] and torch.cuda.is_available():
+        from .masks import PackedMasks
+        return PackedMasks.from_host(M, threshold=True).gene_index_csr()
+    nz = np.nonzero(M)
+    offsets = np.zeros(M.shape[0] + 1, dtype=np.int64)
+    np.cumsum(np.bincount(nz[0], minlength=M.shape[0]), out=offsets[1:])
+    return offsets, nz[1].astype(np.int32)
+
+
+def gene_lists_from_csr(offsets, idx, names):
+    from .masks import gene_lists_from_csr as f
+    return f(offsets, idx, names)
+
+
 def masks_to_gene_lists(masks_npy_path: str, cols, out_ids_npy: str, threshold: float = 0.5):
     """Threshold each mask row (>= threshold) and list the present genes' names in column order;
     duplicate gene names keep their first occurrence (binary_converter.py:29-36)."""
@@ -68,7 +89,8 @@ def masks_to_gene_lists(masks_npy_path: str, cols, out_ids_npy: str, threshold: 
             masks = masks[None, :]
     M = _threshold_rows(masks, P, threshold)
     N = M.shape[0]
-    id_lists = [cols[np.flatnonzero(M[i])].tolist() for i in range(N)]
+    offsets, idx = gene_index_csr(M)
+    id_lists = gene_lists_from_csr(offsets, idx, cols)
     if out_ids_npy:
         os.makedirs(os.path.dirname(out_ids_npy) or ".", exist_ok=True)
         np.save(out_ids_npy, np.array(id_lists, dtype=object))

@@ -53,7 +53,12 @@ def get_latent_variables(model, data_loader, device=None):
 def count_essential_genes(binary_generated_samples, essential_gene_positions):
     """Per sample, how many essential genes are present: a gene counts when ANY of its column
     positions (< G; negative positions index from the end, as numpy does there) is non-zero after
-    `astype(int)` (extras.py:65-85), vectorised over samples instead of the per-sample loop."""
+    `astype(int)` (extras.py:65-85). Packed device masks (gm2.masks.PackedMasks, what --mode sample
+    produces) are counted on the GPU (gm2_mask_count_groups); a host array keeps the reference's
+    host semantics, vectorised over samples instead of the per-sample loop."""
+    from .masks import PackedMasks
+    if isinstance(binary_generated_samples, PackedMasks):
+        return binary_generated_samples.count_groups(essential_gene_positions)
     b = np.asarray(binary_generated_samples)
     G = b.shape[1]
     # the reference tests `astype(int) != 0` (truncation: 0.7 counts as absent)

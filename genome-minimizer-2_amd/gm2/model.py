@@ -259,6 +259,21 @@ class VAE:
                                None if probs is None else probs[s:], G)
         return mask, probs
 
+    def decode_bits(self, z, want_probs=False, chunk=65536):
+        """Like decode_mask, but the masks stay on the device packed 8 genes per byte
+        (gm2.masks.PackedMasks): what --mode sample hands to the mask consumers."""
+        from .masks import PackedMasks
+        z = z.to(self.device, torch.float32).contiguous()
+        N, G = z.shape[0], self.input_dim
+        pm = PackedMasks.empty(N, G, self.device)
+        probs = torch.empty(N, G, dtype=torch.float32, device=self.device) if want_probs else None
+        for s in range(0, N, chunk):
+            n = min(chunk, N - s)
+            ws = self.workspace(native.GM2_F32, min(chunk, N))
+            native.decode_bits(ws, self.params, self.bn, z[s:s + n], n, pm.bits[s:], pm.ld,
+                               None if probs is None else probs[s:], G)
+        return pm, probs
+
     def encode(self, x):
         """(mean, logvar) of the eval-mode encoder (model.py:95-98) for a 0/1 matrix x [B, G]
         (every reference call site encodes an eval()'d model: extras.py:205-228)."""

@@ -26,7 +26,8 @@ S_ONE_MINUS_B1, S_BETA2, S_ONE_MINUS_B2, S_ADAM_EPS = 6, 7, 8, 9
 EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_offsets",
            "gm2_workspace_size", "gm2_workspace_init", "gm2_sync_shadows", "gm2_train_fwd_bwd",
            "gm2_grad_norm", "gm2_adam_step", "gm2_eval_forward", "gm2_decode_mask", "gm2_encode", "gm2_forward", "gm2_backward_outputs",
-           "gm2_reparameterize",
+           "gm2_reparameterize", "gm2_packed_row_bytes", "gm2_decode_bits", "gm2_mask_count_groups",
+           "gm2_mask_row_offsets", "gm2_mask_compact", "gm2_recon_counts",
            "gm2_gemm", "gm2_grad_bucket_bounds", "gm2_wait_grad_bucket", "gm2_set_option", "gm2_get_option", "gm2_timing_begin", "gm2_timing_end"]
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
 OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE = 1, 2, 3
@@ -71,6 +72,12 @@ def lib():
         "gm2_forward": (C.c_int, [dp, i32, C.POINTER(Batch), vp, vp, i32, vp, i64, vp, vp, vp, vp]),
         "gm2_backward_outputs": (C.c_int, [dp, i32, C.POINTER(Batch), vp, i32, vp, i64, vp, vp, vp, vp, vp, vp]),
         "gm2_reparameterize": (C.c_int, [i64, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "gm2_packed_row_bytes": (C.c_int64, [i64]),
+        "gm2_decode_bits": (C.c_int, [dp, vp, vp, vp, i64, vp, i64, vp, i64, vp, vp]),
+        "gm2_mask_count_groups": (C.c_int, [vp, i64, i64, vp, i64, vp, vp, vp]),
+        "gm2_mask_row_offsets": (C.c_int, [vp, i64, i64, vp, vp, vp]),
+        "gm2_mask_compact": (C.c_int, [vp, i64, i64, vp, vp, vp, vp]),
+        "gm2_recon_counts": (C.c_int, [dp, i32, C.POINTER(Batch), vp, vp, C.c_float, vp, vp, vp]),
         "gm2_gemm": (C.c_int, [i32, i32, i32, vp, i64, vp, i64, vp, i64, i64, i64, i64, i32, vp, vp]),
         "gm2_grad_bucket_bounds": (C.c_int, [dp, C.POINTER(C.c_int64)]),
         "gm2_wait_grad_bucket": (C.c_int, [i32, vp]),
@@ -187,6 +194,36 @@ def backward_outputs(ws: Workspace, batch: Batch, params, train, probs, ld_probs
 def reparameterize(n, mu, logvar, eps, z, dz=None, dmu=None, dlogvar=None):
     check(lib().gm2_reparameterize(int(n), ptr(mu), ptr(logvar), ptr(eps), ptr(z), ptr(dz), ptr(dmu), ptr(dlogvar),
                                    stream()), "gm2_reparameterize")
+
+
+def packed_row_bytes(G: int) -> int:
+    """Row pitch (bytes) of a packed mask of G genes (gm2.h)."""
+    return int(lib().gm2_packed_row_bytes(int(G)))
+
+
+def decode_bits(ws: Workspace, params, bn, z, n, bits, ld_bits, probs=None, ld_probs=0):
+    check(lib().gm2_decode_bits(C.byref(ws.d), ptr(params), ptr(bn), ptr(z), int(n), ptr(bits), int(ld_bits),
+                                ptr(probs), int(ld_probs), ws.ptr, stream()), "gm2_decode_bits")
+
+
+def mask_count_groups(bits, n, ld_bits, group_offsets, n_groups, positions, counts):
+    check(lib().gm2_mask_count_groups(ptr(bits), int(n), int(ld_bits), ptr(group_offsets), int(n_groups),
+                                      ptr(positions), ptr(counts), stream()), "gm2_mask_count_groups")
+
+
+def mask_row_offsets(bits, n, ld_bits, keep_bits, offsets):
+    check(lib().gm2_mask_row_offsets(ptr(bits), int(n), int(ld_bits), ptr(keep_bits), ptr(offsets), stream()),
+          "gm2_mask_row_offsets")
+
+
+def mask_compact(bits, n, ld_bits, keep_bits, offsets, indices):
+    check(lib().gm2_mask_compact(ptr(bits), int(n), int(ld_bits), ptr(keep_bits), ptr(offsets), ptr(indices),
+                                 stream()), "gm2_mask_compact")
+
+
+def recon_counts(ws: Workspace, batch: Batch, params, bn, threshold, counts):
+    check(lib().gm2_recon_counts(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), ptr(bn), float(threshold),
+                                 ptr(counts), ws.ptr, stream()), "gm2_recon_counts")
 
 
 def gemm(prec, P, ldp, Q, ldq, Cout, ldc, M, N, K, splits=1, slab=None, p_kmajor=True, q_kmajor=True):

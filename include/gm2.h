@@ -138,6 +138,35 @@ int gm2_decode_mask(const gm2_dims* d, const float* params, const float* bn_runn
                     int64_t n, uint8_t* mask, int64_t ld_mask, float* probs, int64_t ld_probs, void* ws,
                     void* stream);
 
+/* Packed sampled masks: numpy packbits(bitorder='little') rows, bit (g & 7) of byte g / 8 = gene g,
+ * row pitch ld_bits >= gm2_packed_row_bytes(G) (a multiple of 16), bits beyond G zero. 8x less HBM
+ * and PCIe than the u8 mask; what --mode sample keeps on the device for the mask consumers. */
+int64_t gm2_packed_row_bytes(int64_t G);
+
+/* gm2_decode_mask with a packed output: bits [n][ld_bits] (+ optional probs). */
+int gm2_decode_bits(const gm2_dims* d, const float* params, const float* bn_running, const float* z, int64_t n,
+                    uint8_t* bits, int64_t ld_bits, float* probs, int64_t ld_probs, void* ws, void* stream);
+
+/* count_essential_genes (extras.py:49-87) on packed masks: counts[i] = number of groups g (essential
+ * genes) with ANY set position in positions[group_offsets[g] .. group_offsets[g+1]) (all < G). */
+int gm2_mask_count_groups(const uint8_t* bits, int64_t n, int64_t ld_bits, const int32_t* group_offsets,
+                          int64_t n_groups, const int32_t* positions, int32_t* counts, void* stream);
+
+/* masks_to_gene_lists (binary_converter.py:19-76) as a CSR of gene column indices: offsets[n+1]
+ * (int64, exclusive scan of the row popcounts of bits AND keep_bits), then the ascending set
+ * columns of every row at indices[offsets[i] ..]. keep_bits (one packed row, NULL = all) drops
+ * duplicate gene names (binary_converter.py:29-36 keeps the first occurrence). */
+int gm2_mask_row_offsets(const uint8_t* bits, int64_t n, int64_t ld_bits, const uint8_t* keep_bits, int64_t* offsets,
+                         void* stream);
+int gm2_mask_compact(const uint8_t* bits, int64_t n, int64_t ld_bits, const uint8_t* keep_bits, const int64_t* offsets,
+                     int32_t* indices, void* stream);
+
+/* calculate_reconstruction_metrics (training/evaluation/metrics.py:19-64) without materialising the
+ * reconstruction: eval-mode model(x) of `batch` (eps given: the reference samples z there too), then
+ * per strain counts[i] = (TP, FP, FN) of (recon > threshold) against the strain's genes. */
+int gm2_recon_counts(const gm2_dims* d, int precision, const gm2_batch* batch, const float* params,
+                     const float* bn_running, float threshold, int32_t* counts, void* ws, void* stream);
+
 /* Encoder of VAE.encode (model.py:95-98), eval-mode BatchNorm, on `batch` (eps unused):
  * mu and logvar fp32 [n][L] (either may be NULL). Used by get_latent_variables (extras.py:205-228). */
 int gm2_encode(const gm2_dims* d, int precision, const gm2_batch* batch, const float* params,
