@@ -10,9 +10,11 @@ clip, Adam. N>1 (torchrun): one process per GPU, each rank steps its own 4096 ro
 SUM-all-reduced over RCCL every step (weak scaling: value = all ranks' rows / max-rank time).
 
 Also reported (extra fields, not `value`): sampling throughput of `--mode sample` for the v1 preset
-(C3: genomes/s decoded in exact fp32 + thresholded to u8 masks, in HBM), the live-timed dominant
-kernel against the MFMA roofline, and the CPU baseline (the oracle = the reference's algorithm on
-torch-CPU, fp32, all host threads, a bounded sample of the same workload).
+(C3: 1e6 genomes/s decoded in exact fp32, thresholded into packed masks, essential genes counted on
+the device, masks + counts copied to pinned host memory), the same training step in the other GEMM
+precision (f32 next to the bf16 headline), the live-timed dominant kernel against the MFMA roofline,
+and the CPU baseline (the oracle = the reference's algorithm on torch-CPU, fp32, all host threads,
+the same v0 step at batch 4096 on the same matrix; plus the C1 batch-64 point).
 """
 import argparse
 import json
@@ -73,7 +75,7 @@ def parse():
     ap.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sample", action="store_true")
-    ap.add_argument("--sample-genomes", type=int, default=262144)
+    ap.add_argument("--sample-genomes", type=int, default=1000000)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-f32-line", action="store_true")
     return ap.parse_args()
@@ -277,8 +279,14 @@ def main():
 
 
 def sample_bench(a, dev):
-    """C3: v1 preset (hidden 512, latent 32) `--mode sample` decode, genomes/s, masks left in HBM."""
+    """C3: v1 preset (hidden 512, latent 32) `--mode sample` of a.sample_genomes genomes (1e6 by
+    default) in 65,536-genome chunks: z ~ N(0, I) drawn on the device (extras.py:197), exact-fp32
+    decode + threshold into packed masks in HBM (gm2_decode_bits), the essential-gene counts of
+    every genome on the device (gm2_mask_count_groups, a synthetic 300-gene essential table), and
+    the packed masks + counts copied to pinned host memory on a second stream (overlapping the next
+    chunk's decode). genomes/s = all of that, end to end; the .npy write to disk is excluded."""
     from gm2 import native
+    from gm2.masks import essential_groups
     from gm2.model import VAE
     G, H, L = a.genes, 512, 32
     torch.manual_seed(0)
@@ -286,25 +294,55 @@ def sample_bench(a, dev):
     m.eval()
     chunk = 65536
     n = a.sample_genomes
-    z = torch.randn(n, L, device=dev)
-    mask = torch.empty(chunk, G, dtype=torch.uint8, device=dev)
+    ldb = native.packed_row_bytes(G)
+    rng = np.random.Generator(np.random.PCG64(3))
+    ess = {f"e{i}": [int(p) for p in rng.integers(0, G, size=int(rng.integers(1, 4)))] for i in range(300)}
+    offs, pos = essential_groups(ess, G)
+    go, po = torch.from_numpy(offs).to(dev), torch.from_numpy(pos).to(dev)
+    host_bits = torch.empty(n, ldb, dtype=torch.uint8, pin_memory=True)   # where the masks end up
+    host_cnt = torch.empty(n, dtype=torch.int32, pin_memory=True)
+    dbits = [torch.empty(chunk, ldb, dtype=torch.uint8, device=dev) for _ in range(2)]
+    dcnt = [torch.empty(chunk, dtype=torch.int32, device=dev) for _ in range(2)]
+    copy = torch.cuda.Stream(device=dev)
+    done = [torch.cuda.Event(), torch.cuda.Event()]
     ws = m.workspace(native.GM2_F32, chunk)
-    native.decode_mask(ws, m.params, m.bn, z[:chunk], chunk, mask, G)  # warm-up
+
+    def run(timed):
+        z = torch.randn(n, L, device=dev)
+        cur = torch.cuda.current_stream(dev)
+        for k, s in enumerate(range(0, n, chunk)):
+            b = k & 1
+            cnt = min(chunk, n - s)
+            cur.wait_event(done[b])  # the copy of the chunk that last used this buffer has finished
+            native.decode_bits(ws, m.params, m.bn, z[s:s + cnt], cnt, dbits[b], ldb)
+            native.mask_count_groups(dbits[b], cnt, ldb, go, len(offs) - 1, po, dcnt[b])
+            copy.wait_stream(cur)
+            with torch.cuda.stream(copy):
+                host_bits[s:s + cnt].copy_(dbits[b][:cnt], non_blocking=True)
+                host_cnt[s:s + cnt].copy_(dcnt[b][:cnt], non_blocking=True)
+                done[b].record(copy)
+        torch.cuda.synchronize()
+
+    # warm-up on one chunk's worth
+    native.decode_bits(ws, m.params, m.bn, torch.randn(chunk, L, device=dev), chunk, dbits[0], ldb)
     torch.cuda.synchronize()
     native.timing_begin(native.KC_MASK)
     t0 = time.perf_counter()
-    for s in range(0, n, chunk):
-        k = min(chunk, n - s)
-        native.decode_mask(ws, m.params, m.bn, z[s:s + k], k, mask, G)
-    torch.cuda.synchronize()
+    run(True)
     dt = time.perf_counter() - t0
     k_ms, k_n = native.timing_end()
     gps = n / dt
     kflops = 2.0 * chunk * H * G
     ach = kflops / (k_ms / max(k_n, 1) * 1e-3) / 1e12
+    # the packed masks that reached the host are the decode's: spot-check the last chunk on device
+    last = (n - 1) // chunk * chunk
+    assert torch.equal(host_bits[last:n].to(dev), dbits[((n - 1) // chunk) & 1][:n - last])
     traffic, traffic_src = pmc_traffic(a, "k_gemm_mask")
     return {"genomes_per_s": round(gps, 1), "preset": "v1", "genomes": n, "chunk": chunk, "dtype": "f32",
+            "mask_format": "packed bits (numpy packbits, little)", "includes": "z draw, decode, threshold, pack, "
+            "essential-gene counts, D2H of packed masks + counts to pinned host memory",
             "decode_tflops": round(gps * decode_flops_per_genome(G, H, L) / 1e12, 2),
+            "mean_essential_present": round(float(host_cnt.float().mean()), 2),
             "roofline": {"bound": "mfma", "kernel": "k_gemm_mask<f32>", "achieved": round(ach, 2),
                          "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_TFLOPS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,

@@ -82,6 +82,9 @@ def masks_to_gene_lists(masks_npy_path: str, cols, out_ids_npy: str, threshold: 
         cols = cols[keep]
         P = len(cols)
     masks = np.load(masks_npy_path, allow_pickle=True)
+    if masks.dtype == np.uint8 and masks.ndim == 2 and P > 8 and masks.shape[1] == (P + 7) // 8:
+        # `main.py --mode sample --mask-dtype bits`: numpy packbits(bitorder='little') rows
+        masks = np.unpackbits(masks, axis=1, count=P, bitorder="little")
     if masks.ndim == 1:
         if len(masks) and isinstance(masks[0], (list, np.ndarray)):
             masks = np.array([np.asarray(row) for row in masks], dtype=object)

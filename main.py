@@ -20,9 +20,11 @@ runs strain-row data parallelism over RCCL (gm2/ddp.py): every rank trains its s
 rank 0 prints and saves the checkpoint. Other modes run on rank 0 only.
 
 Additions (no reference equivalent): --precision bf16|f32 for the training GEMMs (sampling always
-decodes in exact fp32), --mask-dtype float64|uint8 for the saved masks (the reference writes float64
-via `.astype(float)`, main.py:369-371 / extras.py:200-201; uint8 keeps 1e6-genome runs in memory),
---no-csv to skip the genes x samples CSV.
+decodes in exact fp32), --mask-dtype float64|uint8|bits for the saved masks (the reference writes
+float64 via `.astype(float)`, main.py:369-371 / extras.py:200-201; uint8 keeps 1e6-genome runs in
+memory; bits = numpy packbits(bitorder='little') rows, 1/64 of float64, accepted by convert-samples),
+--no-csv to skip the genes x samples CSV. Sampling keeps the masks packed on the GPU: genome sizes
+and essential-gene counts are computed there (gm2/masks.py) and only the packed rows cross PCIe.
 """
 import argparse
 import os
@@ -51,7 +53,7 @@ def parse_arguments(argv=None):
     p.add_argument("--noise-level", type=float, default=0.1)
     p.add_argument("--project-root", type=str, default=os.environ.get("GM2_PROJECT_ROOT", os.getcwd()))
     p.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
-    p.add_argument("--mask-dtype", choices=["float64", "uint8"], default="float64")
+    p.add_argument("--mask-dtype", choices=["float64", "uint8", "bits"], default="float64")
     p.add_argument("--no-csv", action="store_true")
     return p.parse_args(argv)
 
@@ -107,9 +109,9 @@ def detect_version(model_path):
     return None
 
 
-def focused_samples(model, latent_dim, num_samples, noise_level, device):
+def focused_z(model, latent_dim, num_samples, noise_level, device):
     """main.py:351-370: 100 default samples, the one with fewest genes, then its output-space
-    nearest sample's z (the same index), decoded again under z* + noise_level * N(0, I)."""
+    nearest sample's z (the same index); returns z* + noise_level * N(0, I) [num_samples, L]."""
     import numpy as np
     import torch
     from gm2.extras import sample_from_model
@@ -119,7 +121,12 @@ def focused_samples(model, latent_dim, num_samples, noise_level, device):
     closest = np.argmin(dist)
     z_star = z_temp[closest].unsqueeze(0)
     noise = torch.randn(num_samples, latent_dim, device=device) * noise_level
-    z = z_star + noise
+    return z_star + noise
+
+
+def focused_samples(model, latent_dim, num_samples, noise_level, device):
+    """(u8 mask [N, G] on the device, z) of focused sampling."""
+    z = focused_z(model, latent_dim, num_samples, noise_level, device)
     mask, _ = model.decode_mask(z)
     return mask, z
 
@@ -131,7 +138,7 @@ def run_sampling(args):
     import torch
     from gm2.data import load_and_validate_data
     from gm2.experiments import PRESETS
-    from gm2.extras import count_essential_genes, load_model, sample_from_model, write_samples_to_dataframe
+    from gm2.extras import count_essential_genes, load_model, write_samples_to_dataframe
 
     if not args.model_path:
         print("✗ Model path required for sampling mode")
@@ -162,22 +169,26 @@ def run_sampling(args):
     print(f"- Architecture: {input_dim} -> {config.hidden_dim} -> {config.latent_dim}")
     print(f"- Samples: {args.num_samples}\n- Mode: {args.sampling_mode}\n- Output: {out_dir}")
     if args.sampling_mode == "default":
-        binary, _, _ = sample_from_model(model, config.latent_dim, args.num_samples, device,
-                                         binary_dtype=np.uint8, return_probs=False)
+        with torch.no_grad():
+            z = torch.randn(args.num_samples, config.latent_dim, device=device)  # extras.py:197
     else:
-        mask, _ = focused_samples(model, config.latent_dim, args.num_samples, args.noise_level, device)
-        binary = mask.cpu().numpy()
-    sizes = binary.sum(axis=1, dtype=np.int64)
-    ess = count_essential_genes(binary, essential_gene_positions)
-    print(f"\n✓ Sampling Results:\n- Generated samples: {binary.shape[0]}")
+        z = focused_z(model, config.latent_dim, args.num_samples, args.noise_level, device)
+    packed, _ = model.decode_bits(z)          # masks stay on the GPU, 8 genes per byte
+    sizes = packed.row_sizes()                # binary.sum(axis=1)
+    ess = count_essential_genes(packed, essential_gene_positions)  # on the device
+    print(f"\n✓ Sampling Results:\n- Generated samples: {packed.n}")
     print(f"- Median genome size: {np.median(sizes):.0f} genes")
     print(f"- Genome size range: {np.min(sizes):.0f} - {np.max(sizes):.0f}")
     print(f"- Median essential genes: {np.median(ess):.0f}")
     print(f"- Essential range: {np.min(ess):.0f} - {np.max(ess):.0f}")
-    out = binary.astype(np.float64) if args.mask_dtype == "float64" else binary
+    if args.mask_dtype == "bits":
+        out = packed.to_host()
+    else:
+        out = packed.unpack(np.float64 if args.mask_dtype == "float64" else np.uint8)
     np.save(out_dir / f"{config.trainer_version}_binary_samples_{args.sampling_mode}.npy", out)
     if not args.no_csv:
-        write_samples_to_dataframe(out, all_genes, f"{out_dir}/{config.trainer_version}_data_full_samples_df.csv")
+        rows = out if args.mask_dtype != "bits" else packed.unpack(np.uint8)
+        write_samples_to_dataframe(rows, all_genes, f"{out_dir}/{config.trainer_version}_data_full_samples_df.csv")
     print(f"\n✓ SAMPLING COMPLETE!\n- Results saved to: {out_dir}")
     return True
 

@@ -154,3 +154,24 @@ def test_cli_training_then_sampling(tmp_path, capsys):
     df = pd.read_csv(os.path.join(out, "v0_data_full_samples_df.csv"))
     assert df.shape == (300, 41) and df.columns[0] == "Gene"
     assert x.shape == (96, 300)
+    # --mask-dtype bits: the same masks packed (numpy packbits, bitorder little); the printed
+    # statistics come from the device (sizes, essential counts) and convert-samples reads the file
+    capsys.readouterr()
+    torch.manual_seed(1234)
+    rc = cli.main(["--mode", "sample", "--model-path", ckpt, "--genes-path", pkl, "--num-samples", "40",
+                   "--project-root", root, "--mask-dtype", "bits", "--no-csv"])
+    assert rc == 0
+    printed = capsys.readouterr().out
+    bits = np.load(os.path.join(out, "v0_binary_samples_default.npy"))
+    assert bits.dtype == np.uint8 and bits.shape == (40, (300 + 7) // 8)
+    np.testing.assert_array_equal(np.unpackbits(bits, axis=1, count=300, bitorder="little"), masks.astype(np.uint8))
+    from gm2.extras import count_essential_genes
+    ess = count_essential_genes(masks, pos)
+    assert f"- Median essential genes: {np.median(ess):.0f}" in printed
+    assert f"- Median genome size: {np.median(masks.sum(axis=1)):.0f} genes" in printed
+    ids_out = os.path.join(root, "ids.npy")
+    assert cli.main(["--mode", "convert-samples", "--genes-path", os.path.join(out, "v0_binary_samples_default.npy"),
+                     "--output-file", ids_out, "--project-root", root]) == 0
+    ids = np.load(ids_out, allow_pickle=True)  # written by our own code just above
+    genes = [f"gene{i:05d}" for i in range(300)]
+    assert [list(r) for r in ids] == [[genes[j] for j in np.flatnonzero(r)] for r in masks]
