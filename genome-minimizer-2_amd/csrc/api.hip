@@ -121,7 +121,7 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.Z = take(Bm * d.Lr * es);        // z [Bm][Lr]
   o.dL = take(Bm * d.Gp * es);       // dL/dlogit [Bm][Gp]
   const int64_t maxN = std::max<int64_t>({H, 2 * d.L, d.Lr, 128});
-  o.slab_cap = std::max<int64_t>(1024LL * kTile * kTile, Bm * maxN);
+  o.slab_cap = std::max<int64_t>(1024LL * kTile * kTile, 4 * Bm * maxN);
   o.slabs = take(o.slab_cap * 4);
   // weight-gradient GEMMs run on a side stream: their own split-K scratch, one dY per layer
   o.side_cap = std::max<int64_t>(8LL * H * std::max<int64_t>(H, d.L2r), 1024LL * kTile * kTile);
@@ -791,6 +791,7 @@ int gm2_set_option(int key, int value) {
         if (value != 0 && value != 128 && value != 256) throw Gm2Error("recon tile %d: 0, 128 or 256", value);
         set_recon_tile(value);
         break;
+      case GM2_OPT_SMALL_SPLIT: set_small_split(value); break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });
@@ -802,6 +803,7 @@ int gm2_get_option(int key, int* value) {
       case GM2_OPT_GEMM_PP: *value = get_gemm_pp(); break;
       case GM2_OPT_SIDE_STREAM: *value = side_flag().load(); break;
       case GM2_OPT_RECON_TILE: *value = get_recon_tile(); break;
+      case GM2_OPT_SMALL_SPLIT: *value = get_small_split(); break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });

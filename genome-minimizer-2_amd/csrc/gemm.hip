@@ -833,6 +833,16 @@ static void check_gemm(const GemmArgs<T>& g, int tile) {
 // Tile / split-K plan. Big tiles when they alone fill the chip, or when K is long enough that a
 // split-K slab round trip is cheap next to the work; otherwise the 128-tile, split only when it
 // leaves most CUs idle (and never below 8 K-steps per slice).
+// split-K factor for the 128-tile GEMMs that alone fill the chip with one short-K tile per CU (the
+// hidden-layer GEMMs: 256 tiles, 16 K-steps): > 1 puts that many tiles on each CU so one's loads
+// hide behind another's MFMAs (option GM2_OPT_SMALL_SPLIT; default 1)
+static std::atomic<int>& small_split_flag() {
+  static std::atomic<int> v{1};
+  return v;
+}
+void set_small_split(int s) { small_split_flag().store(std::max(1, std::min(s, 8))); }
+int get_small_split() { return small_split_flag().load(); }
+
 template <typename T>
 GemmPlan plan_gemm(const GemmArgs<T>& g) {
   const int nk = g.K / E<T>::KT;
@@ -841,7 +851,10 @@ GemmPlan plan_gemm(const GemmArgs<T>& g) {
   auto cap = [&](int s) { return std::max(1, std::min({s, 8, std::max(1, nk / 8)})); };
   if (tiles_big >= 256) return {256, 1};
   if (tiles_big > 0 && g.K >= 8192) return {256, cap((256 + tiles_big - 1) / tiles_big)};
-  if (tiles_small >= 192) return {128, 1};
+  if (tiles_small >= 192) {
+    const int ss = small_split_flag().load(std::memory_order_relaxed);
+    return {128, (ss > 1 && tiles_small < 1024 && nk >= 8) ? cap(ss) : 1};
+  }
   return {128, cap((256 + tiles_small - 1) / tiles_small)};
 }
 

@@ -90,6 +90,8 @@ void set_gemm_pp(int on);
 int get_gemm_pp();
 void set_recon_tile(int t);
 int get_recon_tile();
+void set_small_split(int s);
+int get_small_split();
 struct GemmPlan {
   int tile, splits;
 };

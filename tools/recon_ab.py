@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""A/B of the output-layer loss kernel's tile (GM2_OPT_RECON_TILE 128 vs 256) on the C2 step shape,
-interleaved rounds in one process; reports the kernel's HIP-event time (KC_RECON_LOSS) and the step."""
+"""A/B of libgm2 tuning options on the C2 step shape, interleaved rounds in one process; reports the
+output-layer loss kernel's HIP-event time (KC_RECON_LOSS) and the step time.
+Usage: python3 tools/recon_ab.py OPTION v1 v2 ...   (OPTION = recon_tile | small_split | gemm_pp)"""
 import os
 import sys
 import time
@@ -38,10 +39,13 @@ def step(i):
     native.adam_step(ws, model.params, grads, opt.exp_avg, opt.exp_avg_sq, scal[i])
 
 
+opt_name = sys.argv[1] if len(sys.argv) > 1 else "recon_tile"
+vals = [int(v) for v in sys.argv[2:]] or [256, 128]
+key = {"recon_tile": native.OPT_RECON_TILE, "small_split": native.OPT_SMALL_SPLIT, "gemm_pp": native.OPT_GEMM_PP}[opt_name]
 res = {}
 for rnd in range(3):
-    for tile in (256, 128):
-        native.set_option(native.OPT_RECON_TILE, tile)
+    for tile in vals:
+        native.set_option(key, tile)
         for i in range(2):
             step(i)
         torch.cuda.synchronize()
@@ -56,4 +60,4 @@ for rnd in range(3):
 for tile, v in res.items():
     k = sorted(x[0] for x in v)[len(v) // 2]
     st = sorted(x[1] for x in v)[len(v) // 2]
-    print(f"recon tile {tile}: kernel {k * 1e3:.1f} us ({2 * B * H * G / (k * 1e-3) / 1e12:.0f} TF/s), step {st:.3f} ms")
+    print(f"{opt_name} {tile}: recon kernel {k * 1e3:.1f} us ({2 * B * H * G / (k * 1e-3) / 1e12:.0f} TF/s), step {st:.3f} ms")
