@@ -262,6 +262,22 @@ void gemm_to(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64
   launch_slab_sum(c.f(c.slab_off), S, slab, M, N, C0, C1, C1 ? msplit : M, ldc, c.s);
 }
 
+// Pre-BatchNorm Linear: Y = in . W^T + bias (fp32 [Bp][H]) and, when `stats`, the per-128-row
+// chunk (mean, M2) partials of Y -> part. One launch when the GEMM plan is a single pass of 128-row
+// tiles (statistics in the store epilogue); otherwise split-K slabs + k_bn_fwd_partial.
+template <typename T>
+void linear_pre_bn(const Ctx<T>& c, const T* in, int64_t ldin, int Bp, const T* W, int64_t ldw, int B, int H, int K,
+                   const float* bias, float* Y, float* part, bool stats) {
+  GemmArgs<T> g{in, ldin, W, ldw, B, H, K, Bp, H, 0};
+  BnEpi bn;
+  bn.mode = stats ? 1 : 0;
+  bn.part = (float2*)part;
+  bn.ldp = H;
+  if (launch_gemm_bn<T>(g, Y, H, bias, bn, c.s)) return;
+  const int S = gemm_to_slabs<T>(c, in, ldin, Bp, W, ldw, H, B, H, K, H);
+  launch_bn_fwd_partial(c.f(c.slab_off), S, (int64_t)Bp * H, H, bias, B, H, Y, part, c.s);
+}
+
 // the 6 BatchNorm blocks: (linear weight, linear bias, bn gamma, bn beta)
 const int kBlk[6][4] = {{E0W, E0B, E1G, E1BT}, {E3W, E3B, E4G, E4BT}, {E6W, E6B, E7G, E7BT},
                         {D0W, D0B, D1G, D1BT}, {D3W, D3B, D4G, D4BT}, {D6W, D6B, D7G, D7BT}};
@@ -348,9 +364,8 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
       ldin = d.Lr;
       Kin = (int)d.Lp;
     }
-    const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(shadow_in[i]), i == 3 ? d.Lr : Kin, H, B, H, Kin, H);
-    launch_bn_fwd_partial(c.f(l.slabs), S, (int64_t)Bp * H, H, prm + d.off[kBlk[i][1]], B, H, c.f(l.Y[i]),
-                          c.f(l.bnpart), c.s);
+    linear_pre_bn<T>(c, in, ldin, Bp, c.t(shadow_in[i]), i == 3 ? d.Lr : Kin, B, H, Kin, prm + d.off[kBlk[i][1]],
+                     c.f(l.Y[i]), c.f(l.bnpart), train != 0);
     launch_bn_fwd_finalize(c.f(l.bnpart), B, H, train, prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
                            bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, c.f(l.save[i]), c.f(l.bncoef), c.s);
     launch_bn_fwd_apply2<T>(c.f(l.Y[i]), H, c.f(l.bncoef), B, Bp, H, c.t(l.A[i]), c.s);
@@ -400,13 +415,32 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   fork();
   gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
   HIP_OK(hipEventRecord(be->ev[0], w.s));
-  int S = gemm_to_slabs<T>(c, c.t(l.dL), Gp, Bp, c.t(l.sD3), H, H, B, H, Gp, H, 1, 0);
+  // dA_j = dY . W (K-major dY, MN-major W) into the slab area; when the plan allows, the GEMM's
+  // epilogue also takes BatchNorm j's backward partials (sum do, sum (y-mean) do)
+  bool have_part = false;
+  auto dx_pre_bn = [&](const T* dY, int64_t lddy, const T* W, int64_t ldw, int K, int j) {
+    GemmArgs<T> g{dY, lddy, W, ldw, B, H, K, Bp, H, 0, 1, 0};
+    BnEpi bn;
+    bn.mode = 2;
+    bn.part = (float2*)c.f(l.bnpart);
+    bn.ldp = H;
+    bn.Y = c.f(l.Y[j]);
+    bn.ldy = H;
+    bn.save = c.f(l.save[j]);
+    bn.gamma = prm + d.off[kBlk[j][2]];
+    bn.beta = prm + d.off[kBlk[j][3]];
+    bn.H = H;
+    have_part = launch_gemm_bn<T>(g, c.f(c.slab_off), H, nullptr, bn, c.s);
+    return have_part ? 1 : gemm_to_slabs<T>(c, dY, lddy, Bp, W, ldw, H, B, H, K, H, 1, 0);
+  };
+  int S = dx_pre_bn(c.t(l.dL), Gp, c.t(l.sD3), H, Gp, 5);
   const int64_t shadow_w[6] = {l.sE0, l.sE1, l.sE2, l.sD0, l.sD1, l.sD2};
   for (int i = 5; i >= 0; --i) {
     const int64_t slab = (int64_t)Bp * H;
     const bool sum = S > 1;
-    launch_bn_bwd_partial(c.f(c.slab_off), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
-                          prm + d.off[kBlk[i][3]], B, H, c.f(l.bnpart), sum ? c.f(l.DA) : nullptr, c.s);
+    if (!have_part)
+      launch_bn_bwd_partial(c.f(c.slab_off), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
+                            prm + d.off[kBlk[i][3]], B, H, c.f(l.bnpart), sum ? c.f(l.DA) : nullptr, c.s);
     launch_bn_bwd_finalize(c.f(l.bnpart), B, H, train, c.f(l.save[i]), prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
                            gr + d.off[kBlk[i][2]], gr + d.off[kBlk[i][3]], c.f(l.bncoef), c.s);
     launch_bn_bwd_apply2<T>(sum ? c.f(l.DA) : c.f(c.slab_off), c.f(l.Y[i]), H, c.f(l.bncoef), B, Bp, H,
@@ -431,11 +465,11 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       fork();
       gemm_to<T>(w, c.t(l.dH), L2r, L2r, c.t(l.A[2]), H, H, 2 * L, H, Bp, gr + d.off[MUW], gr + d.off[LVW], L, H, 0,
                  0);
-      S = gemm_to_slabs<T>(c, c.t(l.dH), L2r, Bp, c.t(l.sHD), H, H, B, H, (int)d.K2L, H, 1, 0);
+      S = dx_pre_bn(c.t(l.dH), L2r, c.t(l.sHD), H, (int)d.K2L, 2);
       continue;
     }
     gemm_to<T>(w, dY, H, H, c.t(l.A[i - 1]), H, H, H, H, Bp, gr + d.off[kBlk[i][0]], nullptr, 0, H, 0, 0);
-    S = gemm_to_slabs<T>(c, dY, H, Bp, c.t(shadow_w[i]), H, H, B, H, H, H, 1, 0);
+    S = dx_pre_bn(dY, H, c.t(shadow_w[i]), H, H, i - 1);
   }
 }
 
@@ -452,9 +486,8 @@ void decode_chain(const Ctx<T>& c, const float* prm, float* bn, int n, uint8_t* 
   const int64_t shadow_in[3] = {l.sD0, l.sD1, l.sD2};
   for (int j = 0; j < 3; ++j) {
     const int i = 3 + j;
-    const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(shadow_in[j]), ldw, H, n, H, Kin, H);
-    launch_bn_fwd_partial(c.f(l.slabs), S, (int64_t)Bp * H, H, prm + d.off[kBlk[i][1]], n, H, c.f(l.Y[i]),
-                          c.f(l.bnpart), c.s);
+    linear_pre_bn<T>(c, in, ldin, Bp, c.t(shadow_in[j]), ldw, n, H, Kin, prm + d.off[kBlk[i][1]], c.f(l.Y[i]),
+                     c.f(l.bnpart), false);
     launch_bn_fwd_finalize(c.f(l.bnpart), n, H, 0, prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
                            bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, nullptr, c.f(l.bncoef), c.s);
     launch_bn_fwd_apply2<T>(c.f(l.Y[i]), H, c.f(l.bncoef), n, Bp, H, c.t(l.A[i]), c.s);
@@ -669,9 +702,8 @@ int gm2_encode(const gm2_dims* d, int prec, const gm2_batch* batch, const float*
       int Kin = (int)dd.Gp;
       const int64_t sh[3] = {lo.sE0, lo.sE1, lo.sE2};
       for (int i = 0; i < 3; ++i) {
-        const int S = gemm_to_slabs<T>(c, in, ldin, Bp, c.t(sh[i]), Kin, H, B, H, Kin, H);
-        launch_bn_fwd_partial(c.f(lo.slabs), S, (int64_t)Bp * H, H, params + dd.off[kBlk[i][1]], B, H, c.f(lo.Y[i]),
-                              c.f(lo.bnpart), c.s);
+        linear_pre_bn<T>(c, in, ldin, Bp, c.t(sh[i]), Kin, B, H, Kin, params + dd.off[kBlk[i][1]], c.f(lo.Y[i]),
+                         c.f(lo.bnpart), false);
         launch_bn_fwd_finalize(c.f(lo.bnpart), B, H, 0, params + dd.off[kBlk[i][2]], params + dd.off[kBlk[i][3]],
                                bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, nullptr, c.f(lo.bncoef), c.s);
         launch_bn_fwd_apply2<T>(c.f(lo.Y[i]), H, c.f(lo.bncoef), B, Bp, H, c.t(lo.A[i]), c.s);
@@ -792,6 +824,7 @@ int gm2_set_option(int key, int value) {
         set_recon_tile(value);
         break;
       case GM2_OPT_SMALL_SPLIT: set_small_split(value); break;
+      case GM2_OPT_BN_EPILOGUE: set_bn_epilogue(value); break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });
@@ -804,6 +837,7 @@ int gm2_get_option(int key, int* value) {
       case GM2_OPT_SIDE_STREAM: *value = side_flag().load(); break;
       case GM2_OPT_RECON_TILE: *value = get_recon_tile(); break;
       case GM2_OPT_SMALL_SPLIT: *value = get_small_split(); break;
+      case GM2_OPT_BN_EPILOGUE: *value = get_bn_epilogue(); break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });

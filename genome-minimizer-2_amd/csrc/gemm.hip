@@ -388,10 +388,20 @@ __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_
 // Epilogue 1: fp32 store. Rows m < msplit go to C0, rows >= msplit to C1 (row m - msplit); the
 // split-K slice z writes slab z (C0 + z*slab). Optional per-column bias.
 // ---------------------------------------------------------------------------------------------
+//
+// Optional BatchNorm statistics of the stored tile (bn.mode != 0; 128-row tiles, one K pass, no
+// row split -- the host checks): per (128-row chunk = row tile, column) partials in the format of
+// k_bn_fwd_partial / k_bn_bwd_partial, so the separate statistics pass over Y / dA disappears.
+//   mode 1 (forward): v = acc + bias -> (chunk mean, M2), from sums of v - shift in fp32 with the
+//           shift = the tile's first row (stable: the shift is a sample of the column).
+//   mode 2 (backward): acc = dA; do = dA * [y*alpha + beta' > 0] with y read from bn.Y ->
+//           (sum do, sum (y - mean) do).
+// The store loop visits a fixed column per thread (NT % BN == 0), so the sums stay in registers
+// and the NT/BN threads of a column are combined through LDS once at the end.
 template <class C, typename T, bool AK, bool BK, bool PP>
 __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __restrict__ C0, float* __restrict__ C1,
                                                     int msplit, int64_t ldc, int64_t slab,
-                                                    const float* __restrict__ bias) {
+                                                    const float* __restrict__ bias, BnEpi bn) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
   const int kbeg = tl.split * g.k_per_split;
@@ -409,6 +419,15 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
   // accumulator's own layout would write four 64-byte pieces of four rows).
   float* img = (float*)smem;
   static_assert(C::WTM * C::BN * 4 <= C::LDS, "epilogue band must fit the staging LDS");
+  static_assert(C::NT % C::BN == 0, "the store loop keeps one column per thread");
+  const int my_cc = threadIdx.x % C::BN, my_n = tl.n0 + my_cc;
+  const float my_b = (bias && my_n < g.N) ? bias[my_n] : 0.f;
+  float sa = 0.f, sb = 0.f, shift = 0.f, bmean = 0.f, balpha = 0.f, bbeta = 0.f;
+  if (bn.mode == 2 && my_n < g.N) {
+    bmean = bn.save[my_n];
+    balpha = bn.save[bn.H + my_n] * bn.gamma[my_n];
+    bbeta = fmaf(-bmean, balpha, bn.beta[my_n]);
+  }
 #pragma unroll
   for (int h = 0; h < C::WGM; ++h) {
     if (wm == h) {
@@ -421,16 +440,47 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
             img[(mi * 16 + 4 * (lane >> 4) + j) * C::BN + wn * C::WTN + ni * 16 + (lane & 15)] = acc[mi][ni][j];
     }
     __syncthreads();
+    if (h == 0) shift = img[my_cc] + my_b;  // the tile's first row (always < M)
     for (int i = threadIdx.x; i < C::WTM * C::BN; i += C::NT) {
-      const int r = i / C::BN, cc = i % C::BN;
-      const int m = tl.m0 + h * C::WTM + r, n = tl.n0 + cc;
+      const int r = i / C::BN;
+      const int m = tl.m0 + h * C::WTM + r, n = my_n;
       if (m < g.M && n < g.N) {
-        const float v = img[i] + (bias ? bias[n] : 0.f);
+        const float v = img[i] + my_b;
         if (m < msplit) Cz[(int64_t)m * ldc + n] = v;
         else C1[(int64_t)(m - msplit) * ldc + n] = v;
+        if (bn.mode == 1) {
+          const float dv = v - shift;
+          sa += dv;
+          sb = fmaf(dv, dv, sb);
+        } else if (bn.mode == 2) {
+          const float y = bn.Y[(int64_t)m * bn.ldy + n];
+          const float d = fmaf(y, balpha, bbeta) > 0.f ? v : 0.f;
+          sa += d;
+          sb = fmaf(y - bmean, d, sb);
+        }
       }
     }
     __syncthreads();
+  }
+  if (bn.mode) {
+    float2* red = (float2*)smem;
+    red[threadIdx.x] = make_float2(sa, sb);
+    __syncthreads();
+    if (threadIdx.x < C::BN && my_n < g.N) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int k = 0; k < C::NT / C::BN; ++k) {
+        a += red[threadIdx.x + k * C::BN].x;
+        b += red[threadIdx.x + k * C::BN].y;
+      }
+      float2 o = make_float2(a, b);
+      if (bn.mode == 1) {
+        const float nr = (float)min(C::BM, g.M - tl.m0);
+        const float dm = a / nr;
+        o = make_float2(shift + dm, fmaxf(fmaf(-a, dm, b), 0.f));
+      }
+      bn.part[(int64_t)(tl.m0 / C::BM) * bn.ldp + my_n] = o;
+    }
   }
 }
 
@@ -893,24 +943,24 @@ static void ensure_lds_attr(const void* fn, int bytes) {
 
 template <class C, typename T, bool AK, bool BK, bool PP>
 static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
-                           const float* bias, hipStream_t s) {
+                           const float* bias, const BnEpi& bn, hipStream_t s) {
   ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP>, C::LDS);
   hipLaunchKernelGGL((k_gemm_store<C, T, AK, BK, PP>), dim3(tiles), dim3(C::NT), C::LDS, s, a, C0, C1 ? C1 : C0,
-                     C1 ? msplit : (1 << 30), ldc, slab, bias);
+                     C1 ? msplit : (1 << 30), ldc, slab, bias, bn);
 }
 
 template <class C, typename T, bool AK, bool BK>
 static void store_launch(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
-                         const float* bias, hipStream_t s) {
+                         const float* bias, const BnEpi& bn, hipStream_t s) {
   if constexpr (std::is_same_v<C, Big> && sizeof(T) == 2) {
-    if (pp_enabled()) return store_launch_k<C, T, AK, BK, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, s);
+    if (pp_enabled()) return store_launch_k<C, T, AK, BK, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
   }
-  store_launch_k<C, T, AK, BK, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, s);
+  store_launch_k<C, T, AK, BK, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
 }
 
 template <class C, typename T>
 static int store_impl(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
-                      const float* bias, hipStream_t s) {
+                      const float* bias, const BnEpi& bn, hipStream_t s) {
   GemmArgs<T> a = g;
   const int kt = E<T>::KT;
   const int nkt = g.K / kt;
@@ -919,9 +969,9 @@ static int store_impl(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
   splits = (int)((g.K + a.k_per_split - 1) / a.k_per_split);
   const int tiles = (g.Mp / C::BM) * (g.Np / C::BN) * splits;
   TimedLaunch tl(kKcGemmStore, s);
-  if (g.pk && g.qk) store_launch<C, T, true, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, s);
-  else if (g.pk && !g.qk) store_launch<C, T, true, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, s);
-  else if (!g.pk && !g.qk) store_launch<C, T, false, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, s);
+  if (g.pk && g.qk) store_launch<C, T, true, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+  else if (g.pk && !g.qk) store_launch<C, T, true, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+  else if (!g.pk && !g.qk) store_launch<C, T, false, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
   else throw Gm2Error("gemm: layout (P MN-major, Q K-major) not instantiated");
   GM2_CHECK_LAUNCH();
   return splits;
@@ -931,12 +981,33 @@ template <typename T>
 int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
                       const float* bias, hipStream_t s) {
   if (splits < 0) splits = plan_gemm(g).splits;
+  const BnEpi none{};
   if (use_big(g)) {
     check_gemm(g, 256);
-    return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, s);
+    return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
   }
   check_gemm(g, 128);
-  return store_impl<Small, T>(g, splits, C0, C1, msplit, ldc, slab, bias, s);
+  return store_impl<Small, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
+}
+
+// BatchNorm statistics in the store epilogue (GM2_OPT_BN_EPILOGUE, default on): taken when the
+// plan is one pass of 128-row tiles (the statistics chunk), else the caller runs the separate pass
+static std::atomic<int>& bn_epi_flag() {
+  static std::atomic<int> on{1};
+  return on;
+}
+void set_bn_epilogue(int on) { bn_epi_flag().store(on ? 1 : 0, std::memory_order_relaxed); }
+int get_bn_epilogue() { return bn_epi_flag().load(std::memory_order_relaxed); }
+
+template <typename T>
+bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const BnEpi& bn, hipStream_t s) {
+  static_assert(Small::BM == kBnRowChunk, "statistics chunk = row tile");
+  if (!bn_epi_flag().load(std::memory_order_relaxed)) return false;
+  const GemmPlan p = plan_gemm(g);
+  if (p.tile != 128 || p.splits != 1) return false;
+  check_gemm(g, 128);
+  store_impl<Small, T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s);
+  return true;
 }
 
 template <typename T>
@@ -1027,6 +1098,7 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
 }
 
 #define GM2_INST(T)                                                                                              \
+  template bool launch_gemm_bn<T>(const GemmArgs<T>&, float*, int64_t, const float*, const BnEpi&, hipStream_t);   \
   template int launch_gemm_store<T>(const GemmArgs<T>&, int, float*, float*, int, int64_t, int64_t, const float*, \
                                     hipStream_t);                                                                \
   template int gemm_recon_grid_blocks<T>(const GemmArgs<T>&);                                                   \

@@ -77,6 +77,24 @@ struct TimedLaunch {  // records an event pair around a launch when its class is
 };
 
 // ---- gemm.hip ----
+// BatchNorm statistics computed in a GEMM store epilogue (see k_gemm_store)
+struct BnEpi {
+  int mode = 0;             // 0 off; 1 forward (chunk mean, M2) of C; 2 backward (sum do, sum (y-mean) do)
+  float2* part = nullptr;   // [row tile][ldp]
+  int64_t ldp = 0;
+  const float* Y = nullptr;  // mode 2: the layer's pre-BN output, row pitch ldy
+  int64_t ldy = 0;
+  const float* save = nullptr;  // mode 2: mean[H], invstd[H]
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  int H = 0;
+};
+// GEMM + BatchNorm statistics of its output in one launch when the plan allows (one K pass of
+// 128-row tiles); returns false (nothing launched) otherwise
+template <typename T>
+bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const BnEpi& bn, hipStream_t s);
+void set_bn_epilogue(int on);
+int get_bn_epilogue();
 // splits < 0: use plan_gemm's split-K factor. Returns the number of slabs written.
 template <typename T>
 int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc,

@@ -218,8 +218,17 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       the caller's stream. Initial value from env GM2_SIDE_STREAM.
  *   GM2_OPT_RECON_TILE  output-layer loss GEMM tile: 0 = plan (default), 128 or 256 = force.
  *   GM2_OPT_SMALL_SPLIT split-K factor (1..8) of the chip-filling short-K 128-tile GEMMs (the
- *                       hidden layers). */
-enum { GM2_OPT_GEMM_PP = 1, GM2_OPT_SIDE_STREAM = 2, GM2_OPT_RECON_TILE = 3, GM2_OPT_SMALL_SPLIT = 4 };
+ *                       hidden layers).
+ *   GM2_OPT_BN_EPILOGUE 1 = BatchNorm batch statistics (forward) and backward partial sums taken
+ *                       in the producing GEMM's store epilogue where the plan allows (default),
+ *                       0 = always a separate statistics pass. */
+enum {
+  GM2_OPT_GEMM_PP = 1,
+  GM2_OPT_SIDE_STREAM = 2,
+  GM2_OPT_RECON_TILE = 3,
+  GM2_OPT_SMALL_SPLIT = 4,
+  GM2_OPT_BN_EPILOGUE = 5
+};
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);
 

@@ -38,6 +38,16 @@ def gemm_pp(request):
     native.set_option(native.OPT_GEMM_PP, old)
 
 
+@pytest.fixture(params=[0, 1], ids=["bnpass", "bnepi"])
+def bn_epi(request):
+    """BatchNorm statistics in the GEMM store epilogue, or the separate statistics pass
+    (gm2_set_option GM2_OPT_BN_EPILOGUE)."""
+    old = native.get_option(native.OPT_BN_EPILOGUE)
+    native.set_option(native.OPT_BN_EPILOGUE, request.param)
+    yield request.param
+    native.set_option(native.OPT_BN_EPILOGUE, old)
+
+
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
 @pytest.mark.parametrize("prec", ["f32", "bf16"])
 @pytest.mark.parametrize("M,N,K,splits", [(128, 128, 64, 1), (200, 300, 192, 1), (256, 1024, 1024, 1),
@@ -173,9 +183,11 @@ def _prebn_bias(name):
                                             (1000, 128, 64, 64, 1.2, 0.01),
                                             # >= 128 256x256 output tiles: the big-tile recon kernel
                                             (8192, 256, 32, 1024, 0.55, 0.01)])
-def test_train_step_vs_oracle(prec, G, H, L, B, wg, lam, gemm_pp):
+def test_train_step_vs_oracle(prec, G, H, L, B, wg, lam, gemm_pp, bn_epi):
     """One fused fwd+bwd (+clip+L1+Adam) against the oracle's explicit gradients and its
-    autograd-driven step (trainer.py:109-120 semantics)."""
+    autograd-driven step (trainer.py:109-120 semantics). The shapes cover both BatchNorm statistics
+    routes under bn_epi=1: one-pass 128-row-tile GEMMs take them in the epilogue, the split-K
+    input layer of the last shape keeps the separate pass."""
     P, S = perturb_bn(*oracle_state(G, H, L, G + B), seed=9)
     X = synth_x(B, G, B)
     torch.manual_seed(1)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of libgm2 tuning options on the C2 step shape, interleaved rounds in one process; reports the
 output-layer loss kernel's HIP-event time (KC_RECON_LOSS) and the step time.
-Usage: python3 tools/recon_ab.py OPTION v1 v2 ...   (OPTION = recon_tile | small_split | gemm_pp)"""
+Usage: python3 tools/recon_ab.py OPTION v1 v2 ...   (OPTION = recon_tile | small_split | gemm_pp | bn_epilogue)"""
 import os
 import sys
 import time
@@ -41,7 +41,8 @@ def step(i):
 
 opt_name = sys.argv[1] if len(sys.argv) > 1 else "recon_tile"
 vals = [int(v) for v in sys.argv[2:]] or [256, 128]
-key = {"recon_tile": native.OPT_RECON_TILE, "small_split": native.OPT_SMALL_SPLIT, "gemm_pp": native.OPT_GEMM_PP}[opt_name]
+key = {"recon_tile": native.OPT_RECON_TILE, "small_split": native.OPT_SMALL_SPLIT, "gemm_pp": native.OPT_GEMM_PP,
+       "bn_epilogue": native.OPT_BN_EPILOGUE}[opt_name]
 res = {}
 for rnd in range(3):
     for tile in vals:
