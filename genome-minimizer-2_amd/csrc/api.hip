@@ -85,7 +85,8 @@ struct Layout {
   // the forward GEMM and as an MN-major operand ([K=out][N=in]) in the backward dX GEMM
   int64_t sE0, sE1, sE2, sHD, sD0, sD1, sD2, sD3;
   int64_t X, XB, Y[6], A[6], save[6], HD, Z, dL, slabs, slab_cap, side_slabs, side_cap, dY[6], DA, dH;
-  int64_t bncoef, bnpart, colpart, colpart_cap, losspart, losspart_cap, klpart, gradpart, clip, scal0, total;
+  int64_t AT5, dYT0;  // transposed A5 / dY0 [H][Bm]: K-major operands of the dW9 / dWe0 GEMMs
+  int64_t bnpart, colpart, colpart_cap, losspart, losspart_cap, klpart, gradpart, clip, scal0, total;
 };
 
 Layout make_layout(const gm2_dims* gd, int prec) {
@@ -129,8 +130,9 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   for (int i = 0; i < 6; ++i) o.dY[i] = take(Bm * H * es);
   o.DA = take(Bm * H * 4);           // summed split-K input gradient (fp32)
   o.dH = take(Bm * d.L2r * es);      // d(mu | logvar) [Bm][L2r]
+  o.AT5 = take(H * Bm * es);
+  o.dYT0 = take(H * Bm * es);
   o.bnpart = take((Bm / kBnRowChunk) * H * 8);
-  o.bncoef = take(5 * H * 4);
   o.colpart_cap = std::max<int64_t>({(Bm / 64) * d.Gp, (Bm / 64) * H, (Bm / 64) * 2 * d.L});
   o.colpart = take(o.colpart_cap * 4);
   o.losspart_cap = std::max<int64_t>((d.Gp / kTile) * (Bm / kTile) * 2, Bm / 64);
@@ -269,7 +271,7 @@ template <typename T>
 void linear_pre_bn(const Ctx<T>& c, const T* in, int64_t ldin, int Bp, const T* W, int64_t ldw, int B, int H, int K,
                    const float* bias, float* Y, float* part, bool stats) {
   GemmArgs<T> g{in, ldin, W, ldw, B, H, K, Bp, H, 0};
-  BnEpi bn;
+  StoreEpi bn;
   bn.mode = stats ? 1 : 0;
   bn.part = (float2*)part;
   bn.ldp = H;
@@ -366,9 +368,9 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
     }
     linear_pre_bn<T>(c, in, ldin, Bp, c.t(shadow_in[i]), i == 3 ? d.Lr : Kin, B, H, Kin, prm + d.off[kBlk[i][1]],
                      c.f(l.Y[i]), c.f(l.bnpart), train != 0);
-    launch_bn_fwd_finalize(c.f(l.bnpart), B, H, train, prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
-                           bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, c.f(l.save[i]), c.f(l.bncoef), c.s);
-    launch_bn_fwd_apply2<T>(c.f(l.Y[i]), H, c.f(l.bncoef), B, Bp, H, c.t(l.A[i]), c.s);
+    launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train, prm + d.off[kBlk[i][2]],
+                           prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
+                           c.f(l.save[i]), c.t(l.A[i]), c.s);
     in = c.t(l.A[i]);
     ldin = H;
     Kin = H;
@@ -412,15 +414,26 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   BucketEvents* be = bucket_events();
   // output layer: dW9[g][h] = sum_b dL[b][g] A5[b][h] ; dA5[b][h] = sum_g dL[b][g] W9[g][h]
   // (its bias gradient was summed in the forward's recon epilogue, before the fork)
+  // Written as dW9^T[h][g] = sum_b A5^T[h][b] dL[b][g] with A5^T K-major (a transposed copy made
+  // here) and dL MN-major, stored transposed: one transposed-read operand instead of two (the
+  // 256x256 tile is LDS-read bound with two). Plans with split-K keep the both-MN-major form.
   fork();
-  gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
+  {
+    GemmArgs<T> g9{c.t(l.AT5), Bp, c.t(l.dL), Gp, H, G, Bp, H, Gp, 0, 1, 0};
+    if (plan_gemm<T>(g9).splits == 1) {
+      launch_transpose<T>(c.t(l.A[5]), H, Bp, H, c.t(l.AT5), Bp, w.s);
+      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, w.s);
+    } else {
+      gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
+    }
+  }
   HIP_OK(hipEventRecord(be->ev[0], w.s));
   // dA_j = dY . W (K-major dY, MN-major W) into the slab area; when the plan allows, the GEMM's
   // epilogue also takes BatchNorm j's backward partials (sum do, sum (y-mean) do)
   bool have_part = false;
   auto dx_pre_bn = [&](const T* dY, int64_t lddy, const T* W, int64_t ldw, int K, int j) {
     GemmArgs<T> g{dY, lddy, W, ldw, B, H, K, Bp, H, 0, 1, 0};
-    BnEpi bn;
+    StoreEpi bn;
     bn.mode = 2;
     bn.part = (float2*)c.f(l.bnpart);
     bn.ldp = H;
@@ -441,16 +454,17 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     if (!have_part)
       launch_bn_bwd_partial(c.f(c.slab_off), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
                             prm + d.off[kBlk[i][3]], B, H, c.f(l.bnpart), sum ? c.f(l.DA) : nullptr, c.s);
-    launch_bn_bwd_finalize(c.f(l.bnpart), B, H, train, c.f(l.save[i]), prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
-                           gr + d.off[kBlk[i][2]], gr + d.off[kBlk[i][3]], c.f(l.bncoef), c.s);
-    launch_bn_bwd_apply2<T>(sum ? c.f(l.DA) : c.f(c.slab_off), c.f(l.Y[i]), H, c.f(l.bncoef), B, Bp, H,
-                            c.t(l.dY[i]), c.f(l.colpart), c.s);
+    launch_bn_bwd_apply<T>(sum ? c.f(l.DA) : c.f(c.slab_off), c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train,
+                           c.f(l.save[i]), prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]], gr + d.off[kBlk[i][2]],
+                           gr + d.off[kBlk[i][3]], c.t(l.dY[i]), c.f(l.colpart), c.s);
     launch_colsum(c.f(l.colpart), Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, c.s);
     const T* dY = c.t(l.dY[i]);
     if (i == 0) {  // input layer: weight gradient only (on the main stream: nothing left to overlap)
+      // dWe0[h][g] = sum_b dY0^T[h][b] X[b][g]: dY0^T (K-major copy) x X (MN-major)
+      launch_transpose<T>(dY, H, Bp, H, c.t(l.dYT0), Bp, c.s);
       if (sr) order(sr, w.s, c.s);  // join: every hidden-layer weight gradient is final
       HIP_OK(hipEventRecord(be->ev[1], c.s));
-      gemm_to<T>(c, dY, H, H, c.t(l.X), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 0, 0);
+      gemm_to<T>(c, c.t(l.dYT0), Bp, H, c.t(l.X), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0);
       HIP_OK(hipEventRecord(be->ev[2], c.s));
       be->recorded = true;
       break;
@@ -488,9 +502,8 @@ void decode_chain(const Ctx<T>& c, const float* prm, float* bn, int n, uint8_t* 
     const int i = 3 + j;
     linear_pre_bn<T>(c, in, ldin, Bp, c.t(shadow_in[j]), ldw, n, H, Kin, prm + d.off[kBlk[i][1]], c.f(l.Y[i]),
                      c.f(l.bnpart), false);
-    launch_bn_fwd_finalize(c.f(l.bnpart), n, H, 0, prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
-                           bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, nullptr, c.f(l.bncoef), c.s);
-    launch_bn_fwd_apply2<T>(c.f(l.Y[i]), H, c.f(l.bncoef), n, Bp, H, c.t(l.A[i]), c.s);
+    launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), n, Bp, H, 0, prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
+                           bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, nullptr, c.t(l.A[i]), c.s);
     in = c.t(l.A[i]);
     ldin = H;
     Kin = H;
@@ -704,9 +717,9 @@ int gm2_encode(const gm2_dims* d, int prec, const gm2_batch* batch, const float*
       for (int i = 0; i < 3; ++i) {
         linear_pre_bn<T>(c, in, ldin, Bp, c.t(sh[i]), Kin, B, H, Kin, params + dd.off[kBlk[i][1]], c.f(lo.Y[i]),
                          c.f(lo.bnpart), false);
-        launch_bn_fwd_finalize(c.f(lo.bnpart), B, H, 0, params + dd.off[kBlk[i][2]], params + dd.off[kBlk[i][3]],
-                               bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, nullptr, c.f(lo.bncoef), c.s);
-        launch_bn_fwd_apply2<T>(c.f(lo.Y[i]), H, c.f(lo.bncoef), B, Bp, H, c.t(lo.A[i]), c.s);
+        launch_bn_fwd_apply<T>(c.f(lo.Y[i]), H, c.f(lo.bnpart), B, Bp, H, 0, params + dd.off[kBlk[i][2]],
+                               params + dd.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
+                               nullptr, c.t(lo.A[i]), c.s);
         in = c.t(lo.A[i]);
         ldin = H;
         Kin = H;

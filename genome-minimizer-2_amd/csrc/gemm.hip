@@ -35,17 +35,33 @@ namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-template <int BM_, int BN_, int WGM_, int WGN_>
+// Diagnostic timestamps (s_memrealtime, 100 MHz) of the store kernel's phases per workgroup; only
+// compiled into the standalone probe tools/stamp_gemm.hip, never into libgm2.
+#ifdef GM2_STAMPS
+__device__ unsigned long long g_stamp[16384][4];
+#define GM2_STAMP(i) \
+  if (threadIdx.x == 0) g_stamp[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define GM2_STAMP(i)
+#endif
+
+template <int BM_, int BN_, int WGM_, int WGN_, int NS_ = 2>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_;
   static constexpr int NT = 64 * WGM * WGN;          // threads
   static constexpr int WTM = BM / WGM, WTN = BN / WGN;
   static constexpr int FM = WTM / 16, FN = WTN / 16;  // 16x16 fragments per wave
   static constexpr int STAGE = (BM + BN) * 128;      // bytes per pipeline stage
-  static constexpr int LDS = 2 * STAGE;
+  static constexpr int NS = NS_;                     // pipeline stages in LDS
+  static constexpr int LDS = NS * STAGE;
+  static constexpr int LPS = (BM + BN) * 8 / NT;     // global_load_lds per thread per stage
 };
 using Big = Cfg<256, 256, 2, 4>;
 using Small = Cfg<128, 128, 2, 2>;
+// The fp32-output 128x128 tiles (hidden-layer GEMMs: one tile per CU, K = 1024 in 16 steps of
+// ~0.2 us of MFMA each, against ~1 us from global_load_lds issue to landing): a 4-stage ring keeps
+// three K-steps in flight instead of one.
+using SmallDeep = Cfg<128, 128, 2, 2, 4>;
 
 struct TileXY {
   int m0, n0, split, t;
@@ -154,6 +170,15 @@ __device__ __forceinline__ f32x4 frag_f32(const char* tile, int r0, int s, int l
   }
 }
 
+// Wait until at most `r` (0 <= r <= NS - 2; negative = 0) later stages' loads are in flight.
+template <class C>
+__device__ __forceinline__ void wait_stages(int r) {
+  static_assert(C::NS <= 4 && 2 * C::LPS <= 63, "vmcnt range");
+  if (C::NS >= 4 && r >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C::LPS) : "memory");
+  else if (C::NS >= 3 && r >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::LPS) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Main loop. acc[mi][ni][j] = C[m0 + wm*WTM + mi*16 + 4*(lane>>4) + j][n0 + wn*WTN + ni*16 + (lane&15)]
 // AK / BK: P / Q stored K-major (true) or MN-major (false).
 template <class C, typename T, bool AK, bool BK>
@@ -175,13 +200,20 @@ __device__ __forceinline__ void mainloop(const T* __restrict__ P, int64_t ldp, c
     if constexpr (BK) stage_kmajor<C, T, C::BN>(Q, ldq, n0, k0, buf + C::BM * 128, wid, lane);
     else stage_mnmajor<C, T, C::BN>(Q, ldq, n0, k0, buf + C::BM * 128, wid, lane);
   };
-  stage(smem, kbeg);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // NS-stage ring: K-step kt lives in buffer kt % NS; step kt + NS - 1 is issued at the top of
+  // step kt into the buffer step kt - 1 used (every wave passed the barrier after reading it).
+  // The wait at the end of step kt lets the stages after kt + 1 stay in flight (counted vmcnt).
+  constexpr int NS = C::NS;
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st)
+    if (st < nk) stage(smem + st * C::STAGE, kbeg + st * KT);
+  wait_stages<C>(min(NS - 2, nk - 1));
   __syncthreads();
+  GM2_STAMP(1);
 
   for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * C::STAGE;
-    if (kt + 1 < nk) stage(smem + ((kt + 1) & 1) * C::STAGE, kbeg + (kt + 1) * KT);
+    char* cur = smem + (kt % NS) * C::STAGE;
+    if (kt + NS - 1 < nk) stage(smem + ((kt + NS - 1) % NS) * C::STAGE, kbeg + (kt + NS - 1) * KT);
     const char* sA = cur;
     const char* sB = cur + C::BM * 128;
     if constexpr (sizeof(T) == 2) {
@@ -215,7 +247,7 @@ __device__ __forceinline__ void mainloop(const T* __restrict__ P, int64_t ldp, c
         }
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wait_stages<C>(min(NS - 2, nk - 2 - kt));
     __syncthreads();
   }
 }
@@ -396,13 +428,14 @@ __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_
 //           shift = the tile's first row (stable: the shift is a sample of the column).
 //   mode 2 (backward): acc = dA; do = dA * [y*alpha + beta' > 0] with y read from bn.Y ->
 //           (sum do, sum (y - mean) do).
-// The store loop visits a fixed column per thread (NT % BN == 0), so the sums stay in registers
-// and the NT/BN threads of a column are combined through LDS once at the end.
+// The store loop visits 4 fixed columns per thread, so the sums stay in registers and the threads
+// of a column are combined through LDS once at the end.
 template <class C, typename T, bool AK, bool BK, bool PP>
 __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __restrict__ C0, float* __restrict__ C1,
                                                     int msplit, int64_t ldc, int64_t slab,
-                                                    const float* __restrict__ bias, BnEpi bn) {
+                                                    const float* __restrict__ bias, StoreEpi bn) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  GM2_STAMP(0);
   const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
   const int kbeg = tl.split * g.k_per_split;
   const int kend = min(g.K, kbeg + g.k_per_split);
@@ -412,76 +445,138 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
     mainloop_pp<AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
   else
     mainloop<C, T, AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
+  GM2_STAMP(2);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   float* Cz = C0 + (int64_t)tl.split * slab;
-  // Stage one wave-row band (WTM x BN fp32) at a time through the (now free) staging LDS, then
-  // store whole rows: each wave instruction writes 256 contiguous bytes of one C row (the
-  // accumulator's own layout would write four 64-byte pieces of four rows).
+  // Stage one 64-row band of the tile at a time through the (now free) staging LDS (row pitch
+  // BN + 4 floats: the accumulator writes of lanes 16 apart land 16 banks apart), then store whole
+  // rows with 16-byte stores (4 columns per thread; scalar where C's rows are not 16-B aligned or
+  // at the N edge).
+  // Transposed store (bn.trans): 16 lanes write 4 consecutive m each of one column n (256
+  // contiguous bytes of C^T's row n), reading the image down a column (odd pitch: conflict-free).
   float* img = (float*)smem;
-  static_assert(C::WTM * C::BN * 4 <= C::LDS, "epilogue band must fit the staging LDS");
-  static_assert(C::NT % C::BN == 0, "the store loop keeps one column per thread");
-  const int my_cc = threadIdx.x % C::BN, my_n = tl.n0 + my_cc;
-  const float my_b = (bias && my_n < g.N) ? bias[my_n] : 0.f;
-  float sa = 0.f, sb = 0.f, shift = 0.f, bmean = 0.f, balpha = 0.f, bbeta = 0.f;
-  if (bn.mode == 2 && my_n < g.N) {
-    bmean = bn.save[my_n];
-    balpha = bn.save[bn.H + my_n] * bn.gamma[my_n];
-    bbeta = fmaf(-bmean, balpha, bn.beta[my_n]);
+  const int pitch = bn.trans ? C::BN + 1 : C::BN + 4;
+  constexpr int BR = 64, NBANDS = C::BM / BR, BPW = C::WTM / BR;  // bands, bands per wave row
+  static_assert(BR * (C::BN + 4) * 4 <= C::LDS, "epilogue band must fit the staging LDS");
+  constexpr int TPR = C::BN / 4, RPI = C::NT / TPR;  // threads per row, rows per pass
+  static_assert(C::NT % TPR == 0 && BR % RPI == 0 && 2 * C::NT * 16 <= C::LDS, "epilogue shape");
+  const int cq = (threadIdx.x % TPR) * 4, rq = threadIdx.x / TPR;
+  const int n = tl.n0 + cq;
+  const bool vec = ((ldc | slab) & 3) == 0 && ((((uintptr_t)C0) | ((uintptr_t)C1)) & 15) == 0;
+  float bb[4], sa[4], sb[4], sh[4], bmean[4], balpha[4], bbeta[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    bb[u] = (bias && n + u < g.N) ? bias[n + u] : 0.f;
+    sa[u] = sb[u] = sh[u] = bmean[u] = balpha[u] = bbeta[u] = 0.f;
+    if (bn.mode == 2 && n + u < g.N) {
+      bmean[u] = bn.save[n + u];
+      balpha[u] = bn.save[bn.H + n + u] * bn.gamma[n + u];
+      bbeta[u] = fmaf(-bmean[u], balpha[u], bn.beta[n + u]);
+    }
   }
 #pragma unroll
-  for (int h = 0; h < C::WGM; ++h) {
-    if (wm == h) {
+  for (int h = 0; h < NBANDS; ++h) {
+    if (wm == h / BPW) {
+      const int mi0 = (h % BPW) * (BR / 16);
 #pragma unroll
-      for (int mi = 0; mi < C::FM; ++mi)
+      for (int mi = 0; mi < BR / 16; ++mi)
 #pragma unroll
         for (int ni = 0; ni < C::FN; ++ni)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            img[(mi * 16 + 4 * (lane >> 4) + j) * C::BN + wn * C::WTN + ni * 16 + (lane & 15)] = acc[mi][ni][j];
+            img[(mi * 16 + 4 * (lane >> 4) + j) * pitch + wn * C::WTN + ni * 16 + (lane & 15)] = acc[mi0 + mi][ni][j];
     }
     __syncthreads();
-    if (h == 0) shift = img[my_cc] + my_b;  // the tile's first row (always < M)
-    for (int i = threadIdx.x; i < C::WTM * C::BN; i += C::NT) {
-      const int r = i / C::BN;
-      const int m = tl.m0 + h * C::WTM + r, n = my_n;
-      if (m < g.M && n < g.N) {
-        const float v = img[i] + my_b;
-        if (m < msplit) Cz[(int64_t)m * ldc + n] = v;
-        else C1[(int64_t)(m - msplit) * ldc + n] = v;
-        if (bn.mode == 1) {
-          const float dv = v - shift;
-          sa += dv;
-          sb = fmaf(dv, dv, sb);
-        } else if (bn.mode == 2) {
-          const float y = bn.Y[(int64_t)m * bn.ldy + n];
-          const float d = fmaf(y, balpha, bbeta) > 0.f ? v : 0.f;
-          sa += d;
-          sb = fmaf(y - bmean, d, sb);
+    if (bn.trans) {
+      const int q = threadIdx.x & 15;
+      const int m = tl.m0 + h * BR + 4 * q;
+      for (int c = threadIdx.x >> 4; c < C::BN; c += C::NT / 16) {
+        const int nn = tl.n0 + c;
+        if (nn >= g.N || m >= g.M) continue;
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = img[(4 * q + u) * pitch + c];
+        float* dst = C0 + (int64_t)nn * ldc + m;
+        if (vec && m + 3 < g.M) {
+          *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (m + u < g.M) dst[u] = v[u];
+        }
+      }
+      __syncthreads();
+      continue;
+    }
+    if (h == 0 && bn.mode == 1) {  // shift = the tile's first row (always < M)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sh[u] = img[cq + u] + bb[u];
+    }
+    for (int r = rq; r < BR; r += RPI) {
+      const int m = tl.m0 + h * BR + r;
+      if (m >= g.M) break;
+      const float4 w = *(const float4*)(img + r * pitch + cq);
+      const float v[4] = {w.x + bb[0], w.y + bb[1], w.z + bb[2], w.w + bb[3]};
+      float* dst = (m < msplit ? Cz + (int64_t)m * ldc : C1 + (int64_t)(m - msplit) * ldc) + n;
+      if (vec && n + 3 < g.N) {
+        *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (n + u < g.N) dst[u] = v[u];
+      }
+      if (bn.mode == 1) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float dv = v[u] - sh[u];
+          sa[u] += dv;
+          sb[u] = fmaf(dv, dv, sb[u]);
+        }
+      } else if (bn.mode == 2) {
+        const float4 y4 = *(const float4*)(bn.Y + (int64_t)m * bn.ldy + n);
+        const float y[4] = {y4.x, y4.y, y4.z, y4.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float d = fmaf(y[u], balpha[u], bbeta[u]) > 0.f ? v[u] : 0.f;
+          sa[u] += d;
+          sb[u] = fmaf(y[u] - bmean[u], d, sb[u]);
         }
       }
     }
     __syncthreads();
   }
-  if (bn.mode) {
-    float2* red = (float2*)smem;
-    red[threadIdx.x] = make_float2(sa, sb);
+  if (bn.mode) {  // (bn mode: N % 4 == 0, one K pass, 128-row tiles -- checked on the host)
+    float4* red = (float4*)smem;
+    red[2 * threadIdx.x] = make_float4(sa[0], sa[1], sa[2], sa[3]);
+    red[2 * threadIdx.x + 1] = make_float4(sb[0], sb[1], sb[2], sb[3]);
     __syncthreads();
-    if (threadIdx.x < C::BN && my_n < g.N) {
-      float a = 0.f, b = 0.f;
+    if (threadIdx.x < TPR && n < g.N) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), q = a;
 #pragma unroll
-      for (int k = 0; k < C::NT / C::BN; ++k) {
-        a += red[threadIdx.x + k * C::BN].x;
-        b += red[threadIdx.x + k * C::BN].y;
+      for (int k = 0; k < RPI; ++k) {
+        const float4 x = red[2 * (threadIdx.x + k * TPR)], y = red[2 * (threadIdx.x + k * TPR) + 1];
+        a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+        q.x += y.x; q.y += y.y; q.z += y.z; q.w += y.w;
       }
-      float2 o = make_float2(a, b);
-      if (bn.mode == 1) {
-        const float nr = (float)min(C::BM, g.M - tl.m0);
-        const float dm = a / nr;
-        o = make_float2(shift + dm, fmaxf(fmaf(-a, dm, b), 0.f));
+      const float av[4] = {a.x, a.y, a.z, a.w}, qv[4] = {q.x, q.y, q.z, q.w};
+      float2* o = bn.part + (int64_t)(tl.m0 / C::BM) * bn.ldp + n;
+      const float nr = (float)min(C::BM, g.M - tl.m0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (bn.mode == 1) {
+          const float dm = av[u] / nr;
+          o[u] = make_float2(sh[u] + dm, fmaxf(fmaf(-av[u], dm, qv[u]), 0.f));
+        } else {
+          o[u] = make_float2(av[u], qv[u]);
+        }
       }
-      bn.part[(int64_t)(tl.m0 / C::BM) * bn.ldp + my_n] = o;
     }
   }
+#ifdef GM2_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  GM2_STAMP(3);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -943,7 +1038,7 @@ static void ensure_lds_attr(const void* fn, int bytes) {
 
 template <class C, typename T, bool AK, bool BK, bool PP>
 static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
-                           const float* bias, const BnEpi& bn, hipStream_t s) {
+                           const float* bias, const StoreEpi& bn, hipStream_t s) {
   ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP>, C::LDS);
   hipLaunchKernelGGL((k_gemm_store<C, T, AK, BK, PP>), dim3(tiles), dim3(C::NT), C::LDS, s, a, C0, C1 ? C1 : C0,
                      C1 ? msplit : (1 << 30), ldc, slab, bias, bn);
@@ -951,7 +1046,7 @@ static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1
 
 template <class C, typename T, bool AK, bool BK>
 static void store_launch(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
-                         const float* bias, const BnEpi& bn, hipStream_t s) {
+                         const float* bias, const StoreEpi& bn, hipStream_t s) {
   if constexpr (std::is_same_v<C, Big> && sizeof(T) == 2) {
     if (pp_enabled()) return store_launch_k<C, T, AK, BK, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
   }
@@ -960,7 +1055,7 @@ static void store_launch(const GemmArgs<T>& a, int tiles, float* C0, float* C1, 
 
 template <class C, typename T>
 static int store_impl(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
-                      const float* bias, const BnEpi& bn, hipStream_t s) {
+                      const float* bias, const StoreEpi& bn, hipStream_t s) {
   GemmArgs<T> a = g;
   const int kt = E<T>::KT;
   const int nkt = g.K / kt;
@@ -981,13 +1076,28 @@ template <typename T>
 int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
                       const float* bias, hipStream_t s) {
   if (splits < 0) splits = plan_gemm(g).splits;
-  const BnEpi none{};
+  const StoreEpi none{};
   if (use_big(g)) {
     check_gemm(g, 256);
     return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
   }
   check_gemm(g, 128);
-  return store_impl<Small, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
+  return store_impl<SmallDeep, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
+}
+
+template <typename T>
+bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s) {
+  if (plan_gemm(g).splits != 1) return false;
+  StoreEpi ep;
+  ep.trans = 1;
+  if (use_big(g)) {
+    check_gemm(g, 256);
+    store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
+  } else {
+    check_gemm(g, 128);
+    store_impl<SmallDeep, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
+  }
+  return true;
 }
 
 // BatchNorm statistics in the store epilogue (GM2_OPT_BN_EPILOGUE, default on): taken when the
@@ -1000,13 +1110,13 @@ void set_bn_epilogue(int on) { bn_epi_flag().store(on ? 1 : 0, std::memory_order
 int get_bn_epilogue() { return bn_epi_flag().load(std::memory_order_relaxed); }
 
 template <typename T>
-bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const BnEpi& bn, hipStream_t s) {
+bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const StoreEpi& bn, hipStream_t s) {
   static_assert(Small::BM == kBnRowChunk, "statistics chunk = row tile");
   if (!bn_epi_flag().load(std::memory_order_relaxed)) return false;
   const GemmPlan p = plan_gemm(g);
-  if (p.tile != 128 || p.splits != 1) return false;
+  if (p.tile != 128 || p.splits != 1 || (bn.mode && (g.N % 4 || bn.ldy % 4))) return false;
   check_gemm(g, 128);
-  store_impl<Small, T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s);
+  store_impl<SmallDeep, T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s);
   return true;
 }
 
@@ -1098,7 +1208,8 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
 }
 
 #define GM2_INST(T)                                                                                              \
-  template bool launch_gemm_bn<T>(const GemmArgs<T>&, float*, int64_t, const float*, const BnEpi&, hipStream_t);   \
+  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t);                        \
+  template bool launch_gemm_bn<T>(const GemmArgs<T>&, float*, int64_t, const float*, const StoreEpi&, hipStream_t);   \
   template int launch_gemm_store<T>(const GemmArgs<T>&, int, float*, float*, int, int64_t, int64_t, const float*, \
                                     hipStream_t);                                                                \
   template int gemm_recon_grid_blocks<T>(const GemmArgs<T>&);                                                   \

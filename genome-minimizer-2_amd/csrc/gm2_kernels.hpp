@@ -77,8 +77,9 @@ struct TimedLaunch {  // records an event pair around a launch when its class is
 };
 
 // ---- gemm.hip ----
-// BatchNorm statistics computed in a GEMM store epilogue (see k_gemm_store)
-struct BnEpi {
+// Options of the fp32 store epilogue (k_gemm_store): BatchNorm statistics of the stored tile, or
+// a transposed store
+struct StoreEpi {
   int mode = 0;             // 0 off; 1 forward (chunk mean, M2) of C; 2 backward (sum do, sum (y-mean) do)
   float2* part = nullptr;   // [row tile][ldp]
   int64_t ldp = 0;
@@ -88,11 +89,15 @@ struct BnEpi {
   const float* gamma = nullptr;
   const float* beta = nullptr;
   int H = 0;
+  int trans = 0;  // store C^T: C0[n * ldc + m] (no bias, no statistics, one K pass)
 };
 // GEMM + BatchNorm statistics of its output in one launch when the plan allows (one K pass of
 // 128-row tiles); returns false (nothing launched) otherwise
 template <typename T>
-bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const BnEpi& bn, hipStream_t s);
+bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const StoreEpi& bn, hipStream_t s);
+// C^T = (P . Q^T)^T into C [N][ldc] in one launch when the plan is one K pass; false otherwise
+template <typename T>
+bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s);
 void set_bn_epilogue(int on);
 int get_bn_epilogue();
 // splits < 0: use plan_gemm's split-K factor. Returns the number of slabs written.
@@ -145,16 +150,18 @@ void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, 
 void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
                            const float* gamma, const float* beta, int B, int H, float* part, float* dsum,
                            hipStream_t s);
-// BatchNorm v2 (finalize once per column, vectorised elementwise passes)
-void launch_bn_fwd_finalize(const float* part, int B, int H, int train, const float* gamma, const float* beta,
-                            float* rmean, float* rvar, float* save, float* coef, hipStream_t s);
+// dst[c][r] = src[r][c] for an R x Cn block (multiples of 64)
 template <typename T>
-void launch_bn_fwd_apply2(const float* Y, int64_t ld, const float* coef, int B, int Bp, int H, T* A, hipStream_t s);
-void launch_bn_bwd_finalize(const float* part, int B, int H, int train, const float* save, const float* gamma,
-                            const float* beta, float* dgamma, float* dbeta, float* cf, hipStream_t s);
+void launch_transpose(const T* src, int64_t lds_, int R, int Cn, T* dst, int64_t ldd, hipStream_t s);
+// BatchNorm finalize (chunk merge per column) + elementwise apply in one launch per layer
 template <typename T>
-void launch_bn_bwd_apply2(const float* da, const float* Y, int64_t ld, const float* cf, int B, int Bp, int H, T* dY,
-                          float* colpart, hipStream_t s);
+void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
+                         const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,
+                         hipStream_t s);
+template <typename T>
+void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const float* part, int B, int Bp, int H,
+                         int train, const float* save, const float* gamma, const float* beta, float* dgamma,
+                         float* dbeta, T* dY, float* colpart, hipStream_t s);
 // reparameterization + KL (model.py:100-104, loss_components.py:77)
 template <typename T>
 void launch_reparam(const float* slabs, int S, int64_t slab, int L, const float* bmu, const float* blv,

@@ -14,37 +14,42 @@ constexpr double kBnMomentum = 0.1;   // nn.BatchNorm1d default momentum
 
 // ---------------------------------------------------------------------------------------------
 // gather: X[r][c] = data[rows[r]][c] (u8 0/1 -> T) and the row-major target bits of the loss
-// epilogue (bit c%32 of word c/32 of row r). Tile 64 rows x 128 columns, 256 threads: each
-// thread loads 16 bytes of one row (4 rows per pass), expands them to 16 T, and ballots its row's
-// bytes into bits: the 8 lanes of a row hold 128 columns, one ballot per byte index gives bit i of
-// every 16-column chunk of 8 rows, re-assembled per lane into its 16-bit slice of the row's words.
+// epilogue (bit c%32 of word c/32 of row r). A wave streams one strain row at a time, 16 bytes per
+// lane = 1 KiB of contiguous columns per load instruction (2 KiB / 4 KiB per store), four rows
+// per wave in flight; a block = 4 waves x 4 rows x 1024 columns. Each lane's 16 columns give a
+// 16-bit piece of one target word, the even lane of each pair writes the word.
 // ---------------------------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data, int64_t ld_data,
-                                              const int32_t* __restrict__ rows, int B, int G, T* __restrict__ X,
-                                              int64_t ldx, uint32_t* __restrict__ xbits, int64_t ldxb) {
-  const int c0 = blockIdx.x * 128, r0 = blockIdx.y * 64;
-  const int t = threadIdx.x;
-  const int ch = t & 7;  // 16-column chunk
-#pragma unroll 2
-  for (int pass = 0; pass < 2; ++pass) {
-    const int rl = pass * 32 + (t >> 3);
-    const int r = r0 + rl;
-    uint4 v = make_uint4(0, 0, 0, 0);
+                                              const int32_t* __restrict__ rows, int B, int G, int Gp,
+                                              T* __restrict__ X, int64_t ldx, uint32_t* __restrict__ xbits,
+                                              int64_t ldxb) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = blockIdx.x * 1024 + lane * 16;
+  const int rbase = blockIdx.y * 16 + wid * 4;
+  if (c >= Gp) return;  // Gp % 128 == 0: whole 16-column chunks
+  uint4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = rbase + k;
+    v[k] = make_uint4(0, 0, 0, 0);
     if (r < B) {
       const int64_t src = rows ? (int64_t)rows[r] : (int64_t)r;
-      v = *(const uint4*)(data + src * ld_data + c0 + ch * 16);
+      v[k] = *(const uint4*)(data + src * ld_data + c);
     }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = rbase + k;
     uint8_t b[16];
-    *(uint4*)b = v;
+    *(uint4*)b = v[k];
     uint32_t bits = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      if (c0 + ch * 16 + i >= G) b[i] = 0;
+      if (c + i >= G) b[i] = 0;
       bits |= (b[i] ? 1u : 0u) << i;
     }
-    // 16 elements -> 2 (bf16) or 4 (fp32) 16-byte stores
-    T* dst = X + (int64_t)r * ldx + c0 + ch * 16;
+    T* dst = X + (int64_t)r * ldx + c;
     if constexpr (sizeof(T) == 2) {
       uint32_t w[8];
 #pragma unroll
@@ -57,56 +62,82 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data
         *(float4*)(dst + 4 * i) = make_float4((float)b[4 * i], (float)b[4 * i + 1], (float)b[4 * i + 2], (float)b[4 * i + 3]);
     }
     if (xbits) {
-      // lanes ch = 0..7 of this row hold 16-bit pieces of the row's four 32-bit words; even
-      // lanes combine with their odd neighbour and write one word each
-      const uint32_t hi = __shfl_down(bits, 1, 8);
-      if ((ch & 1) == 0) xbits[(int64_t)r * ldxb + (c0 >> 5) + (ch >> 1)] = bits | (hi << 16);
+      const uint32_t hi = __shfl_down(bits, 1, 64);
+      if ((lane & 1) == 0) xbits[(int64_t)r * ldxb + (c >> 5)] = bits | (hi << 16);
     }
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// BN forward partial statistics. Block: 64 columns x 128 rows (4 row groups x 32 rows).
+// BN forward partial statistics of Y = sum of S split-K slabs + bias (the GEMMs whose plan is not
+// one 128-row-tile pass; the others take them in their epilogue). Block: 64 columns x one 128-row
+// chunk; thread = 4 columns (float4) x 8 rows (16 row groups), all 8 rows' loads of a slab in
+// flight together; two-pass (mean, M2) per chunk.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+
 __global__ __launch_bounds__(256) void k_bn_fwd_partial(const float* __restrict__ slabs, int S, int64_t slab,
                                                       int64_t ld, const float* __restrict__ bias, int B, int H,
                                                       float* __restrict__ Y, float2* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rg = threadIdx.x >> 6;
+  __shared__ float4 red[16][16];
+  const int cg = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int col = blockIdx.x * 64 + cg * 4;
   const int r0 = blockIdx.y * kBnRowChunk;
   const int nrows = min(kBnRowChunk, B - r0);
-  const float b = bias ? bias[col] : 0.f;
-  float v[32];
-  float sum = 0.f;
+  const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 b = bias ? *(const float4*)(bias + col) : zero;
+  float4 v[8];
 #pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const int rl = rg + 4 * i;
-    float y = 0.f;
-    if (rl < nrows) {
-      const int64_t o = (int64_t)(r0 + rl) * ld + col;
-      y = slabs[o];
-      for (int s = 1; s < S; ++s) y += slabs[(int64_t)s * slab + o];
-      y += b;
-      Y[o] = y;
-      sum += y;
+  for (int i = 0; i < 8; ++i) {
+    const int rl = rg + 16 * i;
+    v[i] = rl < nrows ? *(const float4*)(slabs + (int64_t)(r0 + rl) * ld + col) : zero;
+  }
+  for (int sl = 1; sl < S; ++sl) {
+    float4 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int rl = rg + 16 * i;
+      w[i] = rl < nrows ? *(const float4*)(slabs + (int64_t)sl * slab + (int64_t)(r0 + rl) * ld + col) : zero;
     }
-    v[i] = y;
-  }
-  red[rg][threadIdx.x & 63] = sum;
-  __syncthreads();
-  const int c = threadIdx.x & 63;
-  const float mean = (red[0][c] + red[1][c] + red[2][c] + red[3][c]) / (float)nrows;
-  __syncthreads();
-  float m2 = 0.f;
 #pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const int rl = rg + 4 * i;
-    if (rl < nrows) { const float d = v[i] - mean; m2 += d * d; }
+    for (int i = 0; i < 8; ++i) v[i] = f4add(v[i], w[i]);
   }
-  red[rg][c] = m2;
+  float4 sum = zero;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int rl = rg + 16 * i;
+    if (rl < nrows) {
+      v[i] = f4add(v[i], b);
+      *(float4*)(Y + (int64_t)(r0 + rl) * ld + col) = v[i];
+      sum = f4add(sum, v[i]);
+    }
+  }
+  red[rg][cg] = sum;
   __syncthreads();
-  if (rg == 0) part[(int64_t)blockIdx.y * H + col] = make_float2(mean, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+  float4 tot = zero;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) tot = f4add(tot, red[k][cg]);
+  const float inv = 1.f / (float)nrows;
+  const float4 mean = make_float4(tot.x * inv, tot.y * inv, tot.z * inv, tot.w * inv);
+  __syncthreads();
+  float4 m2 = zero;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (rg + 16 * i < nrows) {
+      const float dx = v[i].x - mean.x, dy = v[i].y - mean.y, dz = v[i].z - mean.z, dw = v[i].w - mean.w;
+      m2 = make_float4(fmaf(dx, dx, m2.x), fmaf(dy, dy, m2.y), fmaf(dz, dz, m2.z), fmaf(dw, dw, m2.w));
+    }
+  }
+  red[rg][cg] = m2;
+  __syncthreads();
+  if (rg == 0) {
+    float4 q = zero;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) q = f4add(q, red[k][cg]);
+    float4* o = (float4*)(part + (int64_t)blockIdx.y * H + col);
+    o[0] = make_float4(mean.x, q.x, mean.y, q.y);
+    o[1] = make_float4(mean.z, q.z, mean.w, q.w);
+  }
 }
 
 // Chan's parallel merge of per-chunk (mean, M2) -> batch mean and biased variance, in two passes
@@ -133,39 +164,72 @@ __device__ inline void bn_merge(const float2* __restrict__ part, int B, int H, i
 }
 
 // ---------------------------------------------------------------------------------------------
-// BN backward partials: do = dA * [y*alpha+beta' > 0]; sums of do and (y-mean)*do per chunk
+// BN backward partials: do = dA * [y*alpha+beta' > 0] with dA = sum of S slabs (written to dsum when
+// S > 1); sums of do and (y-mean)*do per 128-row chunk. Same block shape as k_bn_fwd_partial.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict__ dslabs, int S, int64_t slab,
                                                       const float* __restrict__ Y, int64_t ld,
                                                       const float* __restrict__ save, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, int B, int H,
                                                       float2* __restrict__ part, float* __restrict__ dsum) {
-  __shared__ float red[2][4][64];
-  const int c = threadIdx.x & 63;
-  const int col = blockIdx.x * 64 + c;
-  const int rg = threadIdx.x >> 6;
+  __shared__ float4 red[2][16][16];
+  const int cg = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int col = blockIdx.x * 64 + cg * 4;
   const int r0 = blockIdx.y * kBnRowChunk;
   const int nrows = min(kBnRowChunk, B - r0);
-  const float mean = save[col], invstd = save[H + col];
-  const float alpha = invstd * gamma[col];
-  const float bprime = fmaf(-mean, alpha, beta[col]);
-  float s1 = 0.f, s2 = 0.f;
-  for (int rl = rg; rl < nrows; rl += 4) {
+  const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 mean = *(const float4*)(save + col), invstd = *(const float4*)(save + H + col);
+  const float4 gm = *(const float4*)(gamma + col), bt = *(const float4*)(beta + col);
+  const float4 al = make_float4(invstd.x * gm.x, invstd.y * gm.y, invstd.z * gm.z, invstd.w * gm.w);
+  const float4 bp = make_float4(fmaf(-mean.x, al.x, bt.x), fmaf(-mean.y, al.y, bt.y), fmaf(-mean.z, al.z, bt.z),
+                                fmaf(-mean.w, al.w, bt.w));
+  float4 da[8], y[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int rl = rg + 16 * i;
     const int64_t o = (int64_t)(r0 + rl) * ld + col;
-    float da = dslabs[o];
-    for (int s = 1; s < S; ++s) da += dslabs[(int64_t)s * slab + o];
-    if (dsum) dsum[o] = da;
-    const float y = Y[o];
-    const float d = fmaf(y, alpha, bprime) > 0.f ? da : 0.f;
-    s1 += d;
-    s2 += (y - mean) * d;
+    da[i] = rl < nrows ? *(const float4*)(dslabs + o) : zero;
+    y[i] = rl < nrows ? *(const float4*)(Y + o) : zero;
   }
-  red[0][rg][c] = s1;
-  red[1][rg][c] = s2;
+  for (int sl = 1; sl < S; ++sl) {
+    float4 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int rl = rg + 16 * i;
+      w[i] = rl < nrows ? *(const float4*)(dslabs + (int64_t)sl * slab + (int64_t)(r0 + rl) * ld + col) : zero;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) da[i] = f4add(da[i], w[i]);
+  }
+  float4 s1 = zero, s2 = zero;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int rl = rg + 16 * i;
+    if (rl < nrows) {
+      if (dsum) *(float4*)(dsum + (int64_t)(r0 + rl) * ld + col) = da[i];
+      const float d0 = fmaf(y[i].x, al.x, bp.x) > 0.f ? da[i].x : 0.f;
+      const float d1 = fmaf(y[i].y, al.y, bp.y) > 0.f ? da[i].y : 0.f;
+      const float d2 = fmaf(y[i].z, al.z, bp.z) > 0.f ? da[i].z : 0.f;
+      const float d3 = fmaf(y[i].w, al.w, bp.w) > 0.f ? da[i].w : 0.f;
+      s1 = f4add(s1, make_float4(d0, d1, d2, d3));
+      s2 = make_float4(fmaf(y[i].x - mean.x, d0, s2.x), fmaf(y[i].y - mean.y, d1, s2.y),
+                       fmaf(y[i].z - mean.z, d2, s2.z), fmaf(y[i].w - mean.w, d3, s2.w));
+    }
+  }
+  red[0][rg][cg] = s1;
+  red[1][rg][cg] = s2;
   __syncthreads();
-  if (rg == 0)
-    part[(int64_t)blockIdx.y * H + col] = make_float2(red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c],
-                                                      red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
+  if (rg == 0) {
+    float4 a = zero, q = zero;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      a = f4add(a, red[0][k][cg]);
+      q = f4add(q, red[1][k][cg]);
+    }
+    float4* o = (float4*)(part + (int64_t)blockIdx.y * H + col);
+    o[0] = make_float4(a.x, q.x, a.y, q.y);
+    o[1] = make_float4(a.z, q.z, a.w, q.w);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -439,6 +503,50 @@ __global__ __launch_bounds__(256) void k_adam_fused(TensorTable tt, const float*
   const float aeps = scal[kScalAdamEps];
   const float cc = clip[0];
   T* sh = (T*)d.shadow;
+  if (e0 + 4096 <= numel) {
+    // whole block: all 16 loads of the thread in flight before the first update
+    float4 pv[4], gv[4], mv[4], vv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t gi = d.off + e0 + (int64_t)(k * 256 + threadIdx.x) * 4;
+      pv[k] = *(const float4*)(p + gi);
+      gv[k] = *(const float4*)(g + gi);
+      mv[k] = *(const float4*)(m + gi);
+      vv[k] = *(const float4*)(v + gi);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t e = e0 + (int64_t)(k * 256 + threadIdx.x) * 4;
+      const int64_t gi = d.off + e;
+      float pe[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w}, ge[4] = {gv[k].x, gv[k].y, gv[k].z, gv[k].w};
+      float me[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w}, ve[4] = {vv[k].x, vv[k].y, vv[k].z, vv[k].w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float gg = (ge[u] + lam * sgnf(pe[u])) * cc;
+        me[u] = me[u] + w1 * (gg - me[u]);
+        ve[u] = ve[u] * b2;
+        ve[u] = ve[u] + w2 * gg * gg;
+        const float denom = sqrtf(ve[u]) / bc2s + aeps;
+        pe[u] = pe[u] + negstep * (me[u] / denom);
+      }
+      *(float4*)(p + gi) = make_float4(pe[0], pe[1], pe[2], pe[3]);
+      *(float4*)(m + gi) = make_float4(me[0], me[1], me[2], me[3]);
+      *(float4*)(v + gi) = make_float4(ve[0], ve[1], ve[2], ve[3]);
+      if (sh) {
+        int64_t r = e / d.cols, c = e - r * d.cols;
+        if ((d.cols & 3) == 0 && (d.sld & 3) == 0) {
+          store4<T>(sh + (d.srow0 + r) * d.sld + c, pe[0], pe[1], pe[2], pe[3]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            sh[(d.srow0 + r) * d.sld + c] = E<T>::cvt(pe[u]);
+            if (++c == d.cols) { c = 0; ++r; }
+          }
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int64_t e = e0 + (int64_t)(k * 256 + threadIdx.x) * 4;  // 4 consecutive elements
@@ -522,106 +630,124 @@ __global__ __launch_bounds__(256) void k_slab_sum(const float* __restrict__ slab
 }
 
 // ---------------------------------------------------------------------------------------------
-// BatchNorm v2: per-column finalize kernels (the fp64 chunk merge runs once per column) and
-// vectorised elementwise apply passes (4 columns per thread).
-// coef layout: [0][H] alpha = invstd*gamma, [1][H] beta' = fma(-mean, alpha, beta)
-// bwd cf layout: [0] mean, [1] alpha, [2] beta', [3] sum(do)/B, [4] sum((y-mean)do)*invstd^2/B
+// BatchNorm finalize + apply in one launch per layer and direction. Every block first turns the
+// chunk partials of its 256 columns into the layer's coefficients (the fp64 chunk merge, ~32
+// L2-resident float2 per column, recomputed identically by each row block) and keeps them in LDS;
+// row block 0 owns the per-column side outputs (save, running statistics, dgamma / dbeta).
+// Then a vectorised elementwise pass over 64 rows x 256 columns (4 columns per thread).
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_bn_fwd_finalize(const float2* __restrict__ part, int B, int H, int train,
-                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                       float* __restrict__ rmean, float* __restrict__ rvar,
-                                                       float* __restrict__ save, float* __restrict__ coef) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= H) return;
+// forward coefficients (alpha = invstd*gamma, beta' = fma(-mean, alpha, beta)) of column `col`
+__device__ inline float2 bn_fwd_coef(const float2* __restrict__ part, int B, int H, int train,
+                                     const float* __restrict__ gamma, const float* __restrict__ beta, float* rmean,
+                                     float* rvar, float* save, int col, bool own) {
   float invstd, meanf;
   if (train) {
     double mean, var;
     bn_merge(part, B, H, col, mean, var);
     invstd = (float)(1.0 / sqrt(var + kBnEps));
     meanf = (float)mean;
-    save[col] = meanf;
-    save[H + col] = invstd;
-    const double unb = B > 1 ? var * (double)B / (double)(B - 1) : var;
-    rmean[col] = (float)(kBnMomentum * mean + (1.0 - kBnMomentum) * (double)rmean[col]);
-    rvar[col] = (float)(kBnMomentum * unb + (1.0 - kBnMomentum) * (double)rvar[col]);
+    if (own) {
+      save[col] = meanf;
+      save[H + col] = invstd;
+      const double unb = B > 1 ? var * (double)B / (double)(B - 1) : var;
+      rmean[col] = (float)(kBnMomentum * mean + (1.0 - kBnMomentum) * (double)rmean[col]);
+      rvar[col] = (float)(kBnMomentum * unb + (1.0 - kBnMomentum) * (double)rvar[col]);
+    }
   } else {
     // eval transform bit-identical to the reference CPU path (pinned in tests): float
     // invstd = 1/sqrt(rv + eps), alpha = gamma*invstd, beta' = fma(-mean, alpha, beta)
     meanf = rmean[col];
     invstd = 1.0f / sqrtf(rvar[col] + (float)kBnEps);
-    if (save) { save[col] = meanf; save[H + col] = invstd; }
+    if (own && save) {
+      save[col] = meanf;
+      save[H + col] = invstd;
+    }
   }
   const float alpha = invstd * gamma[col];
-  coef[col] = alpha;
-  coef[H + col] = fmaf(-meanf, alpha, beta[col]);
+  return make_float2(alpha, fmaf(-meanf, alpha, beta[col]));
 }
 
-// A = relu(y*alpha + beta') for rows < B, 0 for rows in [B, Bp)
+// A = relu(y*alpha + beta') for rows < B, 0 for rows in [B, Bp). Grid: (ceil(H/256), Bp/64).
 template <typename T>
-__global__ __launch_bounds__(256) void k_bn_fwd_apply2(const float* __restrict__ Y, int64_t ld,
-                                                     const float* __restrict__ coef, int B, int Bp, int H,
-                                                     T* __restrict__ A) {
-  const int q4 = H / 4;
-  const int64_t total = (int64_t)Bp * q4;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int r = (int)(i / q4), c = (int)(i % q4) * 4;
+__global__ __launch_bounds__(256) void k_bn_fwd_apply(const float* __restrict__ Y, int64_t ld,
+                                                    const float2* __restrict__ part, int B, int H, int train,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    float* rmean, float* rvar, float* save, T* __restrict__ A) {
+  __shared__ float2 cf[256];
+  const int c0 = blockIdx.x * 256;
+  if (c0 + (int)threadIdx.x < H)
+    cf[threadIdx.x] = bn_fwd_coef(part, B, H, train, gamma, beta, rmean, rvar, save, c0 + threadIdx.x,
+                                  blockIdx.y == 0);
+  __syncthreads();
+  const int cl = (threadIdx.x & 63) * 4, rg = threadIdx.x >> 6;
+  const int c = c0 + cl;
+  if (c >= H) return;  // H % 128 == 0: the last block may cover only 128 of its 256 columns
+  const float2 k0 = cf[cl], k1 = cf[cl + 1], k2 = cf[cl + 2], k3 = cf[cl + 3];
+  const int r0 = blockIdx.y * 64;
+#pragma unroll 4
+  for (int rl = rg; rl < 64; rl += 4) {
+    const int r = r0 + rl;
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
     if (r < B) {
       const float4 y = *(const float4*)(Y + (int64_t)r * ld + c);
-      const float4 al = *(const float4*)(coef + c);
-      const float4 be = *(const float4*)(coef + H + c);
-      o.x = fmaxf(fmaf(y.x, al.x, be.x), 0.f);
-      o.y = fmaxf(fmaf(y.y, al.y, be.y), 0.f);
-      o.z = fmaxf(fmaf(y.z, al.z, be.z), 0.f);
-      o.w = fmaxf(fmaf(y.w, al.w, be.w), 0.f);
+      o.x = fmaxf(fmaf(y.x, k0.x, k0.y), 0.f);
+      o.y = fmaxf(fmaf(y.y, k1.x, k1.y), 0.f);
+      o.z = fmaxf(fmaf(y.z, k2.x, k2.y), 0.f);
+      o.w = fmaxf(fmaf(y.w, k3.x, k3.y), 0.f);
     }
     store4<T>(A + (int64_t)r * ld + c, o.x, o.y, o.z, o.w);
   }
 }
 
-// train = 0: eval-mode BatchNorm is the affine map y -> (y - rm)*invstd*gamma + beta, whose backward
-// has no batch-coupling terms (grad_mean = proj_scale = 0)
-__global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float2* __restrict__ part, int B, int H, int train,
-                                                       const float* __restrict__ save, const float* __restrict__ gamma,
-                                                       const float* __restrict__ beta, float* __restrict__ dgamma,
-                                                       float* __restrict__ dbeta, float* __restrict__ cf) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= H) return;
-  double s1 = 0.0, s2 = 0.0;
-  const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
-#pragma unroll 8
-  for (int ch = 0; ch < nch; ++ch) {
-    const float2 p = part[(int64_t)ch * H + col];
-    s1 += p.x;
-    s2 += p.y;
-  }
-  const float mean = save[col], invstd = save[H + col];
-  const float alpha = invstd * gamma[col];
-  dgamma[col] = (float)(s2 * invstd);
-  dbeta[col] = (float)s1;
-  cf[col] = mean;
-  cf[H + col] = alpha;
-  cf[2 * H + col] = fmaf(-mean, alpha, beta[col]);
-  cf[3 * H + col] = train ? (float)(s1 / B) : 0.f;
-  cf[4 * H + col] = train ? (float)(s2 * (double)invstd * invstd / B) : 0.f;
-}
-
-// dx = (do - grad_mean - (y-mean)*proj_scale) * alpha, do = da*[y*alpha+beta' > 0]; rows >= B -> 0.
-// Block: 256 columns x 64 rows (4 row groups); per-(64-row chunk, column) sums of dx -> colpart.
+// dx = (do - grad_mean - (y-mean)*proj_scale) * alpha, do = da*[y*alpha+beta' > 0]; rows >= B -> 0;
+// grad_mean = sum(do)/B, proj_scale = sum((y-mean)do)*invstd^2/B in train mode; in eval mode
+// BatchNorm is the affine map y -> (y - rm)*invstd*gamma + beta and both are 0 (no batch
+// coupling). dgamma = sum((y-mean)do)*invstd, dbeta = sum(do) from the chunk partials (fp64).
+// Per-(64-row chunk, column) sums of dx -> colpart (the pre-BN Linear bias gradient).
 template <typename T>
-__global__ __launch_bounds__(256) void k_bn_bwd_apply2(const float* __restrict__ da, const float* __restrict__ Y,
-                                                     int64_t ld, const float* __restrict__ cf, int B, int H,
-                                                     T* __restrict__ dY, float* __restrict__ colpart) {
+__global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ da, const float* __restrict__ Y,
+                                                    int64_t ld, const float2* __restrict__ part, int B, int H,
+                                                    int train, const float* __restrict__ save,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                    T* __restrict__ dY, float* __restrict__ colpart) {
+  __shared__ float4 cf4[5][64];  // [mean, alpha, beta', grad_mean, proj_scale][column / 4]
   __shared__ float4 red[4][64];
+  float* cf = (float*)cf4;
+  const int c0 = blockIdx.x * 256;
+  {
+    const int t = threadIdx.x, col = c0 + t;
+    if (col < H) {
+      double s1 = 0.0, s2 = 0.0;
+      const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
+#pragma unroll 8
+      for (int ch = 0; ch < nch; ++ch) {
+        const float2 p = part[(int64_t)ch * H + col];
+        s1 += p.x;
+        s2 += p.y;
+      }
+      const float mean = save[col], invstd = save[H + col];
+      const float alpha = invstd * gamma[col];
+      if (blockIdx.y == 0) {
+        dgamma[col] = (float)(s2 * invstd);
+        dbeta[col] = (float)s1;
+      }
+      cf[t] = mean;
+      cf[256 + t] = alpha;
+      cf[512 + t] = fmaf(-mean, alpha, beta[col]);
+      cf[768 + t] = train ? (float)(s1 / B) : 0.f;
+      cf[1024 + t] = train ? (float)(s2 * (double)invstd * invstd / B) : 0.f;
+    }
+  }
+  __syncthreads();
   const int cg = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 256 + cg * 4;
+  const int c = c0 + cg * 4;
   const int r0 = blockIdx.y * 64;
-  const bool ok = c < H;  // H % 128 == 0: the last block may cover only 128 of its 256 columns
+  const bool ok = c < H;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (ok) {
-    const float4 mean = *(const float4*)(cf + c), al = *(const float4*)(cf + H + c);
-    const float4 be = *(const float4*)(cf + 2 * H + c), gm = *(const float4*)(cf + 3 * H + c);
-    const float4 ps = *(const float4*)(cf + 4 * H + c);
+    const float4 mean = cf4[0][cg], al = cf4[1][cg], be = cf4[2][cg], gm = cf4[3][cg], ps = cf4[4][cg];
+#pragma unroll 4
     for (int rl = rg; rl < 64; rl += 4) {
       const int r = r0 + rl;
       float4 dx = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -648,6 +774,30 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply2(const float* __restrict__
     float4 v = red[0][cg];
     for (int k = 1; k < 4; ++k) { v.x += red[k][cg].x; v.y += red[k][cg].y; v.z += red[k][cg].z; v.w += red[k][cg].w; }
     *(float4*)(colpart + (int64_t)blockIdx.y * H + c) = v;
+  }
+}
+
+// dst[c][r] = src[r][c] over an R x Cn block (both multiples of 64): 64 x 64 tiles through LDS,
+// 16-byte loads and stores (each output row segment = 64 contiguous elements). Used for the small
+// activations whose transposed copy turns a weight-gradient GEMM's MN-major operand K-major.
+template <typename T>
+__global__ __launch_bounds__(256) void k_transpose(const T* __restrict__ src, int64_t lds_, T* __restrict__ dst,
+                                                 int64_t ldd) {
+  constexpr int EPC = 16 / sizeof(T), CPR = 64 / EPC, RPP = 256 / CPR;
+  __shared__ __attribute__((aligned(16))) T tile[64][64 + EPC];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int ch = threadIdx.x % CPR, rr = threadIdx.x / CPR;
+#pragma unroll
+  for (int p = 0; p < 64; p += RPP)
+    *(uint4*)&tile[p + rr][ch * EPC] = *(const uint4*)(src + (r0 + p + rr) * lds_ + c0 + ch * EPC);
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 64; p += RPP) {
+    const int c = p + rr;
+    T v[EPC];
+#pragma unroll
+    for (int j = 0; j < EPC; ++j) v[j] = tile[ch * EPC + j][c];
+    *(uint4*)(dst + (c0 + c) * ldd + r0 + ch * EPC) = *(const uint4*)v;
   }
 }
 
@@ -679,8 +829,8 @@ void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* row
                         int Gp, int Bp, uint32_t* xbits, int64_t ldxb, hipStream_t s) {
   if (Gp % 128 || Bp % 64 || ld_data % 16 || ld_data < Gp || ((uintptr_t)data & 15) || (xbits && ldxb * 32 < Gp))
     throw Gm2Error("gather: bad layout (Gp=%d Bp=%d ld=%lld)", Gp, Bp, (long long)ld_data);
-  hipLaunchKernelGGL(k_gather<T>, dim3(Gp / 128, Bp / 64), dim3(256), 0, s, data, ld_data, rows, B, G, X, ldx, xbits,
-                     ldxb);
+  hipLaunchKernelGGL(k_gather<T>, dim3((Gp + 1023) / 1024, Bp / 16), dim3(256), 0, s, data, ld_data, rows, B, G, Gp, X,
+                     ldx, xbits, ldxb);
   GM2_CHECK_LAUNCH();
 }
 
@@ -696,6 +846,7 @@ void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, 
 void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
                            const float* gamma, const float* beta, int B, int H, float* part, float* dsum,
                            hipStream_t s) {
+  if (H % 64) throw Gm2Error("bn: H %% 64");
   const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
   hipLaunchKernelGGL(k_bn_bwd_partial, dim3(H / 64, nch), dim3(256), 0, s, dslabs, S, slab, Y, ld, save, gamma,
                      beta, B, H, (float2*)part, dsum);
@@ -746,33 +897,30 @@ void launch_colsum(const float* part, int rows, int64_t ld, int64_t n, float* ou
   GM2_CHECK_LAUNCH();
 }
 
-void launch_bn_fwd_finalize(const float* part, int B, int H, int train, const float* gamma, const float* beta,
-                            float* rmean, float* rvar, float* save, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((H + 255) / 256), dim3(256), 0, s, (const float2*)part, B, H, train,
-                     gamma, beta, rmean, rvar, save, coef);
+template <typename T>
+void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
+                         const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,
+                         hipStream_t s) {
+  if (H % 128 || ld % 4 || Bp % 64) throw Gm2Error("bn_fwd_apply: H %% 128, ld %% 4, Bp %% 64");
+  hipLaunchKernelGGL(k_bn_fwd_apply<T>, dim3((H + 255) / 256, Bp / 64), dim3(256), 0, s, Y, ld, (const float2*)part,
+                     B, H, train, gamma, beta, rmean, rvar, save, A);
+  GM2_CHECK_LAUNCH();
+}
+template <typename T>
+void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const float* part, int B, int Bp, int H,
+                         int train, const float* save, const float* gamma, const float* beta, float* dgamma,
+                         float* dbeta, T* dY, float* colpart, hipStream_t s) {
+  if (H % 128 || ld % 4 || Bp % 64) throw Gm2Error("bn_bwd_apply: H %% 128, ld %% 4, Bp %% 64");
+  hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3((H + 255) / 256, Bp / 64), dim3(256), 0, s, da, Y, ld,
+                     (const float2*)part, B, H, train, save, gamma, beta, dgamma, dbeta, dY, colpart);
   GM2_CHECK_LAUNCH();
 }
 
 template <typename T>
-void launch_bn_fwd_apply2(const float* Y, int64_t ld, const float* coef, int B, int Bp, int H, T* A, hipStream_t s) {
-  if (H % 4 || ld % 4) throw Gm2Error("bn_apply: H %% 4");
-  const int64_t nb = std::min<int64_t>(2048, ((int64_t)Bp * H / 4 + 255) / 256);
-  hipLaunchKernelGGL(k_bn_fwd_apply2<T>, dim3((unsigned)nb), dim3(256), 0, s, Y, ld, coef, B, Bp, H, A);
-  GM2_CHECK_LAUNCH();
-}
-
-void launch_bn_bwd_finalize(const float* part, int B, int H, int train, const float* save, const float* gamma,
-                            const float* beta, float* dgamma, float* dbeta, float* cf, hipStream_t s) {
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((H + 255) / 256), dim3(256), 0, s, (const float2*)part, B, H, train, save, gamma,
-                     beta, dgamma, dbeta, cf);
-  GM2_CHECK_LAUNCH();
-}
-
-template <typename T>
-void launch_bn_bwd_apply2(const float* da, const float* Y, int64_t ld, const float* cf, int B, int Bp, int H, T* dY,
-                          float* colpart, hipStream_t s) {
-  if (H % 128) throw Gm2Error("bn_bwd_apply: H %% 128");
-  hipLaunchKernelGGL(k_bn_bwd_apply2<T>, dim3((H + 255) / 256, Bp / 64), dim3(256), 0, s, da, Y, ld, cf, B, H, dY, colpart);
+void launch_transpose(const T* src, int64_t lds_, int R, int Cn, T* dst, int64_t ldd, hipStream_t s) {
+  if (R % 64 || Cn % 64 || (lds_ * sizeof(T)) % 16 || (ldd * sizeof(T)) % 16)
+    throw Gm2Error("transpose: %d x %d block, pitches must be 16-B multiples", R, Cn);
+  hipLaunchKernelGGL(k_transpose<T>, dim3(Cn / 64, R / 64), dim3(256), 0, s, src, lds_, dst, ldd);
   GM2_CHECK_LAUNCH();
 }
 
@@ -835,9 +983,12 @@ void launch_grad_finalize(const double* part, int nblocks, const float* scal, fl
   template void launch_sigmoid_bwd<T>(const float*, const float*, int64_t, int, int, int, int, T*, int64_t,     \
                                       float*, hipStream_t);                                                     \
   template void launch_shadow_sync<T>(const TensorTable&, const float*, hipStream_t);                          \
-  template void launch_bn_fwd_apply2<T>(const float*, int64_t, const float*, int, int, int, T*, hipStream_t);  \
-  template void launch_bn_bwd_apply2<T>(const float*, const float*, int64_t, const float*, int, int, int, T*,    \
-                                        float*, hipStream_t);                                                  \
+  template void launch_bn_fwd_apply<T>(const float*, int64_t, const float*, int, int, int, int, const float*,   \
+                                       const float*, float*, float*, float*, T*, hipStream_t);                   \
+  template void launch_bn_bwd_apply<T>(const float*, const float*, int64_t, const float*, int, int, int, int,    \
+                                       const float*, const float*, const float*, float*, float*, T*, float*,    \
+                                       hipStream_t);                                                            \
+  template void launch_transpose<T>(const T*, int64_t, int, int, T*, int64_t, hipStream_t);                    \
   template void launch_adam_fused<T>(const TensorTable&, const float*, float*, float*, float*, const float*,    \
                                      const float*, hipStream_t);
 GM2_INST(float)

@@ -22,6 +22,7 @@ shapes = [
     ("dA5  dL.W9     ", 1, 0, B, H, G),
     ("dW9  dL^T.A5   ", 0, 0, G, H, B),
     ("dWe0 dY^T.X    ", 0, 0, H, G, B),
+    ("dWe0 dYT.X  nn ", 1, 0, H, G, B),
     ("hid fwd A.W^T  ", 1, 1, B, H, H),
     ("hid dX dY.W    ", 1, 0, B, H, H),
     ("hid dW dY^T.A  ", 0, 0, H, H, B),

@@ -39,26 +39,34 @@ def step(i):
     native.adam_step(ws, model.params, grads, opt.exp_avg, opt.exp_avg_sq, scal[i])
 
 
-opt_name = sys.argv[1] if len(sys.argv) > 1 else "recon_tile"
-vals = [int(v) for v in sys.argv[2:]] or [256, 128]
-key = {"recon_tile": native.OPT_RECON_TILE, "small_split": native.OPT_SMALL_SPLIT, "gemm_pp": native.OPT_GEMM_PP,
-       "bn_epilogue": native.OPT_BN_EPILOGUE}[opt_name]
-res = {}
-for rnd in range(3):
-    for tile in vals:
-        native.set_option(key, tile)
-        for i in range(2):
-            step(i)
-        torch.cuda.synchronize()
-        native.timing_begin(native.KC_RECON_LOSS)
-        t0 = time.perf_counter()
-        for i in range(10):
-            step(i + 2)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / 10
-        ms, n = native.timing_end()
-        res.setdefault(tile, []).append((ms / n, dt * 1e3))
-for tile, v in res.items():
-    k = sorted(x[0] for x in v)[len(v) // 2]
-    st = sorted(x[1] for x in v)[len(v) // 2]
-    print(f"{opt_name} {tile}: recon kernel {k * 1e3:.1f} us ({2 * B * H * G / (k * 1e-3) / 1e12:.0f} TF/s), step {st:.3f} ms")
+KEYS = {"recon_tile": native.OPT_RECON_TILE, "small_split": native.OPT_SMALL_SPLIT, "gemm_pp": native.OPT_GEMM_PP,
+        "bn_epilogue": native.OPT_BN_EPILOGUE}
+
+
+def main():
+    opt_name = sys.argv[1] if len(sys.argv) > 1 else "recon_tile"
+    vals = [int(v) for v in sys.argv[2:]] or [256, 128]
+    key = KEYS[opt_name]
+    res = {}
+    for rnd in range(3):
+        for tile in vals:
+            native.set_option(key, tile)
+            for i in range(2):
+                step(i)
+            torch.cuda.synchronize()
+            native.timing_begin(native.KC_RECON_LOSS)
+            t0 = time.perf_counter()
+            for i in range(10):
+                step(i + 2)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / 10
+            ms, n = native.timing_end()
+            res.setdefault(tile, []).append((ms / n, dt * 1e3))
+    for tile, v in res.items():
+        k = sorted(x[0] for x in v)[len(v) // 2]
+        st = sorted(x[1] for x in v)[len(v) // 2]
+        print(f"{opt_name} {tile}: recon kernel {k * 1e3:.1f} us ({2 * B * H * G / (k * 1e-3) / 1e12:.0f} TF/s), step {st:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
