@@ -1,0 +1,16 @@
+#!/bin/bash
+# full GPU iteration: every -m gpu test, the default bench line (what the driver runs), then a
+# rocprofv3 kernel-trace summary of a short bench. Each step under its own limit; stop at the first
+# crash / timeout.
+cd "$GRAFT_REPO_ROOT" || exit 2
+mkdir -p gpurun_out
+export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
+T=${1:-f}
+timeout -k 10 700 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread -rf > gpurun_out/gpu_tests_$T.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/gpu_tests_$T.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python3 bench.py > gpurun_out/bench_$T.log 2>&1
+rc=$?; echo "bench rc=$rc" >> gpurun_out/bench_$T.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$T -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-f32-line --sample-genomes 262144 > gpurun_out/prof_$T.log 2>&1
+echo "prof rc=$?" >> gpurun_out/prof_$T.log

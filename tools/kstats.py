@@ -9,7 +9,7 @@
     the kernel's algorithmic MFMA count where it is known;
   * HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE passes (FETCH_SIZE x2 on gfx950).
 
-Usage: python3 tools/kstats.py TAG [out.json]   (reads gpurun_out/{prof,pmc_mfma,pmc_fetch,pmc_write}_TAG)
+Usage: python3 tools/kstats.py TAG [out.json|-] [timed steps]   (reads gpurun_out/{prof,pmc_mfma,pmc_fetch,pmc_write}_TAG)
 """
 import collections
 import csv
@@ -57,7 +57,10 @@ def step_breakdown(tag, steps):
 
 
 def mfma(tag):
-    c, names = counters(f"gpurun_out/pmc_mfma_{tag}")
+    try:
+        c, names = counters(f"gpurun_out/pmc_mfma_{tag}")
+    except FileNotFoundError:
+        return {}
     per = collections.defaultdict(list)
     for d, v in c.items():
         if v.get("GRBM_GUI_ACTIVE", 0) <= 0:
@@ -104,4 +107,5 @@ def main(tag, dst=None, steps=6):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 and sys.argv[2] != "-" else None,
+         int(sys.argv[3]) if len(sys.argv) > 3 else 6)
