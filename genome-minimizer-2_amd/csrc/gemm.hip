@@ -68,15 +68,15 @@ struct TileXY {
 };
 
 // XCD-aware, grouped tile order (see header)
-template <class C>
-__device__ __forceinline__ TileXY tile_of(int tm, int tn) {
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
+__device__ __forceinline__ int xcd_wg(int bid, int nwg) {
   const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int ntile = tm * tn;
-  const int split = wg / ntile;
-  const int t = wg - split * ntile;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+__device__ __forceinline__ int xcd_wg() { return xcd_wg(blockIdx.x, gridDim.x); }
+
+// logical tile t (GROUP_M = 8 supergroups, m fastest) -> tile origin
+template <class C>
+__device__ __forceinline__ TileXY tile_at(int t, int tm, int tn, int split) {
   constexpr int GROUP = 8;
   const int per_group = GROUP * tn;
   const int grp = t / per_group;
@@ -86,6 +86,14 @@ __device__ __forceinline__ TileXY tile_of(int tm, int tn) {
   const int pm = first_m + in % gsize;
   const int pn = in / gsize;
   return {pm * C::BM, pn * C::BN, split, pm * tn + pn};
+}
+
+template <class C>
+__device__ __forceinline__ TileXY tile_of(int tm, int tn) {
+  const int wg = xcd_wg();
+  const int ntile = tm * tn;
+  const int split = wg / ntile;
+  return tile_at<C>(wg - split * ntile, tm, tn, split);
 }
 
 // ---- operand staging (HBM -> LDS with global_load_lds_dwordx4; LDS destination lane-linear) ----
@@ -436,9 +444,36 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
                                                     const float* __restrict__ bias, StoreEpi bn) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   GM2_STAMP(0);
-  const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
-  const int kbeg = tl.split * g.k_per_split;
-  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
+  TileXY tl;
+  int kbeg, kend;
+  // Remainder mode (bn.rem > 0, one K pass): the first ntile - rem tiles run whole; each of the
+  // last rem tiles (the ones that would leave most CUs idle in the final round) runs as two
+  // K-halves into bn.rem_slab [rem][2][BM][BN], summed into C by k_rem_sum.
+  bool remtile = false;
+  float* outp = C0;
+  if (bn.rem > 0) {
+    // by dispatch order: blocks [0, full) are the whole tiles (XCD-remapped among themselves), the
+    // last 2*rem blocks the halves, spread over every XCD (a remap over the whole grid would put
+    // the last logical tiles on one XCD)
+    const int full = tm * tn - bn.rem, bid = blockIdx.x;
+    if (bid < full) {
+      tl = tile_at<C>(xcd_wg(bid, full), tm, tn, 0);
+      kbeg = 0;
+      kend = g.K;
+    } else {
+      const int r = bid - full;
+      tl = tile_at<C>(full + (r >> 1), tm, tn, 0);
+      kbeg = (r & 1) * g.k_per_split;
+      kend = min(g.K, kbeg + g.k_per_split);
+      remtile = true;
+      outp = bn.rem_slab + (int64_t)r * C::BM * C::BN;
+    }
+  } else {
+    tl = tile_of<C>(tm, tn);
+    kbeg = tl.split * g.k_per_split;
+    kend = min(g.K, kbeg + g.k_per_split);
+  }
   const int nk = (kend - kbeg) / E<T>::KT;
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP)
@@ -447,7 +482,18 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
     mainloop<C, T, AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
   GM2_STAMP(2);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
-  float* Cz = C0 + (int64_t)tl.split * slab;
+  // output rows: outp + (m - mo) * outld + (n - no) for m < msplit (a remainder tile: its own
+  // dense [BM][BN] slice), C1 + (m - msplit) * ldc otherwise
+  int64_t outld = ldc;
+  int mo = 0, no = 0;
+  if (remtile) {
+    outld = C::BN;
+    mo = tl.m0;
+    no = tl.n0;
+    msplit = 1 << 30;
+  } else {
+    outp = C0 + (int64_t)tl.split * slab;
+  }
   // Stage one 64-row band of the tile at a time through the (now free) staging LDS (row pitch
   // BN + 4 floats: the accumulator writes of lanes 16 apart land 16 banks apart), then store whole
   // rows with 16-byte stores (4 columns per thread; scalar where C's rows are not 16-B aligned or
@@ -462,7 +508,11 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
   static_assert(C::NT % TPR == 0 && BR % RPI == 0 && 2 * C::NT * 16 <= C::LDS, "epilogue shape");
   const int cq = (threadIdx.x % TPR) * 4, rq = threadIdx.x / TPR;
   const int n = tl.n0 + cq;
-  const bool vec = ((ldc | slab) & 3) == 0 && ((((uintptr_t)C0) | ((uintptr_t)C1)) & 15) == 0;
+  const bool vec = remtile || (((ldc | slab) & 3) == 0 && ((((uintptr_t)C0) | ((uintptr_t)C1)) & 15) == 0);
+  // rows that are not 16-B aligned (ldc % 4 != 0, e.g. the [H][G] input-layer gradient at odd G):
+  // each row's chunks shift to its first 16-B boundary, the head elements go scalar
+  const bool shiftvec = !vec && slab == 0 && !bias && bn.mode == 0 && !bn.trans && msplit >= g.M &&
+                        (((uintptr_t)C0) & 3) == 0;
   float bb[4], sa[4], sb[4], sh[4], bmean[4], balpha[4], bbeta[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -487,7 +537,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
             img[(mi * 16 + 4 * (lane >> 4) + j) * pitch + wn * C::WTN + ni * 16 + (lane & 15)] = acc[mi0 + mi][ni][j];
     }
     __syncthreads();
-    if (bn.trans) {
+    if (bn.trans && !remtile) {
       const int q = threadIdx.x & 15;
       const int m = tl.m0 + h * BR + 4 * q;
       for (int c = threadIdx.x >> 4; c < C::BN; c += C::NT / 16) {
@@ -515,9 +565,26 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
     for (int r = rq; r < BR; r += RPI) {
       const int m = tl.m0 + h * BR + r;
       if (m >= g.M) break;
+      if (shiftvec) {
+        float* rowp = outp + (int64_t)m * ldc + tl.n0;
+        const float* src = img + r * pitch;
+        const int a = (int)((4u - (uint32_t)(((uintptr_t)rowp >> 2) & 3u)) & 3u);
+        const int c = a + cq;
+        if (c + 3 < C::BN && tl.n0 + c + 3 < g.N) {
+          *(float4*)(rowp + c) = make_float4(src[c], src[c + 1], src[c + 2], src[c + 3]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (c + u < C::BN && tl.n0 + c + u < g.N) rowp[c + u] = src[c + u];
+        }
+        if (cq == 0)
+          for (int u = 0; u < a; ++u)
+            if (tl.n0 + u < g.N) rowp[u] = src[u];
+        continue;
+      }
       const float4 w = *(const float4*)(img + r * pitch + cq);
       const float v[4] = {w.x + bb[0], w.y + bb[1], w.z + bb[2], w.w + bb[3]};
-      float* dst = (m < msplit ? Cz + (int64_t)m * ldc : C1 + (int64_t)(m - msplit) * ldc) + n;
+      float* dst = m < msplit ? outp + (int64_t)(m - mo) * outld + (n - no) : C1 + (int64_t)(m - msplit) * ldc + n;
       if (vec && n + 3 < g.N) {
         *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
       } else {
@@ -597,21 +664,31 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
 // ---------------------------------------------------------------------------------------------
 // The loss epilogue's element loop. No per-element guards: padded genes (g >= G) have a zero
 // weight row and a zero bias, so their logit is exactly 0 and their BCE / sum(p) contributions are
-// exact constants the kernel subtracts per tile; padded strains are masked by `smask` inside the
-// accumulating FMAs. Padded dL entries are harmless: every consumer multiplies them by
+// exact constants the kernel subtracts per tile; padded strains' sums are dropped per column. Padded dL entries are harmless: every consumer multiplies them by
 // zero-padded operands (W9 shadow rows >= G, A5 rows >= B) or never reads them.
 //
-// FAST (bf16 training) element math, select-free: with ns = (x ? -1 : +1) built from the target
-// bit by integer ops, t = sigmoid(-ns*l) is the BCE argument (p for x = 1, 1-p for x = 0), and
-//   -log t (clamped at 100) ; p - x = ns*(1-t) ; p(1-p) = t(1-t) ; p = [x == 0] - ns*t,
-// so sum(p) = (number of x == 0 targets) + sum(-ns*t). Hardware exp2 / rcp / log2 (~1 ulp), BCE
-// summed in log2 units (scaled by ln 2 once per tile), and (p-x)/max(q,1e-12)*q folded to
-// (p-x)*min(q*1e12, 1): the reference's value up to rounding.
+// FAST (bf16 training) element math, in the reference's own quantities: p = sigmoid(l) as
+// rcp(1 + exp2(-l log2 e)) (hardware ~1 ulp), 1 - p formed in fp32 from p exactly as the reference
+// forms it (so a p that rounds to 1.0 gives the reference's log(0) -> -100 clamp and zero gradient),
+//   BCE = -max(log(x ? p : 1-p), -100)          (log(1-p) for log1p(-p): same value up to rounding)
+//   dl  = (p - x) * min(p(1-p) * 1e12, 1) + w*gamma * p(1-p)
+// which is the reference's ((p-x)/max(p(1-p),1e-12) + w*gamma) * (1-p) * p up to rounding. The
+// selects are bit-field ops on a 0 / -1 mask from the target bit (x ? p : 1-p as |x ? p : p-1|,
+// p - x as x ? p-1 : p), BCE is summed in log2 units and scaled by -ln 2 once per tile, and the
+// bias arrives pre-scaled (nb = -b log2 e). BCE and sum(p) are summed per strain column and masked
+// once per column (padded strains).
 // Exact (fp32 parity) path: the reference's formula order, p computed first.
-template <class C, typename T, bool FAST>
+// (m & a) | (~m & b) as one v_bfi_b32 (the compiler rewrites the C form into compare + select)
+__device__ __forceinline__ float bfi(int m, float a, float b) {
+  float r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+
+template <class C, typename T, bool FAST, bool WG, bool GRAD>
 __device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], const uint32_t* __restrict__ xrow,
                                            int64_t ldxb, const float* bias_s, int N, int n0, int wm, int wn, int q,
-                                           int c, float wgam, bool with_grad, T* img, float& bce, float& psum) {
+                                           int c, float wgam, T* img, float& bce, float& psum) {
   constexpr int PR = C::BM + 8;
   constexpr int XW = C::WTM / 32;  // target words of this wave's gene span per strain row
   static_assert(XW == 4 || XW == 2, "wave gene span");
@@ -622,7 +699,6 @@ __device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], con
   for (int ni = 0; ni < C::FN; ++ni) {
     const int sl = wn * C::WTN + ni * 16 + c;  // strain (tile-local)
     const bool sok = n0 + sl < N;
-    const float sm = sok ? 1.0f : 0.0f;
     uint32_t xw[XW];
     const uint32_t* xp = xrow + (int64_t)(n0 + sl) * ldxb;
     if (sok) {
@@ -637,56 +713,62 @@ __device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], con
 #pragma unroll
       for (int k = 0; k < XW; ++k) xw[k] = 0u;
     }
+    // this lane's genes of word k sit at bits (mi & 1) * 16 + j after the shift by 4q
+#pragma unroll
+    for (int k = 0; k < XW; ++k) xw[k] >>= 4 * q;
     T* irow = img + sl * PR + wm * C::WTM + 4 * q;
+    float bce_c = 0.f, ps_c = 0.f;
+    // the tile's bias slice sits in LDS (zero beyond G; pre-scaled by -log2 e on the FAST path);
+    // slice mi + 1 is read while slice mi is computed
+    const float* bsl = bias_s + wm * C::WTM + 4 * q;
+    float4 b4n = *(const float4*)bsl;
 #pragma unroll
     for (int mi = 0; mi < C::FM; ++mi) {
-      // the tile's bias slice sits in LDS (zero beyond G)
-      const float4 b4 = *(const float4*)(bias_s + wm * C::WTM + mi * 16 + 4 * q);
+      const float4 b4 = b4n;
+      if (mi + 1 < C::FM) b4n = *(const float4*)(bsl + (mi + 1) * 16);
       const float bn[4] = {b4.x, b4.y, b4.z, b4.w};
-      const uint32_t xb = xw[mi >> 1] >> ((mi & 1) * 16 + 4 * q);
       float dl4[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float l = acc[mi][ni][j] + bn[j];
         if constexpr (FAST) {
-          const uint32_t sb = (xb << (31 - j)) & 0x80000000u;     // sign bit set iff x = 1
-          const float ns = __uint_as_float(sb | 0x3F800000u);      // x ? -1 : +1
-          const float t = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(__uint_as_float(__float_as_uint(l) ^ sb) * 1.4426950408889634f));
-          const float omt = 1.0f - t;
-          bce = fmaf(sm, fminf(-__builtin_amdgcn_logf(t), 144.26950408889634f), bce);  // min(-ln t,100)/ln 2
-          psum = fmaf(-ns * sm, t, psum);
-          const float qq = t * omt;
-          dl4[j] = fmaf(ns * omt, fminf(qq * 1e12f, 1.0f), wgam * qq);
+          const int msk = __builtin_amdgcn_sbfe((int)xw[mi >> 1], (mi & 1) * 16 + j, 1);  // x ? -1 : 0
+          const float y = fmaf(acc[mi][ni][j], -1.4426950408889634f, bn[j]);  // -l log2 e
+          const float p = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(y));
+          const float nomp = p - 1.0f;  // -(1 - p)
+          const float arg = bfi(msk, p, nomp);  // x ? p : p - 1
+          bce_c += fmaxf(__builtin_amdgcn_logf(fabsf(arg)), -144.26950408889634f);  // max(log2, -100/ln 2)
+          ps_c += p;
+          const float r = bfi(msk, nomp, p);    // p - x
+          const float s = __builtin_amdgcn_fmed3f(nomp * -1e12f * p, 0.0f, 1.0f);
+          float dl = r * s;
+          if constexpr (WG) dl = fmaf(-wgam, nomp * p, dl);
+          dl4[j] = dl;
         } else {
+          const uint32_t xb = xw[mi >> 1] >> ((mi & 1) * 16);
           const bool x = (xb >> j) & 1u;
+          const float l = acc[mi][ni][j] + bn[j];
           const float p = 1.0f / (1.0f + expf(-l));
-          bce = fmaf(sm, x ? -fmaxf(logf(p), -100.f) : -fmaxf(log1pf(-p), -100.f), bce);
-          psum = fmaf(sm, p, psum);
+          bce_c += x ? -fmaxf(logf(p), -100.f) : -fmaxf(log1pf(-p), -100.f);
+          ps_c += p;
           const float omp = 1.0f - p;
           const float dp = (p - (x ? 1.0f : 0.0f)) / fmaxf(omp * p, 1e-12f) + wgam;
           dl4[j] = dp * omp * p;
         }
       }
-      if (with_grad) {
+      if constexpr (GRAD) {
         if constexpr (sizeof(T) == 2) {
           uint2 pk;
-          pk.x = (uint32_t)f2bf(dl4[0]) | ((uint32_t)f2bf(dl4[1]) << 16);
-          pk.y = (uint32_t)f2bf(dl4[2]) | ((uint32_t)f2bf(dl4[3]) << 16);
+          pk.x = f2bf2(dl4[0], dl4[1]);
+          pk.y = f2bf2(dl4[2], dl4[3]);
           *(uint2*)(irow + mi * 16) = pk;
         } else {
           *(f32x4*)(irow + mi * 16) = f32x4{dl4[0], dl4[1], dl4[2], dl4[3]};
         }
       }
     }
-    if constexpr (FAST) {
-      // sum(p) = #(x == 0 targets of the valid strains) + sum(-ns*t): the q == 0 lanes count
-      // their strain's zero bits over the wave's WTM genes (q = 1..3 lanes hold the same words)
-      if (q == 0) {
-        int ones = 0;
-#pragma unroll
-        for (int k = 0; k < XW; ++k) ones += __builtin_popcount(xw[k]);
-        psum = fmaf(sm, (float)(C::WTM - ones), psum);
-      }
+    if (sok) {
+      bce += bce_c;
+      psum += ps_c;
     }
   }
 }
@@ -694,17 +776,17 @@ __device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], con
 // BCE / sum(p) of one padded gene (logit exactly 0, target 0): p = 1/2, BCE = -log(1/2)
 template <bool FAST>
 __device__ __forceinline__ void recon_pad_const(float& e0, float& p0) {
-  if constexpr (FAST) {
-    const float t = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(0.f));
-    e0 = fminf(-__builtin_amdgcn_logf(t), 144.26950408889634f) * 0.6931471805599453f;
-    p0 = t;
+  if constexpr (FAST) {  // the FAST element math at l = 0, x = 0
+    const float p = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(0.f));
+    e0 = -fmaxf(__builtin_amdgcn_logf(fabsf(p - 1.0f)), -144.26950408889634f) * 0.6931471805599453f;
+    p0 = p;
   } else {
     p0 = 1.0f / (1.0f + expf(-0.f));
     e0 = -fmaxf(log1pf(-p0), -100.f);
   }
 }
 
-template <class C, typename T, bool PP>
+template <class C, typename T, bool PP, bool GRAD>
 __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const float* __restrict__ bias,
                                                          const uint32_t* __restrict__ xbits, int64_t ldxb,
                                                          int with_grad, const float* __restrict__ scal,
@@ -724,7 +806,10 @@ __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const 
   float* colred = (float*)(smem + IMG);  // [RG][BM]
   float* red = colred + RG * C::BM;     // [2][32]
   float* bias_s = red + 64;             // [BM]
-  for (int i = threadIdx.x; i < C::BM; i += C::NT) bias_s[i] = tl.m0 + i < g.M ? bias[tl.m0 + i] : 0.f;
+  for (int i = threadIdx.x; i < C::BM; i += C::NT) {
+    const float b = tl.m0 + i < g.M ? bias[tl.m0 + i] : 0.f;
+    bias_s[i] = FAST ? b * -1.4426950408889634f : b;
+  }
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP)
     mainloop_pp<true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
@@ -735,10 +820,16 @@ __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const 
   const float wgam = scal[kScalWGamma];
   float bce = 0.f, psum = 0.f;
   T* img = (T*)smem;  // LDS image [BN strains][BM genes + 8] of T
-  recon_tile<C, T, FAST>(acc, xbits + ((tl.m0 + wm * C::WTM) >> 5), ldxb, bias_s, g.N, tl.n0, wm, wn, q, c, wgam,
-                         with_grad, img, bce, psum);
-  if constexpr (FAST) bce *= 0.6931471805599453f;
-  if (with_grad) {
+  // the gene-abundance term (w*gamma != 0, presets v1-v3) adds one FMA per element: a uniform
+  // branch between the two element loops
+  if (wgam != 0.f)
+    recon_tile<C, T, FAST, true, GRAD>(acc, xbits + ((tl.m0 + wm * C::WTM) >> 5), ldxb, bias_s, g.N, tl.n0, wm, wn, q,
+                                       c, wgam, img, bce, psum);
+  else
+    recon_tile<C, T, FAST, false, GRAD>(acc, xbits + ((tl.m0 + wm * C::WTM) >> 5), ldxb, bias_s, g.N, tl.n0, wm, wn,
+                                        q, c, wgam, img, bce, psum);
+  if constexpr (FAST) bce *= -0.6931471805599453f;
+  if constexpr (GRAD) {
     __syncthreads();
     // dL rows (strains) of BM genes: full 16-byte stores along each row. Thread i keeps one chunk
     // column (EPC genes) over rows i/CPR, +RG, ...: the same pass sums that chunk's dl over the
@@ -785,7 +876,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const 
     loss_part[tl.t * 2 + 0] = a;
     loss_part[tl.t * 2 + 1] = b;
   }
-  if (with_grad) {
+  if constexpr (GRAD) {
     for (int cc = threadIdx.x; cc < C::BM; cc += C::NT) {
       const int gg = tl.m0 + cc;
       float v = 0.f;
@@ -963,6 +1054,51 @@ TimedLaunch::~TimedLaunch() {
   if (idx >= 0) (void)hipEventRecord(tstate().ev[idx].second, s);
 }
 
+// C (or C^T) of the remainder tiles = the sum of their two K-half slices (fixed order). Block b
+// covers 4 rows (C) or 4 columns (C^T: 4 consecutive m per thread, one C^T row per 64 threads) of
+// remainder tile b / (BM/4), so the stores are 16-B runs either way.
+template <class C>
+__global__ __launch_bounds__(256) void k_rem_sum(const float* __restrict__ slab, int full, int tm, int tn, int M, int N,
+                                                 float* __restrict__ Cout, int64_t ldc, int trans) {
+  constexpr int BPT = C::BM / 4, TS = C::BM * C::BN;
+  static_assert(C::BM == 256 && C::BN == 256, "256 x 256 remainder tiles");
+  const int i = blockIdx.x / BPT;
+  const int grp = (blockIdx.x % BPT) * 4 + (threadIdx.x >> 6), e4 = (threadIdx.x & 63) * 4;
+  const TileXY tl = tile_at<C>(full + i, tm, tn, 0);
+  const float* s0 = slab + (int64_t)(2 * i) * TS;
+  float v[4];
+  if (!trans) {  // row grp, columns e4..e4+3
+    const int m = tl.m0 + grp;
+    if (m >= M) return;
+    const float4 a = *(const float4*)(s0 + grp * C::BN + e4), b = *(const float4*)(s0 + TS + grp * C::BN + e4);
+    v[0] = a.x + b.x; v[1] = a.y + b.y; v[2] = a.z + b.z; v[3] = a.w + b.w;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (tl.n0 + e4 + u < N) Cout[(int64_t)m * ldc + tl.n0 + e4 + u] = v[u];
+  } else {  // column grp (a C^T row), rows e4..e4+3
+    const int n = tl.n0 + grp;
+    if (n >= N) return;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = s0[(e4 + u) * C::BN + grp] + s0[TS + (e4 + u) * C::BN + grp];
+    float* dst = Cout + (int64_t)n * ldc + tl.m0 + e4;
+    if (tl.m0 + e4 + 3 < M && ((((uintptr_t)dst) & 15) == 0)) {
+      *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (tl.m0 + e4 + u < M) dst[u] = v[u];
+    }
+  }
+}
+
+// Tiles of a one-pass big-tile GEMM that land in a final round under half full (256 CUs): run
+// as two K-halves (remainder mode of k_gemm_store). 0 = none.
+static int rem_tiles(int ntile, int nkt) {
+  if (ntile <= 256 || nkt < 16) return 0;
+  const int r = ntile % 256;
+  return (r > 0 && r <= 128) ? r : 0;
+}
+
 // ------------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------------
@@ -1023,6 +1159,14 @@ static bool pp_enabled() { return pp_flag().load(std::memory_order_relaxed) != 0
 void set_gemm_pp(int on) { pp_flag().store(on ? 1 : 0, std::memory_order_relaxed); }
 int get_gemm_pp() { return pp_flag().load(std::memory_order_relaxed); }
 
+// remainder mode (GM2_OPT_GEMM_REM, default on): see rem_tiles
+static std::atomic<int>& rem_flag() {
+  static std::atomic<int> on{1};
+  return on;
+}
+void set_gemm_rem(int on) { rem_flag().store(on ? 1 : 0, std::memory_order_relaxed); }
+int get_gemm_rem() { return rem_flag().load(std::memory_order_relaxed); }
+
 // hipFuncAttributeMaxDynamicSharedMemorySize is per device: remember (device, kernel) pairs
 static void ensure_lds_attr(const void* fn, int bytes) {
   static std::mutex mu;
@@ -1059,36 +1203,73 @@ static int store_impl(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
   GemmArgs<T> a = g;
   const int kt = E<T>::KT;
   const int nkt = g.K / kt;
-  splits = std::max(1, std::min(splits, nkt));
-  a.k_per_split = (int)(round_up(nkt, splits) / splits) * kt;
-  splits = (int)((g.K + a.k_per_split - 1) / a.k_per_split);
-  const int tiles = (g.Mp / C::BM) * (g.Np / C::BN) * splits;
-  TimedLaunch tl(kKcGemmStore, s);
-  if (g.pk && g.qk) store_launch<C, T, true, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
-  else if (g.pk && !g.qk) store_launch<C, T, true, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
-  else if (!g.pk && !g.qk) store_launch<C, T, false, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
-  else throw Gm2Error("gemm: layout (P MN-major, Q K-major) not instantiated");
-  GM2_CHECK_LAUNCH();
+  const int ntile = (g.Mp / C::BM) * (g.Np / C::BN);
+  int tiles;
+  if (bn.rem > 0) {  // remainder mode: ntile - rem whole tiles + rem tiles as two K-halves
+    if (bias || bn.mode || bn.rem >= ntile || !bn.rem_slab) throw Gm2Error("gemm: bad remainder launch");
+    a.k_per_split = (int)(round_up(nkt, 2) / 2) * kt;
+    tiles = ntile + bn.rem;
+    splits = 1;
+  } else {
+    splits = std::max(1, std::min(splits, nkt));
+    a.k_per_split = (int)(round_up(nkt, splits) / splits) * kt;
+    splits = (int)((g.K + a.k_per_split - 1) / a.k_per_split);
+    tiles = ntile * splits;
+  }
+  {
+    TimedLaunch tl(kKcGemmStore, s);
+    if (g.pk && g.qk) store_launch<C, T, true, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+    else if (g.pk && !g.qk) store_launch<C, T, true, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+    else if (!g.pk && !g.qk) store_launch<C, T, false, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+    else throw Gm2Error("gemm: layout (P MN-major, Q K-major) not instantiated");
+    GM2_CHECK_LAUNCH();
+  }
+  if (bn.rem > 0) {
+    if constexpr (C::BN == 256) {
+      hipLaunchKernelGGL(k_rem_sum<C>, dim3(bn.rem * (C::BM / 4)), dim3(256), 0, s, bn.rem_slab, ntile - bn.rem,
+                         g.Mp / C::BM, g.Np / C::BN, g.M, g.N, C0, ldc, bn.trans);
+      GM2_CHECK_LAUNCH();
+    } else {
+      throw Gm2Error("gemm: remainder mode needs the 256-wide tile");
+    }
+  }
   return splits;
+}
+
+// remainder mode for a one-pass 256-tile launch when the scratch holds its slices
+template <typename T>
+static StoreEpi rem_epi(const GemmArgs<T>& g, float* scratch, int64_t scratch_floats) {
+  StoreEpi ep;
+  if (!scratch || !rem_flag().load(std::memory_order_relaxed)) return ep;
+  const int r = rem_tiles((g.Mp / 256) * (g.Np / 256), g.K / E<T>::KT);
+  if (r > 0 && (int64_t)r * 2 * 256 * 256 <= scratch_floats) {
+    ep.rem = r;
+    ep.rem_slab = scratch;
+  }
+  return ep;
 }
 
 template <typename T>
 int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
-                      const float* bias, hipStream_t s) {
+                      const float* bias, hipStream_t s, float* scratch, int64_t scratch_floats) {
   if (splits < 0) splits = plan_gemm(g).splits;
-  const StoreEpi none{};
   if (use_big(g)) {
     check_gemm(g, 256);
-    return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
+    const StoreEpi ep = (splits == 1 && !bias && (!C1 || msplit >= g.M)) ? rem_epi(g, scratch, scratch_floats)
+                                                                         : StoreEpi{};
+    return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, ep, s);
   }
+  const StoreEpi none{};
   check_gemm(g, 128);
   return store_impl<SmallDeep, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
 }
 
 template <typename T>
-bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s) {
+bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, float* scratch,
+                       int64_t scratch_floats) {
   if (plan_gemm(g).splits != 1) return false;
   StoreEpi ep;
+  if (use_big(g)) ep = rem_epi(g, scratch, scratch_floats);
   ep.trans = 1;
   if (use_big(g)) {
     check_gemm(g, 256);
@@ -1142,9 +1323,13 @@ static void recon_impl_k(const GemmArgs<T>& g, const float* bias, const uint32_t
   if (ldx * 32 < g.Mp || (ldx & 3)) throw Gm2Error("recon: target bit rows too short");
   constexpr int lds = recon_lds_bytes<C, T>();
   static_assert(lds <= 160 * 1024, "LDS budget");
-  ensure_lds_attr((const void*)k_gemm_recon_loss<C, T, PP>, lds);
-  hipLaunchKernelGGL((k_gemm_recon_loss<C, T, PP>), dim3((g.Mp / C::BM) * (g.Np / C::BN)), dim3(C::NT), lds, s, g,
-                     bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol);
+  auto go = [&](auto kern) {
+    ensure_lds_attr((const void*)kern, lds);
+    hipLaunchKernelGGL(kern, dim3((g.Mp / C::BM) * (g.Np / C::BN)), dim3(C::NT), lds, s, g, bias, X, ldx, with_grad,
+                       scal, dL, ldd, loss_part, colpart, ldcol);
+  };
+  if (with_grad) go(k_gemm_recon_loss<C, T, PP, true>);
+  else go(k_gemm_recon_loss<C, T, PP, false>);
 }
 
 template <class C, typename T>
@@ -1208,10 +1393,10 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
 }
 
 #define GM2_INST(T)                                                                                              \
-  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t);                        \
+  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t, float*, int64_t);      \
   template bool launch_gemm_bn<T>(const GemmArgs<T>&, float*, int64_t, const float*, const StoreEpi&, hipStream_t);   \
   template int launch_gemm_store<T>(const GemmArgs<T>&, int, float*, float*, int, int64_t, int64_t, const float*, \
-                                    hipStream_t);                                                                \
+                                    hipStream_t, float*, int64_t);                                               \
   template int gemm_recon_grid_blocks<T>(const GemmArgs<T>&);                                                   \
   template int gemm_recon_row_tiles<T>(const GemmArgs<T>&);                                                     \
   template GemmPlan plan_gemm<T>(const GemmArgs<T>&);                                                          \

@@ -21,6 +21,13 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+// two floats -> packed bf16 pair (lo = a) in one v_cvt_pk_bf16_f32
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+__device__ __forceinline__ uint32_t f2bf2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
+}
+
 // element-type adaptors: T is float (exact fp32 path) or bf16_t (bf16 MFMA path)
 template <typename T> struct E;
 template <> struct E<float> {

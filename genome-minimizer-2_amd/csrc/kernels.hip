@@ -416,8 +416,8 @@ template <typename T>
 __device__ __forceinline__ void store4(T* dst, float a, float b, float c, float d) {
   if constexpr (sizeof(T) == 2) {
     uint2 pk;
-    pk.x = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
-    pk.y = (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16);
+    pk.x = f2bf2(a, b);
+    pk.y = f2bf2(c, d);
     *(uint2*)dst = pk;
   } else {
     *(float4*)dst = make_float4(a, b, c, d);

@@ -9,7 +9,10 @@ Both route through the gfx950 kernels of libgm2.so (gm2 package); there is no CP
 
   --mode convert-samples --genes-path masks.npy [--output-file ids.npy]   run_binary_converter (:617-645)
         (host-side; the consumer of the sampled masks, explore_data/binary_converter.py)
-Modes outside the MI355X hot path (explore, preprocess, minimizer, experiment)
+  --mode minimizer --genes-path ids.npy [--genome-path wild_type.gb] [--single-file | --output-file f.fasta]
+        [--output-dir d] [--model-name m]   run_genome_minimizer (:528-614), the consumer of the gene
+        lists (gm2/minimizer.py: interval-union host rewrite of minimizer/minimizer_2.py)
+Modes outside the MI355X hot path (explore, preprocess, experiment)
 exit with code 2 and a message. Data files are looked up under the project root as in
 utils/directories.py:13-20 (default: $GM2_PROJECT_ROOT or the current directory; --project-root).
 Return codes follow main.py:647-692: 0 success, 1 failure.
@@ -37,7 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "genome-minimizer-2_amd"))
 
 MODES = ["training", "experiment", "minimizer", "explore", "preprocess", "sample", "convert-samples"]
-IMPLEMENTED = ("training", "sample", "convert-samples")
+IMPLEMENTED = ("training", "sample", "convert-samples", "minimizer")
 
 
 def parse_arguments(argv=None):
@@ -55,6 +58,11 @@ def parse_arguments(argv=None):
     p.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
     p.add_argument("--mask-dtype", choices=["float64", "uint8", "bits"], default="float64")
     p.add_argument("--no-csv", action="store_true")
+    p.add_argument("--genome-path", type=str, default=None,
+                   help="GenBank genome (default: <project root>/data/wild_type_sequence.gb)")
+    p.add_argument("--output-dir", type=str, default="./minimized_genomes")
+    p.add_argument("--single-file", action="store_true")
+    p.add_argument("--model-name", type=str, default="default")
     return p.parse_args(argv)
 
 
@@ -215,6 +223,53 @@ def run_binary_converter(args):
     return True
 
 
+def run_genome_minimizer(args):
+    """main.py:528-614 (same checks, messages and output layout)."""
+    from gm2.minimizer import process_multiple_genomes_multiple_files, process_multiple_genomes_single_file
+    print("\n" + "=" * 80 + "\nGENOME MINIMIZER RUN\n" + "=" * 80)
+    genome_path = args.genome_path or os.path.join(args.project_root, "data", "wild_type_sequence.gb")
+    if not os.path.exists(genome_path):
+        print(f"✗ Genome file not found: {genome_path}")
+        return None
+    if not args.genes_path:
+        print("✗ Genes path required for genome minimizer")
+        return None
+    if not os.path.exists(args.genes_path):
+        print(f"✗ Genes file not found: {args.genes_path}")
+        return None
+    print(f"\n{'=' * 80}\nProcessing genome: {Path(genome_path).name}\nUsing genes from: {Path(args.genes_path).name}"
+          f"\nModel name: {args.model_name}\n{'=' * 80}")
+    try:
+        if args.output_file:
+            output_dir, output_filename = Path(args.output_file).parent, Path(args.output_file).name
+        elif args.single_file:
+            output_dir, output_filename = Path(args.output_dir), f"minimized_genomes_{args.model_name}.fasta"
+        else:
+            output_dir, output_filename = Path(args.output_dir), None
+        output_dir.mkdir(parents=True, exist_ok=True)
+        print(f"✓ Created output directory: {output_dir}")
+        if args.single_file or args.output_file:
+            output_file = output_dir / output_filename
+            print(f"Generating single FASTA file: {output_file}")
+            result = process_multiple_genomes_single_file(genome_path=genome_path, genes_path=args.genes_path,
+                                                          model_name=args.model_name, output_file=str(output_file))
+            print("\n✓ GENOME MINIMIZATION COMPLETED!")
+            print(f"- Single file generated: {output_file}")
+        else:
+            print(f"Generating multiple files in: {output_dir}")
+            result = process_multiple_genomes_multiple_files(genome_path=genome_path, genes_path=args.genes_path,
+                                                             model_name=args.model_name, output_dir=str(output_dir))
+            print("\n✓ GENOME MINIMIZATION COMPLETED!")
+        print(f"- Processed: {result['genome_count']} genomes")
+        print(f"- Average percentage reduction: {result['average_reduction_pct']:.1f}%")
+        print(f"- Average genome length: {result['average_length_bp']:,.1f} bp")
+        return result
+    except Exception as e:
+        print(f"✗ Error during genome minimization: {e}")
+        traceback.print_exc()
+        return None
+
+
 def main(argv=None):
     args = parse_arguments(argv)
     dist = None
@@ -241,7 +296,7 @@ def _main(args):
         print(f"✗ --mode {args.mode} is outside the MI355X hot path of this build (SURVEY.md §2); "
               "use the reference for it")
         return 2
-    if args.mode != "convert-samples" and not check_data_availability(args.project_root):
+    if args.mode not in ("convert-samples", "minimizer") and not check_data_availability(args.project_root):
         print("\n✗ Cannot proceed without required data files")
         return 1
     try:
@@ -249,6 +304,15 @@ def _main(args):
             return 0 if run_sampling(args) else 1
         if args.mode == "convert-samples":
             return 0 if run_binary_converter(args) else 1
+        if args.mode == "minimizer":
+            if run_genome_minimizer(args) is None:
+                return 1
+            print("\n" + "=" * 80 + "\nPROCESS COMPLETED!\n" + "=" * 80)
+            if args.single_file or args.output_file:
+                print("- Check for the generated FASTA file\n")
+            else:
+                print(f"- Check the {args.output_dir}/ directory for minimized genomes\n")
+            return 0
         results = run_single_experiment(args)
         if results is None:
             return 1
