@@ -116,7 +116,7 @@ def test_two_rank_step(tmp_path):
 @pytest.mark.parametrize("world", [2])
 def test_main_cli_modes_without_gpu(world, tmp_path):
     import main as cli
-    assert cli.main(["--mode", "minimizer"]) == 2
+    assert cli.main(["--mode", "minimizer", "--project-root", str(tmp_path)]) == 1  # no genome file
     assert cli.main(["--mode", "explore"]) == 2
     assert cli.main(["--mode", "training", "--project-root", str(tmp_path)]) == 1  # no data files
     assert cli.detect_version("/x/saved_VAE_v2.pt") == "v2" and cli.detect_version("model.pt") is None
