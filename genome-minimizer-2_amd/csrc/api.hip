@@ -191,16 +191,7 @@ SideRes* side_res() {
   std::lock_guard<std::mutex> lk(mu);
   SideRes& r = per_dev[dev];
   if (!r.side) {
-    // env GM2_SIDE_PRIO = low / high: the side stream at the device's least / greatest priority
-    // (measurement switch; default: normal priority)
-    const char* pe = getenv("GM2_SIDE_PRIO");
-    if (pe && (pe[0] == 'l' || pe[0] == 'h')) {
-      int least = 0, greatest = 0;
-      HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      HIP_OK(hipStreamCreateWithPriority(&r.side, hipStreamNonBlocking, pe[0] == 'l' ? least : greatest));
-    } else {
-      HIP_OK(hipStreamCreateWithFlags(&r.side, hipStreamNonBlocking));
-    }
+    HIP_OK(hipStreamCreateWithFlags(&r.side, hipStreamNonBlocking));
     r.ev.resize(64);
     for (auto& e : r.ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
@@ -266,7 +257,7 @@ void gemm_to(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64
   const int64_t slab = round_up((int64_t)M * N, 4);
   if ((int64_t)S * slab > c.slab_cap) S = 1;
   if (S <= 1) {
-    launch_gemm_store<T>(g, 1, C0, C1, msplit, ldc, 0, nullptr, c.s, c.f(c.slab_off), c.slab_cap);
+    launch_gemm_store<T>(g, 1, C0, C1, msplit, ldc, 0, nullptr, c.s);
     return;
   }
   S = launch_gemm_store<T>(g, S, c.f(c.slab_off), nullptr, 0, N, slab, nullptr, c.s);
@@ -426,12 +417,14 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   // Written as dW9^T[h][g] = sum_b A5^T[h][b] dL[b][g] with A5^T K-major (a transposed copy made
   // here) and dL MN-major, stored transposed: one transposed-read operand instead of two (the
   // 256x256 tile is LDS-read bound with two). Plans with split-K keep the both-MN-major form.
+  // (Forking it last instead, beside the input-layer dWe0 GEMM, measured the same step time on one
+  // GPU; first keeps gradient bucket 0 early for the data-parallel exchange.)
   fork();
   {
     GemmArgs<T> g9{c.t(l.AT5), Bp, c.t(l.dL), Gp, H, G, Bp, H, Gp, 0, 1, 0};
     if (plan_gemm<T>(g9).splits == 1) {
       launch_transpose<T>(c.t(l.A[5]), H, Bp, H, c.t(l.AT5), Bp, w.s);
-      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, w.s, w.f(w.slab_off), w.slab_cap);
+      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, w.s);
     } else {
       gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
     }
@@ -753,9 +746,8 @@ int gm2_gemm(int prec, int pk, int qk, const void* P, int64_t ldp, const void* Q
       GemmArgs<T> g{(const T*)P, ldp, (const T*)Q, ldq, (int)M, (int)N, (int)K, (int)round_up(M, kTile),
                     (int)round_up(N, kTile), 0, pk ? 1 : 0, qk ? 1 : 0};
       if (splits < 0) splits = plan_gemm(g).splits;  // the hot path's own tile / split-K plan
-      if (splits == 0 || splits == 1) {  // slab_ws (optional): remainder-mode scratch, 2 Mp Np floats
-        launch_gemm_store<T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, (hipStream_t)stream, slab_ws,
-                             slab_ws ? 2 * round_up(M, 256) * round_up(N, 256) : 0);
+      if (splits == 0 || splits == 1) {
+        launch_gemm_store<T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, (hipStream_t)stream);
       } else {
         if (!slab_ws) throw Gm2Error("gemm: split-K needs slab_ws");
         const int S = launch_gemm_store<T>(g, splits, slab_ws, nullptr, 0, ldc, (int64_t)M * ldc, nullptr,
@@ -848,7 +840,6 @@ int gm2_set_option(int key, int value) {
         break;
       case GM2_OPT_SMALL_SPLIT: set_small_split(value); break;
       case GM2_OPT_BN_EPILOGUE: set_bn_epilogue(value); break;
-      case GM2_OPT_GEMM_REM: set_gemm_rem(value); break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });
@@ -862,7 +853,6 @@ int gm2_get_option(int key, int* value) {
       case GM2_OPT_RECON_TILE: *value = get_recon_tile(); break;
       case GM2_OPT_SMALL_SPLIT: *value = get_small_split(); break;
       case GM2_OPT_BN_EPILOGUE: *value = get_bn_epilogue(); break;
-      case GM2_OPT_GEMM_REM: *value = get_gemm_rem(); break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });

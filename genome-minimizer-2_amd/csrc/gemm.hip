@@ -371,6 +371,7 @@ __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_
   for (int h = 0; h < 4; ++h) issue(0, h);
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   pp::barrier();
+  GM2_STAMP(1);
   if (wm == 1) pp::barrier();  // stagger: group 1 one barrier behind
   for (int t = 0; t < nk; ++t) {
     const bool more = t + 1 < nk;
@@ -444,36 +445,9 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
                                                     const float* __restrict__ bias, StoreEpi bn) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   GM2_STAMP(0);
-  const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
-  TileXY tl;
-  int kbeg, kend;
-  // Remainder mode (bn.rem > 0, one K pass): the first ntile - rem tiles run whole; each of the
-  // last rem tiles (the ones that would leave most CUs idle in the final round) runs as two
-  // K-halves into bn.rem_slab [rem][2][BM][BN], summed into C by k_rem_sum.
-  bool remtile = false;
-  float* outp = C0;
-  if (bn.rem > 0) {
-    // by dispatch order: blocks [0, full) are the whole tiles (XCD-remapped among themselves), the
-    // last 2*rem blocks the halves, spread over every XCD (a remap over the whole grid would put
-    // the last logical tiles on one XCD)
-    const int full = tm * tn - bn.rem, bid = blockIdx.x;
-    if (bid < full) {
-      tl = tile_at<C>(xcd_wg(bid, full), tm, tn, 0);
-      kbeg = 0;
-      kend = g.K;
-    } else {
-      const int r = bid - full;
-      tl = tile_at<C>(full + (r >> 1), tm, tn, 0);
-      kbeg = (r & 1) * g.k_per_split;
-      kend = min(g.K, kbeg + g.k_per_split);
-      remtile = true;
-      outp = bn.rem_slab + (int64_t)r * C::BM * C::BN;
-    }
-  } else {
-    tl = tile_of<C>(tm, tn);
-    kbeg = tl.split * g.k_per_split;
-    kend = min(g.K, kbeg + g.k_per_split);
-  }
+  const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
+  const int kbeg = tl.split * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = (kend - kbeg) / E<T>::KT;
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP)
@@ -482,18 +456,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
     mainloop<C, T, AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
   GM2_STAMP(2);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
-  // output rows: outp + (m - mo) * outld + (n - no) for m < msplit (a remainder tile: its own
-  // dense [BM][BN] slice), C1 + (m - msplit) * ldc otherwise
-  int64_t outld = ldc;
-  int mo = 0, no = 0;
-  if (remtile) {
-    outld = C::BN;
-    mo = tl.m0;
-    no = tl.n0;
-    msplit = 1 << 30;
-  } else {
-    outp = C0 + (int64_t)tl.split * slab;
-  }
+  float* Cz = C0 + (int64_t)tl.split * slab;
   // Stage one 64-row band of the tile at a time through the (now free) staging LDS (row pitch
   // BN + 4 floats: the accumulator writes of lanes 16 apart land 16 banks apart), then store whole
   // rows with 16-byte stores (4 columns per thread; scalar where C's rows are not 16-B aligned or
@@ -508,7 +471,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
   static_assert(C::NT % TPR == 0 && BR % RPI == 0 && 2 * C::NT * 16 <= C::LDS, "epilogue shape");
   const int cq = (threadIdx.x % TPR) * 4, rq = threadIdx.x / TPR;
   const int n = tl.n0 + cq;
-  const bool vec = remtile || (((ldc | slab) & 3) == 0 && ((((uintptr_t)C0) | ((uintptr_t)C1)) & 15) == 0);
+  const bool vec = ((ldc | slab) & 3) == 0 && ((((uintptr_t)C0) | ((uintptr_t)C1)) & 15) == 0;
   // rows that are not 16-B aligned (ldc % 4 != 0, e.g. the [H][G] input-layer gradient at odd G):
   // each row's chunks shift to its first 16-B boundary, the head elements go scalar
   const bool shiftvec = !vec && slab == 0 && !bias && bn.mode == 0 && !bn.trans && msplit >= g.M &&
@@ -537,7 +500,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
             img[(mi * 16 + 4 * (lane >> 4) + j) * pitch + wn * C::WTN + ni * 16 + (lane & 15)] = acc[mi0 + mi][ni][j];
     }
     __syncthreads();
-    if (bn.trans && !remtile) {
+    if (bn.trans) {
       const int q = threadIdx.x & 15;
       const int m = tl.m0 + h * BR + 4 * q;
       for (int c = threadIdx.x >> 4; c < C::BN; c += C::NT / 16) {
@@ -566,7 +529,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
       const int m = tl.m0 + h * BR + r;
       if (m >= g.M) break;
       if (shiftvec) {
-        float* rowp = outp + (int64_t)m * ldc + tl.n0;
+        float* rowp = C0 + (int64_t)m * ldc + tl.n0;
         const float* src = img + r * pitch;
         const int a = (int)((4u - (uint32_t)(((uintptr_t)rowp >> 2) & 3u)) & 3u);
         const int c = a + cq;
@@ -584,7 +547,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
       }
       const float4 w = *(const float4*)(img + r * pitch + cq);
       const float v[4] = {w.x + bb[0], w.y + bb[1], w.z + bb[2], w.w + bb[3]};
-      float* dst = m < msplit ? outp + (int64_t)(m - mo) * outld + (n - no) : C1 + (int64_t)(m - msplit) * ldc + n;
+      float* dst = (m < msplit ? Cz + (int64_t)m * ldc : C1 + (int64_t)(m - msplit) * ldc) + n;
       if (vec && n + 3 < g.N) {
         *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
       } else {
@@ -1054,51 +1017,6 @@ TimedLaunch::~TimedLaunch() {
   if (idx >= 0) (void)hipEventRecord(tstate().ev[idx].second, s);
 }
 
-// C (or C^T) of the remainder tiles = the sum of their two K-half slices (fixed order). Block b
-// covers 4 rows (C) or 4 columns (C^T: 4 consecutive m per thread, one C^T row per 64 threads) of
-// remainder tile b / (BM/4), so the stores are 16-B runs either way.
-template <class C>
-__global__ __launch_bounds__(256) void k_rem_sum(const float* __restrict__ slab, int full, int tm, int tn, int M, int N,
-                                                 float* __restrict__ Cout, int64_t ldc, int trans) {
-  constexpr int BPT = C::BM / 4, TS = C::BM * C::BN;
-  static_assert(C::BM == 256 && C::BN == 256, "256 x 256 remainder tiles");
-  const int i = blockIdx.x / BPT;
-  const int grp = (blockIdx.x % BPT) * 4 + (threadIdx.x >> 6), e4 = (threadIdx.x & 63) * 4;
-  const TileXY tl = tile_at<C>(full + i, tm, tn, 0);
-  const float* s0 = slab + (int64_t)(2 * i) * TS;
-  float v[4];
-  if (!trans) {  // row grp, columns e4..e4+3
-    const int m = tl.m0 + grp;
-    if (m >= M) return;
-    const float4 a = *(const float4*)(s0 + grp * C::BN + e4), b = *(const float4*)(s0 + TS + grp * C::BN + e4);
-    v[0] = a.x + b.x; v[1] = a.y + b.y; v[2] = a.z + b.z; v[3] = a.w + b.w;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (tl.n0 + e4 + u < N) Cout[(int64_t)m * ldc + tl.n0 + e4 + u] = v[u];
-  } else {  // column grp (a C^T row), rows e4..e4+3
-    const int n = tl.n0 + grp;
-    if (n >= N) return;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = s0[(e4 + u) * C::BN + grp] + s0[TS + (e4 + u) * C::BN + grp];
-    float* dst = Cout + (int64_t)n * ldc + tl.m0 + e4;
-    if (tl.m0 + e4 + 3 < M && ((((uintptr_t)dst) & 15) == 0)) {
-      *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (tl.m0 + e4 + u < M) dst[u] = v[u];
-    }
-  }
-}
-
-// Tiles of a one-pass big-tile GEMM that land in a final round under half full (256 CUs): run
-// as two K-halves (remainder mode of k_gemm_store). 0 = none.
-static int rem_tiles(int ntile, int nkt) {
-  if (ntile <= 256 || nkt < 16) return 0;
-  const int r = ntile % 256;
-  return (r > 0 && r <= 128) ? r : 0;
-}
-
 // ------------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------------
@@ -1159,14 +1077,6 @@ static bool pp_enabled() { return pp_flag().load(std::memory_order_relaxed) != 0
 void set_gemm_pp(int on) { pp_flag().store(on ? 1 : 0, std::memory_order_relaxed); }
 int get_gemm_pp() { return pp_flag().load(std::memory_order_relaxed); }
 
-// remainder mode (GM2_OPT_GEMM_REM, default on): see rem_tiles
-static std::atomic<int>& rem_flag() {
-  static std::atomic<int> on{1};
-  return on;
-}
-void set_gemm_rem(int on) { rem_flag().store(on ? 1 : 0, std::memory_order_relaxed); }
-int get_gemm_rem() { return rem_flag().load(std::memory_order_relaxed); }
-
 // hipFuncAttributeMaxDynamicSharedMemorySize is per device: remember (device, kernel) pairs
 static void ensure_lds_attr(const void* fn, int bytes) {
   static std::mutex mu;
@@ -1203,73 +1113,36 @@ static int store_impl(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
   GemmArgs<T> a = g;
   const int kt = E<T>::KT;
   const int nkt = g.K / kt;
-  const int ntile = (g.Mp / C::BM) * (g.Np / C::BN);
-  int tiles;
-  if (bn.rem > 0) {  // remainder mode: ntile - rem whole tiles + rem tiles as two K-halves
-    if (bias || bn.mode || bn.rem >= ntile || !bn.rem_slab) throw Gm2Error("gemm: bad remainder launch");
-    a.k_per_split = (int)(round_up(nkt, 2) / 2) * kt;
-    tiles = ntile + bn.rem;
-    splits = 1;
-  } else {
-    splits = std::max(1, std::min(splits, nkt));
-    a.k_per_split = (int)(round_up(nkt, splits) / splits) * kt;
-    splits = (int)((g.K + a.k_per_split - 1) / a.k_per_split);
-    tiles = ntile * splits;
-  }
-  {
-    TimedLaunch tl(kKcGemmStore, s);
-    if (g.pk && g.qk) store_launch<C, T, true, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
-    else if (g.pk && !g.qk) store_launch<C, T, true, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
-    else if (!g.pk && !g.qk) store_launch<C, T, false, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
-    else throw Gm2Error("gemm: layout (P MN-major, Q K-major) not instantiated");
-    GM2_CHECK_LAUNCH();
-  }
-  if (bn.rem > 0) {
-    if constexpr (C::BN == 256) {
-      hipLaunchKernelGGL(k_rem_sum<C>, dim3(bn.rem * (C::BM / 4)), dim3(256), 0, s, bn.rem_slab, ntile - bn.rem,
-                         g.Mp / C::BM, g.Np / C::BN, g.M, g.N, C0, ldc, bn.trans);
-      GM2_CHECK_LAUNCH();
-    } else {
-      throw Gm2Error("gemm: remainder mode needs the 256-wide tile");
-    }
-  }
+  splits = std::max(1, std::min(splits, nkt));
+  a.k_per_split = (int)(round_up(nkt, splits) / splits) * kt;
+  splits = (int)((g.K + a.k_per_split - 1) / a.k_per_split);
+  const int tiles = (g.Mp / C::BM) * (g.Np / C::BN) * splits;
+  TimedLaunch tl(kKcGemmStore, s);
+  if (g.pk && g.qk) store_launch<C, T, true, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+  else if (g.pk && !g.qk) store_launch<C, T, true, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+  else if (!g.pk && !g.qk) store_launch<C, T, false, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+  else throw Gm2Error("gemm: layout (P MN-major, Q K-major) not instantiated");
+  GM2_CHECK_LAUNCH();
   return splits;
-}
-
-// remainder mode for a one-pass 256-tile launch when the scratch holds its slices
-template <typename T>
-static StoreEpi rem_epi(const GemmArgs<T>& g, float* scratch, int64_t scratch_floats) {
-  StoreEpi ep;
-  if (!scratch || !rem_flag().load(std::memory_order_relaxed)) return ep;
-  const int r = rem_tiles((g.Mp / 256) * (g.Np / 256), g.K / E<T>::KT);
-  if (r > 0 && (int64_t)r * 2 * 256 * 256 <= scratch_floats) {
-    ep.rem = r;
-    ep.rem_slab = scratch;
-  }
-  return ep;
 }
 
 template <typename T>
 int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
-                      const float* bias, hipStream_t s, float* scratch, int64_t scratch_floats) {
+                      const float* bias, hipStream_t s) {
   if (splits < 0) splits = plan_gemm(g).splits;
+  const StoreEpi none{};
   if (use_big(g)) {
     check_gemm(g, 256);
-    const StoreEpi ep = (splits == 1 && !bias && (!C1 || msplit >= g.M)) ? rem_epi(g, scratch, scratch_floats)
-                                                                         : StoreEpi{};
-    return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, ep, s);
+    return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
   }
-  const StoreEpi none{};
   check_gemm(g, 128);
   return store_impl<SmallDeep, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
 }
 
 template <typename T>
-bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, float* scratch,
-                       int64_t scratch_floats) {
+bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s) {
   if (plan_gemm(g).splits != 1) return false;
   StoreEpi ep;
-  if (use_big(g)) ep = rem_epi(g, scratch, scratch_floats);
   ep.trans = 1;
   if (use_big(g)) {
     check_gemm(g, 256);
@@ -1393,10 +1266,10 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
 }
 
 #define GM2_INST(T)                                                                                              \
-  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t, float*, int64_t);      \
+  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t);                        \
   template bool launch_gemm_bn<T>(const GemmArgs<T>&, float*, int64_t, const float*, const StoreEpi&, hipStream_t);   \
   template int launch_gemm_store<T>(const GemmArgs<T>&, int, float*, float*, int, int64_t, int64_t, const float*, \
-                                    hipStream_t, float*, int64_t);                                               \
+                                    hipStream_t);                                                                \
   template int gemm_recon_grid_blocks<T>(const GemmArgs<T>&);                                                   \
   template int gemm_recon_row_tiles<T>(const GemmArgs<T>&);                                                     \
   template GemmPlan plan_gemm<T>(const GemmArgs<T>&);                                                          \

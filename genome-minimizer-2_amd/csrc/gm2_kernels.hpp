@@ -90,27 +90,20 @@ struct StoreEpi {
   const float* beta = nullptr;
   int H = 0;
   int trans = 0;  // store C^T: C0[n * ldc + m] (no bias, no statistics, one K pass)
-  int rem = 0;    // remainder mode: the last `rem` tiles as two K-halves into rem_slab (k_gemm_store)
-  float* rem_slab = nullptr;
 };
 // GEMM + BatchNorm statistics of its output in one launch when the plan allows (one K pass of
 // 128-row tiles); returns false (nothing launched) otherwise
 template <typename T>
 bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const StoreEpi& bn, hipStream_t s);
 // C^T = (P . Q^T)^T into C [N][ldc] in one launch when the plan is one K pass; false otherwise
-// (scratch: fp32 space for the remainder-mode slices of a one-pass 256-tile launch, or nullptr)
 template <typename T>
-bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, float* scratch = nullptr,
-                       int64_t scratch_floats = 0);
+bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s);
 void set_bn_epilogue(int on);
 int get_bn_epilogue();
 // splits < 0: use plan_gemm's split-K factor. Returns the number of slabs written.
 template <typename T>
 int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc,
-                      int64_t slab, const float* bias, hipStream_t s, float* scratch = nullptr,
-                      int64_t scratch_floats = 0);
-void set_gemm_rem(int on);
-int get_gemm_rem();
+                      int64_t slab, const float* bias, hipStream_t s);
 template <typename T>
 int gemm_recon_grid_blocks(const GemmArgs<T>& g);
 template <typename T>

@@ -17,8 +17,11 @@ constexpr double kBnMomentum = 0.1;   // nn.BatchNorm1d default momentum
 // epilogue (bit c%32 of word c/32 of row r). A wave streams one strain row at a time, 16 bytes per
 // lane = 1 KiB of contiguous columns per load instruction (2 KiB / 4 KiB per store), four rows
 // per wave in flight; a block = 4 waves x 4 rows x 1024 columns. Each lane's 16 columns give a
-// 16-bit piece of one target word, the even lane of each pair writes the word.
+// 16-bit piece of one target word, the even lane of each pair writes the word. Rows and X stream
+// (non-temporal loads / stores: read once here, X re-read from HBM by the input-layer GEMMs).
 // ---------------------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data, int64_t ld_data,
                                               const int32_t* __restrict__ rows, int B, int G, int Gp,
@@ -35,7 +38,8 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data
     v[k] = make_uint4(0, 0, 0, 0);
     if (r < B) {
       const int64_t src = rows ? (int64_t)rows[r] : (int64_t)r;
-      v[k] = *(const uint4*)(data + src * ld_data + c);
+      const u32x4 t = __builtin_nontemporal_load((const u32x4*)(data + src * ld_data + c));
+      v[k] = make_uint4(t[0], t[1], t[2], t[3]);
     }
   }
 #pragma unroll
@@ -54,8 +58,8 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data
       uint32_t w[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) w[i] = (b[2 * i] ? 0x3F80u : 0u) | ((b[2 * i + 1] ? 0x3F80u : 0u) << 16);
-      *(uint4*)dst = make_uint4(w[0], w[1], w[2], w[3]);
-      *(uint4*)(dst + 8) = make_uint4(w[4], w[5], w[6], w[7]);
+      __builtin_nontemporal_store(u32x4{w[0], w[1], w[2], w[3]}, (u32x4*)dst);
+      __builtin_nontemporal_store(u32x4{w[4], w[5], w[6], w[7]}, (u32x4*)(dst + 8));
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -426,6 +430,16 @@ __device__ __forceinline__ void store4(T* dst, float a, float b, float c, float 
 
 __device__ __forceinline__ float sgnf(float x) { return (float)((x > 0.f) - (x < 0.f)); }
 
+// 16-byte non-temporal (streaming) load / store: for data every pass touches exactly once
+// (measured on the Adam pass: 650 -> 546 us, 5.4 -> 6.45 TB/s)
+__device__ __forceinline__ float4 ntload4(const float* p) {
+  const f32x4 v = __builtin_nontemporal_load((const f32x4*)p);
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void ntstore4(float* p, const float (&v)[4]) {
+  __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, (f32x4*)p);
+}
+
 __global__ __launch_bounds__(256) void k_grad_stats(const float* __restrict__ p, const float* __restrict__ g,
                                                   int64_t n, const float* __restrict__ scal,
                                                   double* __restrict__ part) {
@@ -436,7 +450,7 @@ __global__ __launch_bounds__(256) void k_grad_stats(const float* __restrict__ p,
   const int64_t stride = (int64_t)gridDim.x * 256;
   if (lam != 0.f) {  // L1 present: the norm needs sign(p), the loss needs sum|p|
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
-      const float4 pv = *(const float4*)(p + 4 * i), gv = *(const float4*)(g + 4 * i);
+      const float4 pv = ntload4(p + 4 * i), gv = ntload4(g + 4 * i);
       const float a = gv.x + lam * sgnf(pv.x), b = gv.y + lam * sgnf(pv.y);
       const float c = gv.z + lam * sgnf(pv.z), d = gv.w + lam * sgnf(pv.w);
       ss += (double)a * a + (double)b * b + (double)c * c + (double)d * d;
@@ -449,7 +463,7 @@ __global__ __launch_bounds__(256) void k_grad_stats(const float* __restrict__ p,
     }
   } else {  // no L1 term (v0): gradients only, half the traffic
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
-      const float4 gv = *(const float4*)(g + 4 * i);
+      const float4 gv = ntload4(g + 4 * i);
       ss += (double)gv.x * gv.x + (double)gv.y * gv.y + (double)gv.z * gv.z + (double)gv.w * gv.w;
     }
     for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
@@ -504,15 +518,16 @@ __global__ __launch_bounds__(256) void k_adam_fused(TensorTable tt, const float*
   const float cc = clip[0];
   T* sh = (T*)d.shadow;
   if (e0 + 4096 <= numel) {
-    // whole block: all 16 loads of the thread in flight before the first update
+    // whole block: all 16 loads of the thread in flight before the first update; every byte is
+    // touched once per step, so loads and stores are non-temporal (streamed past the caches)
     float4 pv[4], gv[4], mv[4], vv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int64_t gi = d.off + e0 + (int64_t)(k * 256 + threadIdx.x) * 4;
-      pv[k] = *(const float4*)(p + gi);
-      gv[k] = *(const float4*)(g + gi);
-      mv[k] = *(const float4*)(m + gi);
-      vv[k] = *(const float4*)(v + gi);
+      pv[k] = ntload4(p + gi);
+      gv[k] = ntload4(g + gi);
+      mv[k] = ntload4(m + gi);
+      vv[k] = ntload4(v + gi);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -529,9 +544,9 @@ __global__ __launch_bounds__(256) void k_adam_fused(TensorTable tt, const float*
         const float denom = sqrtf(ve[u]) / bc2s + aeps;
         pe[u] = pe[u] + negstep * (me[u] / denom);
       }
-      *(float4*)(p + gi) = make_float4(pe[0], pe[1], pe[2], pe[3]);
-      *(float4*)(m + gi) = make_float4(me[0], me[1], me[2], me[3]);
-      *(float4*)(v + gi) = make_float4(ve[0], ve[1], ve[2], ve[3]);
+      ntstore4(p + gi, pe);
+      ntstore4(m + gi, me);
+      ntstore4(v + gi, ve);
       if (sh) {
         int64_t r = e / d.cols, c = e - r * d.cols;
         if ((d.cols & 3) == 0 && (d.sld & 3) == 0) {

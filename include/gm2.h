@@ -200,9 +200,7 @@ int gm2_reparameterize(int64_t n, const float* mu, const float* logvar, const fl
  * the M (N) extent is padded to a multiple of 128 in the allocation, K % 64 == 0, pads zero.
  * (P MN-major with Q K-major is not instantiated.) splits 0/1: one pass straight into C; > 1: that
  * many split-K slices; < 0: the hot path's own tile / split plan (at most 8 slices). Split runs
- * need slab_ws (fp32, splits * M * ldc elements) and sum the slices into C. One-pass runs take
- * slab_ws as optional scratch (NULL allowed; else at least 2 * Mp * Np floats with Mp, Np = M, N
- * rounded up to 256) for the remainder mode (GM2_OPT_GEMM_REM). */
+ * need slab_ws (fp32, splits * M * ldc elements) and sum the slices into C. */
 int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t ldp, const void* Q,
              int64_t ldq, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, int splits,
              float* slab_ws, void* stream);
@@ -223,17 +221,13 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       hidden layers).
  *   GM2_OPT_BN_EPILOGUE 1 = BatchNorm batch statistics (forward) and backward partial sums taken
  *                       in the producing GEMM's store epilogue where the plan allows (default),
- *                       0 = always a separate statistics pass.
- *   GM2_OPT_GEMM_REM    1 = one-pass 256-tile GEMMs whose last round would be under half full run
- *                       those last tiles as two K-halves summed by a small pass (default; needs
- *                       the slab scratch), 0 = off. */
+ *                       0 = always a separate statistics pass. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
   GM2_OPT_RECON_TILE = 3,
   GM2_OPT_SMALL_SPLIT = 4,
-  GM2_OPT_BN_EPILOGUE = 5,
-  GM2_OPT_GEMM_REM = 6
+  GM2_OPT_BN_EPILOGUE = 5
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);

@@ -90,21 +90,9 @@ def test_gemm(prec, layout, M, N, K, splits, gemm_pp):
                                                ("dWe0nn", "nn", 1024, 55039, 4096), ("enc0", "nt", 4096, 1024, 55040),
                                                ("dA5", "nn", 4096, 1024, 55040), ("hid", "nt", 4096, 1024, 1024),
                                                ("hid_dX", "nn", 4096, 1024, 1024), ("hid_dW", "tn", 1024, 1024, 4096)])
-@pytest.mark.parametrize("rem", [1, 0])
-def test_gemm_hot_shapes(name, layout, M, N, K, gemm_pp, rem):
-    """Also covers the remainder mode (860 tiles of 256x256: the last 92 as two K-halves summed by
-    k_rem_sum; GM2_OPT_GEMM_REM) and the row-shifted 16-B stores of an odd ldc (N = 55,039: the
-    [H][G] input-layer gradient rows are not 16-B aligned)."""
-    if not rem and name not in ("dW9", "dWe0", "dWe0u"):
-        pytest.skip("remainder mode only changes the 860-tile shapes")
-    native.set_option(native.OPT_GEMM_REM, rem)
-    try:
-        _hot_shape(name, layout, M, N, K)
-    finally:
-        native.set_option(native.OPT_GEMM_REM, 1)
-
-
-def _hot_shape(name, layout, M, N, K):
+def test_gemm_hot_shapes(name, layout, M, N, K, gemm_pp):
+    """(dWe0u / dWe0nn: N = 55,039 = ldc, the [H][G] input-layer gradient whose rows are not 16-B
+    aligned: row-shifted 16-B stores.)"""
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(M + N + K)
     Mp, Np = -(-M // 128) * 128, -(-N // 128) * 128
