@@ -472,10 +472,13 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
   const int cq = (threadIdx.x % TPR) * 4, rq = threadIdx.x / TPR;
   const int n = tl.n0 + cq;
   const bool vec = ((ldc | slab) & 3) == 0 && ((((uintptr_t)C0) | ((uintptr_t)C1)) & 15) == 0;
-  // rows that are not 16-B aligned (ldc % 4 != 0, e.g. the [H][G] input-layer gradient at odd G):
-  // each row's chunks shift to its first 16-B boundary, the head elements go scalar
+  // Rows that are not 16-B aligned (ldc % 4 != 0, e.g. the [H][G] input-layer gradient at odd G):
+  // row m's elements go into the image shifted by e_m = (address of (m, n0) in floats) % 4, so
+  // every image chunk of 4 is one aligned 16-B global chunk; only the two end chunks of a row are
+  // partial. e_m depends on the row only through m % 4 (j of the accumulator layout).
   const bool shiftvec = !vec && slab == 0 && !bias && bn.mode == 0 && !bn.trans && msplit >= g.M &&
                         (((uintptr_t)C0) & 3) == 0;
+  const int e_base = (int)(((uintptr_t)(C0 + (int64_t)tl.m0 * ldc + tl.n0) >> 2) & 3), l3 = (int)(ldc & 3);
   float bb[4], sa[4], sb[4], sh[4], bmean[4], balpha[4], bbeta[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -497,7 +500,8 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
         for (int ni = 0; ni < C::FN; ++ni)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            img[(mi * 16 + 4 * (lane >> 4) + j) * pitch + wn * C::WTN + ni * 16 + (lane & 15)] = acc[mi0 + mi][ni][j];
+            img[(mi * 16 + 4 * (lane >> 4) + j) * pitch + wn * C::WTN + ni * 16 + (lane & 15) +
+                (shiftvec ? (e_base + j * l3) & 3 : 0)] = acc[mi0 + mi][ni][j];
     }
     __syncthreads();
     if (bn.trans) {
@@ -529,20 +533,24 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
       const int m = tl.m0 + h * BR + r;
       if (m >= g.M) break;
       if (shiftvec) {
-        float* rowp = C0 + (int64_t)m * ldc + tl.n0;
-        const float* src = img + r * pitch;
-        const int a = (int)((4u - (uint32_t)(((uintptr_t)rowp >> 2) & 3u)) & 3u);
-        const int c = a + cq;
-        if (c + 3 < C::BN && tl.n0 + c + 3 < g.N) {
-          *(float4*)(rowp + c) = make_float4(src[c], src[c + 1], src[c + 2], src[c + 3]);
+        const int e = (e_base + r * l3) & 3;  // image position p holds column p - e
+        float* rowp = C0 + (int64_t)m * ldc + tl.n0 - e;  // rowp + p: 16-B aligned for p % 4 == 0
+        const float4 w = *(const float4*)(img + r * pitch + cq);
+        const int c0 = cq - e;
+        if (c0 >= 0 && tl.n0 + c0 + 3 < g.N) {
+          *(float4*)(rowp + cq) = w;
         } else {
+          const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
           for (int u = 0; u < 4; ++u)
-            if (c + u < C::BN && tl.n0 + c + u < g.N) rowp[c + u] = src[c + u];
+            if (c0 + u >= 0 && tl.n0 + c0 + u < g.N) rowp[cq + u] = wv[u];
         }
-        if (cq == 0)
-          for (int u = 0; u < a; ++u)
-            if (tl.n0 + u < g.N) rowp[u] = src[u];
+        if (cq == 0 && e > 0) {  // the end chunk: positions BN .. BN + e - 1
+          const float4 t = *(const float4*)(img + r * pitch + C::BN);
+          const float tv[4] = {t.x, t.y, t.z, t.w};
+          for (int u = 0; u < e; ++u)
+            if (tl.n0 + C::BN - e + u < g.N) rowp[C::BN + u] = tv[u];
+        }
         continue;
       }
       const float4 w = *(const float4*)(img + r * pitch + cq);
