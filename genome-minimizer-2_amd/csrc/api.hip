@@ -386,11 +386,8 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   GemmArgs<T> g{c.t(l.sD3), H, c.t(l.A[5]), H, (int)d.G, B, H, (int)d.Gp, Bp, 0};
   launch_gemm_recon_loss<T>(g, prm + d.off[D9B], (const uint32_t*)(c.ws + l.XB), d.Gp / 32, with_grad, scal, c.t(l.dL),
                             d.Gp, c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
-  const int nblk = gemm_recon_grid_blocks<T>(g);
-  launch_reduce_to(c.f(l.losspart), nblk, 2, 2, loss + 0, c.s);
-  launch_reduce_to(c.f(l.klpart), Bp / 64, 1, 1, loss + 2, c.s);
-  if (with_grad)
-    launch_colsum(c.f(l.colpart), gemm_recon_row_tiles<T>(g), d.Gp, (int)d.G, grads + d.off[D9B], nullptr, 0, c.s);
+  launch_fwd_tail(c.f(l.losspart), gemm_recon_grid_blocks<T>(g), c.f(l.klpart), Bp / 64, loss, c.f(l.colpart),
+                  gemm_recon_row_tiles<T>(g), d.Gp, (int)d.G, with_grad ? grads + d.off[D9B] : nullptr, c.s);
 }
 
 // Backward. Every operand is read in the layout its producer wrote: weight gradients use MN-major P
@@ -586,9 +583,7 @@ int gm2_grad_norm(const gm2_dims* d, int prec, const float* params, const float*
     double* part = (double*)((char*)ws + lo.gradpart);
     float* clip = (float*)((char*)ws + lo.clip);
     launch_grad_stats(params, grads, n, scalars, part, nb, (hipStream_t)stream);
-    launch_grad_finalize(part, nb, scalars, clip, loss + 3, (hipStream_t)stream);
-    // loss[4] = norm (fp32 -> fp64) via a tiny copy kernel-free path: reuse reduce_to on clip[1]
-    launch_reduce_to(clip + 1, 1, 1, 1, loss + 4, (hipStream_t)stream);
+    launch_grad_finalize(part, nb, scalars, clip, loss + 3, (hipStream_t)stream);  // loss[3], loss[4]
   });
 }
 

@@ -184,8 +184,10 @@ void launch_colsum(const float* part, int rows, int64_t ld, int64_t n, float* ou
 // C0/C1 (row split at msplit) = sum of S split-K slabs [S][M][N] (slab stride `slab`)
 void launch_slab_sum(const float* slabs, int S, int64_t slab, int M, int N, float* C0, float* C1, int msplit,
                      int64_t ldc, hipStream_t s);
-// out[i] = sum of partial buffers in double, fixed order (loss record slots)
-void launch_reduce_to(const float* part, int n, int stride, int count, double* out, hipStream_t s);
+// forward tail: loss[0..1] = sums of the output-layer tile partials (stride 2), loss[2] = sum of
+// the KL partials; cout[c] (when non-null) = sum over `rows` of cpart[r][c]
+void launch_fwd_tail(const float* lpart, int nl, const float* kpart, int nk, double* loss, const float* cpart, int rows,
+                     int64_t ld, int64_t n, float* cout, hipStream_t s);
 
 // ---- masks.hip: consumers of the packed sampled masks ----
 void launch_count_groups(const uint8_t* bits, int64_t n, int64_t ldb, const int32_t* goff, int64_t ngroups,
@@ -222,8 +224,9 @@ void launch_adam_fused(const TensorTable& tt, const float* grads, float* params,
 // sum((g + lambda*sign(p))^2) and sum(|p|) over all params -> partials; then finalize
 void launch_grad_stats(const float* params, const float* grads, int64_t n, const float* scal, double* part,
                        int nblocks, hipStream_t s);
+// clip coefficient / norm -> clip_out[0..1]; loss_slots (when non-null) [0] = sum |theta|, [1] = norm
 void launch_grad_finalize(const double* part, int nblocks, const float* scal, float* clip_out,
-                          double* loss_l1abs, hipStream_t s);
+                          double* loss_slots, hipStream_t s);
 
 int grad_stats_blocks(int64_t n);
 

@@ -364,18 +364,36 @@ __global__ __launch_bounds__(256) void k_sigmoid_bwd(const float* __restrict__ p
   colpart[(int64_t)blockIdx.y * Gp + c] = cs;
 }
 
-__global__ __launch_bounds__(256) void k_reduce_to(const float* __restrict__ part, int n, int stride, int count,
-                                                 double* __restrict__ out) {
+// The forward's tail in one launch: block 0 = loss slots [0], [1] (sum of the output-layer tile
+// partials) and [2] (KL partials), fp64 per-thread strided sums + wave sums; blocks 1.. = the
+// output-layer bias gradient column sums in k_colsum2's order (rows = strain tiles).
+__global__ __launch_bounds__(256) void k_fwd_tail(const float* __restrict__ lpart, int nl, const float* __restrict__ kpart,
+                                                int nk, double* __restrict__ loss, const float* __restrict__ cpart,
+                                                int rows, int64_t ld, int64_t n, float* __restrict__ cout) {
   __shared__ double red[4];
-  for (int k = 0; k < count; ++k) {
-    double s = 0.0;
-    for (int i = threadIdx.x; i < n; i += 256) s += (double)part[(int64_t)i * stride + k];
-    s = wave_sum_d(s);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) out[k] = red[0] + red[1] + red[2] + red[3];
-    __syncthreads();
+  __shared__ float redf[4][64];
+  if (blockIdx.x == 0) {
+    for (int k = 0; k < 3; ++k) {
+      const float* part = k < 2 ? lpart + k : kpart;
+      const int cnt = k < 2 ? nl : nk, stride = k < 2 ? 2 : 1;
+      double s = 0.0;
+      for (int i = threadIdx.x; i < cnt; i += 256) s += (double)part[(int64_t)i * stride];
+      s = wave_sum_d(s);
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+      __syncthreads();
+      if (threadIdx.x == 0) loss[k] = red[0] + red[1] + red[2] + red[3];
+      __syncthreads();
+    }
+    return;
   }
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int64_t c = (int64_t)(blockIdx.x - 1) * 64 + cl;
+  float sum = 0.f;
+  if (c < n)
+    for (int r = rg; r < rows; r += 4) sum += cpart[(int64_t)r * ld + c];
+  redf[rg][cl] = sum;
+  __syncthreads();
+  if (rg == 0 && c < n) cout[c] = (redf[0][cl] + redf[1][cl]) + (redf[2][cl] + redf[3][cl]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -497,7 +515,10 @@ __global__ __launch_bounds__(256) void k_grad_finalize(const double* __restrict_
     if (mx > 0.f) c = fminf(mx / (norm + 1e-6f), 1.0f);
     clip[0] = c;
     clip[1] = norm;
-    if (l1abs) *l1abs = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    if (l1abs) {  // loss record slots 3 (sum |theta|) and 4 (the norm)
+      l1abs[0] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+      l1abs[1] = (double)norm;
+    }
   }
 }
 
@@ -718,7 +739,8 @@ __global__ __launch_bounds__(256) void k_bn_fwd_apply(const float* __restrict__ 
 // grad_mean = sum(do)/B, proj_scale = sum((y-mean)do)*invstd^2/B in train mode; in eval mode
 // BatchNorm is the affine map y -> (y - rm)*invstd*gamma + beta and both are 0 (no batch
 // coupling). dgamma = sum((y-mean)do)*invstd, dbeta = sum(do) from the chunk partials (fp64).
-// Per-(64-row chunk, column) sums of dx -> colpart (the pre-BN Linear bias gradient).
+// Per-(64-row chunk, column) sums of dx -> colpart (the pre-BN Linear bias gradient; summed by
+// k_colsum2 -- an in-launch last-arriver sum measured +30 us per launch on this shape).
 template <typename T>
 __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ da, const float* __restrict__ Y,
                                                     int64_t ld, const float2* __restrict__ part, int B, int H,
@@ -939,10 +961,14 @@ void launch_transpose(const T* src, int64_t lds_, int R, int Cn, T* dst, int64_t
   GM2_CHECK_LAUNCH();
 }
 
-void launch_reduce_to(const float* part, int n, int stride, int count, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_to, dim3(1), dim3(256), 0, s, part, n, stride, count, out);
+void launch_fwd_tail(const float* lpart, int nl, const float* kpart, int nk, double* loss, const float* cpart, int rows,
+                     int64_t ld, int64_t n, float* cout, hipStream_t s) {
+  const int64_t cb = cout ? (n + 63) / 64 : 0;
+  hipLaunchKernelGGL(k_fwd_tail, dim3((unsigned)(1 + cb)), dim3(256), 0, s, lpart, nl, kpart, nk, loss, cpart, rows, ld,
+                     n, cout);
   GM2_CHECK_LAUNCH();
 }
+
 
 template <typename T>
 void launch_shadow_sync(const TensorTable& tt, const float* params, hipStream_t s) {
