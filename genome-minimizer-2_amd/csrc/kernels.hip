@@ -145,17 +145,39 @@ __global__ __launch_bounds__(256) void k_bn_fwd_partial(const float* __restrict_
 }
 
 // Chan's parallel merge of per-chunk (mean, M2) -> batch mean and biased variance, in two passes
-// (mean = sum n_c mean_c / B ; M2 = sum M2_c + n_c (mean_c - mean)^2), fp64, loads unrolled
-__device__ inline void bn_merge(const float2* __restrict__ part, int B, int H, int col, double& mean, double& var) {
+// (mean = sum n_c mean_c / B ; M2 = sum M2_c + n_c (mean_c - mean)^2), fp64. Up to 32 chunks
+// (B <= 4096) the partials are loaded once, all in flight, and both passes run from registers.
+__device__ __forceinline__ void bn_merge(const float2* __restrict__ part, int B, int H, int col, double& mean, double& var) {
   const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
-  double s = 0.0;
+  double s = 0.0, mu, M2 = 0.0;
+  if (nch <= 32) {
+    // branch-free: chunks past nch re-read the last chunk with weight 0 (exact no-ops), so all 32
+    // loads of each pass are independent and in flight together
+#pragma unroll
+    for (int ch = 0; ch < 32; ++ch) {
+      const int cc = min(ch, nch - 1);
+      const double nb = (double)max(0, min(kBnRowChunk, B - ch * kBnRowChunk));
+      s += nb * (double)part[(int64_t)cc * H + col].x;
+    }
+    mu = s / (double)B;
+#pragma unroll
+    for (int ch = 0; ch < 32; ++ch) {
+      const int cc = min(ch, nch - 1);
+      const double nb = (double)max(0, min(kBnRowChunk, B - ch * kBnRowChunk));
+      const float2 p = part[(int64_t)cc * H + col];
+      const double dlt = (double)p.x - mu;
+      M2 += (ch < nch ? (double)p.y : 0.0) + nb * dlt * dlt;
+    }
+    mean = mu;
+    var = M2 / (double)B;
+    return;
+  }
 #pragma unroll 8
   for (int ch = 0; ch < nch; ++ch) {
     const double nb = (double)min(kBnRowChunk, B - ch * kBnRowChunk);
     s += nb * (double)part[(int64_t)ch * H + col].x;
   }
-  const double mu = s / (double)B;
-  double M2 = 0.0;
+  mu = s / (double)B;
 #pragma unroll 8
   for (int ch = 0; ch < nch; ++ch) {
     const double nb = (double)min(kBnRowChunk, B - ch * kBnRowChunk);
@@ -673,7 +695,7 @@ __global__ __launch_bounds__(256) void k_slab_sum(const float* __restrict__ slab
 // Then a vectorised elementwise pass over 64 rows x 256 columns (4 columns per thread).
 // ---------------------------------------------------------------------------------------------
 // forward coefficients (alpha = invstd*gamma, beta' = fma(-mean, alpha, beta)) of column `col`
-__device__ inline float2 bn_fwd_coef(const float2* __restrict__ part, int B, int H, int train,
+__device__ __forceinline__ float2 bn_fwd_coef(const float2* __restrict__ part, int B, int H, int train,
                                      const float* __restrict__ gamma, const float* __restrict__ beta, float* rmean,
                                      float* rvar, float* save, int col, bool own) {
   float invstd, meanf;
@@ -711,25 +733,27 @@ __global__ __launch_bounds__(256) void k_bn_fwd_apply(const float* __restrict__ 
                                                     float* rmean, float* rvar, float* save, T* __restrict__ A) {
   __shared__ float2 cf[256];
   const int c0 = blockIdx.x * 256;
+  const int cl = (threadIdx.x & 63) * 4, rg = threadIdx.x >> 6;
+  const int c = c0 + cl;
+  const int r0 = blockIdx.y * 64;
   if (c0 + (int)threadIdx.x < H)
     cf[threadIdx.x] = bn_fwd_coef(part, B, H, train, gamma, beta, rmean, rvar, save, c0 + threadIdx.x,
                                   blockIdx.y == 0);
   __syncthreads();
-  const int cl = (threadIdx.x & 63) * 4, rg = threadIdx.x >> 6;
-  const int c = c0 + cl;
   if (c >= H) return;  // H % 128 == 0: the last block may cover only 128 of its 256 columns
   const float2 k0 = cf[cl], k1 = cf[cl + 1], k2 = cf[cl + 2], k3 = cf[cl + 3];
-  const int r0 = blockIdx.y * 64;
-#pragma unroll 4
-  for (int rl = rg; rl < 64; rl += 4) {
-    const int r = r0 + rl;
+  float4 y[16];  // all 16 rows of this thread in flight at once (rows >= B re-read row B-1, unused)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) y[i] = *(const float4*)(Y + (int64_t)min(r0 + rg + 4 * i, B - 1) * ld + c);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int r = r0 + rg + 4 * i;
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
     if (r < B) {
-      const float4 y = *(const float4*)(Y + (int64_t)r * ld + c);
-      o.x = fmaxf(fmaf(y.x, k0.x, k0.y), 0.f);
-      o.y = fmaxf(fmaf(y.y, k1.x, k1.y), 0.f);
-      o.z = fmaxf(fmaf(y.z, k2.x, k2.y), 0.f);
-      o.w = fmaxf(fmaf(y.w, k3.x, k3.y), 0.f);
+      o.x = fmaxf(fmaf(y[i].x, k0.x, k0.y), 0.f);
+      o.y = fmaxf(fmaf(y[i].y, k1.x, k1.y), 0.f);
+      o.z = fmaxf(fmaf(y[i].z, k2.x, k2.y), 0.f);
+      o.w = fmaxf(fmaf(y[i].w, k3.x, k3.y), 0.f);
     }
     store4<T>(A + (int64_t)r * ld + c, o.x, o.y, o.z, o.w);
   }
@@ -752,16 +776,29 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
   __shared__ float4 red[4][64];
   float* cf = (float*)cf4;
   const int c0 = blockIdx.x * 256;
+  const int cg = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = c0 + cg * 4;
+  const int r0 = blockIdx.y * 64;
+  const bool ok = c < H;
   {
     const int t = threadIdx.x, col = c0 + t;
     if (col < H) {
       double s1 = 0.0, s2 = 0.0;
       const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
+      if (nch <= 32) {  // every chunk partial in flight at once, summed in chunk order
+#pragma unroll
+        for (int ch = 0; ch < 32; ++ch) {
+          const float2 p = part[(int64_t)min(ch, nch - 1) * H + col];
+          s1 += ch < nch ? (double)p.x : 0.0;
+          s2 += ch < nch ? (double)p.y : 0.0;
+        }
+      } else {
 #pragma unroll 8
-      for (int ch = 0; ch < nch; ++ch) {
-        const float2 p = part[(int64_t)ch * H + col];
-        s1 += p.x;
-        s2 += p.y;
+        for (int ch = 0; ch < nch; ++ch) {
+          const float2 p = part[(int64_t)ch * H + col];
+          s1 += p.x;
+          s2 += p.y;
+        }
       }
       const float mean = save[col], invstd = save[H + col];
       const float alpha = invstd * gamma[col];
@@ -777,21 +814,24 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
     }
   }
   __syncthreads();
-  const int cg = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = c0 + cg * 4;
-  const int r0 = blockIdx.y * 64;
-  const bool ok = c < H;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (ok) {
+    // all 16 rows of dA and Y of this thread in flight at once
+    float4 av[16], yv[16];  // (rows >= B re-read row B-1, unused)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t o = (int64_t)min(r0 + rg + 4 * i, B - 1) * ld + c;
+      av[i] = *(const float4*)(da + o);
+      yv[i] = *(const float4*)(Y + o);
+    }
     const float4 mean = cf4[0][cg], al = cf4[1][cg], be = cf4[2][cg], gm = cf4[3][cg], ps = cf4[4][cg];
-#pragma unroll 4
-    for (int rl = rg; rl < 64; rl += 4) {
-      const int r = r0 + rl;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = r0 + rg + 4 * i;
       float4 dx = make_float4(0.f, 0.f, 0.f, 0.f);
       if (r < B) {
-        const int64_t o = (int64_t)r * ld + c;
-        const float4 a = *(const float4*)(da + o);
-        const float4 y = *(const float4*)(Y + o);
+        const float4 a = av[i];
+        const float4 y = yv[i];
         const float d0 = fmaf(y.x, al.x, be.x) > 0.f ? a.x : 0.f;
         const float d1 = fmaf(y.y, al.y, be.y) > 0.f ? a.y : 0.f;
         const float d2 = fmaf(y.z, al.z, be.z) > 0.f ? a.z : 0.f;
