@@ -90,21 +90,24 @@ __global__ __launch_bounds__(256) void k_bn_fwd_partial(const float* __restrict_
   const int nrows = min(kBnRowChunk, B - r0);
   const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
   const float4 b = bias ? *(const float4*)(bias + col) : zero;
+  // rows past nrows re-read the chunk's last row (never used): branch-free loads, and up to four
+  // slabs' loads in flight together
   float4 v[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int rl = rg + 16 * i;
-    v[i] = rl < nrows ? *(const float4*)(slabs + (int64_t)(r0 + rl) * ld + col) : zero;
-  }
-  for (int sl = 1; sl < S; ++sl) {
-    float4 w[8];
+  for (int i = 0; i < 8; ++i) v[i] = *(const float4*)(slabs + (int64_t)(r0 + min(rg + 16 * i, nrows - 1)) * ld + col);
+  for (int sl = 1; sl < S; sl += 3) {
+    float4 w[3][8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int rl = rg + 16 * i;
-      w[i] = rl < nrows ? *(const float4*)(slabs + (int64_t)sl * slab + (int64_t)(r0 + rl) * ld + col) : zero;
-    }
+    for (int u = 0; u < 3; ++u)
+      if (sl + u < S)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = f4add(v[i], w[i]);
+        for (int i = 0; i < 8; ++i)
+          w[u][i] = *(const float4*)(slabs + (int64_t)(sl + u) * slab + (int64_t)(r0 + min(rg + 16 * i, nrows - 1)) * ld + col);
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (sl + u < S)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = f4add(v[i], w[u][i]);
   }
   float4 sum = zero;
 #pragma unroll
@@ -209,23 +212,28 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict_
   const float4 al = make_float4(invstd.x * gm.x, invstd.y * gm.y, invstd.z * gm.z, invstd.w * gm.w);
   const float4 bp = make_float4(fmaf(-mean.x, al.x, bt.x), fmaf(-mean.y, al.y, bt.y), fmaf(-mean.z, al.z, bt.z),
                                 fmaf(-mean.w, al.w, bt.w));
+  // rows past nrows re-read the chunk's last row (never used): branch-free loads, and up to four
+  // slabs' loads in flight together
   float4 da[8], y[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int rl = rg + 16 * i;
-    const int64_t o = (int64_t)(r0 + rl) * ld + col;
-    da[i] = rl < nrows ? *(const float4*)(dslabs + o) : zero;
-    y[i] = rl < nrows ? *(const float4*)(Y + o) : zero;
+    const int64_t o = (int64_t)(r0 + min(rg + 16 * i, nrows - 1)) * ld + col;
+    da[i] = *(const float4*)(dslabs + o);
+    y[i] = *(const float4*)(Y + o);
   }
-  for (int sl = 1; sl < S; ++sl) {
-    float4 w[8];
+  for (int sl = 1; sl < S; sl += 3) {
+    float4 w[3][8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int rl = rg + 16 * i;
-      w[i] = rl < nrows ? *(const float4*)(dslabs + (int64_t)sl * slab + (int64_t)(r0 + rl) * ld + col) : zero;
-    }
+    for (int u = 0; u < 3; ++u)
+      if (sl + u < S)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) da[i] = f4add(da[i], w[i]);
+        for (int i = 0; i < 8; ++i)
+          w[u][i] = *(const float4*)(dslabs + (int64_t)(sl + u) * slab + (int64_t)(r0 + min(rg + 16 * i, nrows - 1)) * ld + col);
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (sl + u < S)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) da[i] = f4add(da[i], w[u][i]);
   }
   float4 s1 = zero, s2 = zero;
 #pragma unroll
@@ -669,11 +677,29 @@ __global__ __launch_bounds__(256) void k_slab_sum(const float* __restrict__ slab
                                                 float* __restrict__ C0, float* __restrict__ C1, int msplit,
                                                 int64_t ldc) {
   const int64_t total = (int64_t)M * N;
+  // rows of C are 16-B aligned and N % 4 == 0: the 4 elements of a thread are one row's float4
+  const bool vec = (N & 3) == 0 && (ldc & 3) == 0 && ((((uintptr_t)C0) | ((uintptr_t)C1)) & 15) == 0;
   for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < total; i += (int64_t)gridDim.x * 1024) {
     float4 a = *(const float4*)(slabs + i);
-    for (int s = 1; s < S; ++s) {
-      const float4 b = *(const float4*)(slabs + s * slab + i);
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    if (S <= 8) {  // every slab's load in flight, summed in slab order
+      float4 b[7];
+#pragma unroll
+      for (int s = 1; s < 8; ++s)
+        if (s < S) b[s - 1] = *(const float4*)(slabs + s * slab + i);
+#pragma unroll
+      for (int s = 1; s < 8; ++s)
+        if (s < S) { a.x += b[s - 1].x; a.y += b[s - 1].y; a.z += b[s - 1].z; a.w += b[s - 1].w; }
+    } else {
+      for (int s = 1; s < S; ++s) {
+        const float4 b = *(const float4*)(slabs + s * slab + i);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+    }
+    if (vec && i + 3 < total) {
+      const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+      float* dst = m < msplit ? C0 + (int64_t)m * ldc + n : C1 + (int64_t)(m - msplit) * ldc + n;
+      *(float4*)dst = a;
+      continue;
     }
     const float e[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
@@ -885,8 +911,17 @@ __global__ __launch_bounds__(256) void k_colsum2(const float* __restrict__ part,
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int64_t c = (int64_t)blockIdx.x * 64 + cl;
   float s = 0.f;
-  if (c < n)
-    for (int r = rg; r < rows; r += 4) s += part[(int64_t)r * ld + c];
+  if (c < n) {
+    int r = rg;
+    for (; r + 60 < rows; r += 64) {  // 16 rows' loads in flight, summed in row order
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = part[(int64_t)(r + 4 * u) * ld + c];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    for (; r < rows; r += 4) s += part[(int64_t)r * ld + c];
+  }
   red[rg][cl] = s;
   __syncthreads();
   if (rg == 0 && c < n) {
