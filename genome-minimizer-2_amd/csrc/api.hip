@@ -87,6 +87,8 @@ struct Layout {
   int64_t X, XB, Y[6], A[6], save[6], HD, Z, dL, slabs, slab_cap, side_slabs, side_cap, dY[6], DA, dH;
   int64_t AT5, dYT0;  // transposed A5 / dY0 [H][Bm]: K-major operands of the dW9 / dWe0 GEMMs
   int64_t bnpart, colpart, colpart_cap, losspart, losspart_cap, klpart, gradpart, clip, scal0, total;
+  int64_t colbwd, colbwd_cap;  // per-layer bias-gradient partials of the backward (summed on the side stream)
+  int64_t nahdr, nasq;         // norm-ahead header int[4] and per-tile sums of squares (NormAhead)
 };
 
 Layout make_layout(const gm2_dims* gd, int prec) {
@@ -139,6 +141,10 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.losspart = take(o.losspart_cap * 4);
   o.klpart = take((Bm / 64) * 4);
   o.gradpart = take(2048 * 2 * 8);
+  o.colbwd_cap = (Bm / 64) * std::max<int64_t>(H, 2 * d.L);
+  o.colbwd = take(7 * o.colbwd_cap * 4);
+  o.nahdr = take(16);
+  o.nasq = take(2 * (d.Gp / kTile + 1) * (H / kTile + 1) * 8);
   o.clip = take(64);
   o.scal0 = take(GM2_NUM_SCALARS * 4);
   o.total = cur;
@@ -264,6 +270,28 @@ void gemm_to(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64
   launch_slab_sum(c.f(c.slab_off), S, slab, M, N, C0, C1, C1 ? msplit : M, ldc, c.s);
 }
 
+// The two big weight-gradient GEMMs of the backward (output layer dW9, stored transposed; input
+// layer dWe0). When both are one K pass (`direct`) their epilogues also write per-tile sums of
+// squares, [sq9 | sq0] in the norm-ahead area, so gm2_grad_norm need not re-read 2 x H x G floats.
+template <typename T>
+struct BigGrads {
+  GemmArgs<T> g9, g0;
+  bool direct;
+  int n9, n0;
+};
+template <typename T>
+BigGrads<T> big_grads(const Ctx<T>& c, int Bp) {
+  const Layout& l = c.lo;
+  const int H = (int)c.d.H, G = (int)c.d.G, Gp = (int)c.d.Gp;
+  BigGrads<T> r{{c.t(l.AT5), Bp, c.t(l.dL), Gp, H, G, Bp, H, Gp, 0, 1, 0},
+                {c.t(l.dYT0), Bp, c.t(l.X), Gp, H, G, Bp, H, Gp, 0, 1, 0}, false, 0, 0};
+  r.direct = plan_gemm<T>(r.g9).splits == 1 && plan_gemm<T>(r.g0).splits == 1;
+  r.n9 = gemm_tiles<T>(r.g9);
+  r.n0 = gemm_tiles<T>(r.g0);
+  if ((int64_t)(r.n9 + r.n0) > 2 * (c.d.Gp / kTile + 1) * (c.d.H / kTile + 1)) r.direct = false;
+  return r;
+}
+
 // Pre-BatchNorm Linear: Y = in . W^T + bias (fp32 [Bp][H]) and, when `stats`, the per-128-row
 // chunk (mean, M2) partials of Y -> part. One launch when the GEMM plan is a single pass of 128-row
 // tiles (statistics in the store epilogue); otherwise split-K slabs + k_bn_fwd_partial.
@@ -340,7 +368,7 @@ TensorTable make_table(const Ctx<T>& c, int kind = 0) {
 template <typename T>
 void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, int train, int with_grad,
              const float* scal, double* loss, float* grads, float* probs = nullptr, int64_t ld_probs = 0,
-             int* counts = nullptr, float thr = 0.5f) {
+             int* counts = nullptr, float thr = 0.5f, bool norm_hdr = false) {
   const Dims& d = c.d;
   const Layout& l = c.lo;
   const int B = (int)b->n;
@@ -386,8 +414,15 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   GemmArgs<T> g{c.t(l.sD3), H, c.t(l.A[5]), H, (int)d.G, B, H, (int)d.Gp, Bp, 0};
   launch_gemm_recon_loss<T>(g, prm + d.off[D9B], (const uint32_t*)(c.ws + l.XB), d.Gp / 32, with_grad, scal, c.t(l.dL),
                             d.Gp, c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
+  int na_ok = 0, na_n = 0;
+  if (norm_hdr) {  // the training call: record whether its backward takes the clip statistics
+    const BigGrads<T> bg = big_grads<T>(c, Bp);
+    na_ok = bg.direct ? 1 : 0;
+    na_n = bg.n9 + bg.n0;
+  }
   launch_fwd_tail(c.f(l.losspart), gemm_recon_grid_blocks<T>(g), c.f(l.klpart), Bp / 64, loss, c.f(l.colpart),
-                  gemm_recon_row_tiles<T>(g), d.Gp, (int)d.G, with_grad ? grads + d.off[D9B] : nullptr, c.s);
+                  gemm_recon_row_tiles<T>(g), d.Gp, (int)d.G, with_grad ? grads + d.off[D9B] : nullptr,
+                  norm_hdr ? (int*)(c.ws + l.nahdr) : nullptr, na_ok, na_n, c.s);
 }
 
 // Backward. Every operand is read in the layout its producer wrote: weight gradients use MN-major P
@@ -416,12 +451,14 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   // 256x256 tile is LDS-read bound with two). Plans with split-K keep the both-MN-major form.
   // (Forking it last instead, beside the input-layer dWe0 GEMM, measured the same step time on one
   // GPU; first keeps gradient bucket 0 early for the data-parallel exchange.)
+  const BigGrads<T> bg = big_grads<T>(c, Bp);
+  double* nasq = (double*)(c.ws + l.nasq);
   fork();
   {
-    GemmArgs<T> g9{c.t(l.AT5), Bp, c.t(l.dL), Gp, H, G, Bp, H, Gp, 0, 1, 0};
+    const GemmArgs<T>& g9 = bg.g9;
     if (plan_gemm<T>(g9).splits == 1) {
       launch_transpose<T>(c.t(l.A[5]), H, Bp, H, c.t(l.AT5), Bp, w.s);
-      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, w.s);
+      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, w.s, bg.direct ? nasq : nullptr);
     } else {
       gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
     }
@@ -453,29 +490,33 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     if (!have_part)
       launch_bn_bwd_partial(c.f(c.slab_off), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
                             prm + d.off[kBlk[i][3]], B, H, c.f(l.bnpart), sum ? c.f(l.DA) : nullptr, c.s);
+    // bias-gradient partials go to this layer's own slice: their column sum runs on the side stream
+    float* colp = c.f(l.colbwd) + (int64_t)i * l.colbwd_cap;
     launch_bn_bwd_apply<T>(sum ? c.f(l.DA) : c.f(c.slab_off), c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train,
                            c.f(l.save[i]), prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]], gr + d.off[kBlk[i][2]],
-                           gr + d.off[kBlk[i][3]], c.t(l.dY[i]), c.f(l.colpart), c.s);
-    launch_colsum(c.f(l.colpart), Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, c.s);
+                           gr + d.off[kBlk[i][3]], c.t(l.dY[i]), colp, c.s);
+    fork();
+    launch_colsum(colp, Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, w.s);
     const T* dY = c.t(l.dY[i]);
     if (i == 0) {  // input layer: weight gradient only (on the main stream: nothing left to overlap)
       // dWe0[h][g] = sum_b dY0^T[h][b] X[b][g]: dY0^T (K-major copy) x X (MN-major)
       launch_transpose<T>(dY, H, Bp, H, c.t(l.dYT0), Bp, c.s);
       if (sr) order(sr, w.s, c.s);  // join: every hidden-layer weight gradient is final
       HIP_OK(hipEventRecord(be->ev[1], c.s));
-      gemm_to<T>(c, c.t(l.dYT0), Bp, H, c.t(l.X), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0);
+      if (!bg.direct || !launch_gemm_sq<T>(bg.g0, gr + d.off[E0W], G, nasq + bg.n9, c.s))
+        gemm_to<T>(c, c.t(l.dYT0), Bp, H, c.t(l.X), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0);
       HIP_OK(hipEventRecord(be->ev[2], c.s));
       be->recorded = true;
       break;
     }
-    fork();
     if (i == 3) {  // decoder input layer, then back through the reparameterisation and the heads
       gemm_to<T>(w, dY, H, H, c.t(l.Z), Lr, Lr, H, L, Bp, gr + d.off[D0W], nullptr, 0, L, 0, 0);
       S = gemm_to_slabs<T>(c, dY, H, Bp, c.t(l.sD0), Lr, Lr, B, L, H, L, 1, 0);
+      float* colh = c.f(l.colbwd) + 6 * l.colbwd_cap;
       launch_reparam_bwd<T>(c.f(c.slab_off), S, (int64_t)Bp * L, L, c.f(l.HD), b->eps, scal, B, Bp, L, c.t(l.dH),
-                            L2r, dmu_ext, dlv_ext, c.f(l.colpart), c.s);
-      launch_colsum(c.f(l.colpart), Bp / 64, 2 * L, 2 * L, gr + d.off[MUB], gr + d.off[LVB], L, c.s);
+                            L2r, dmu_ext, dlv_ext, colh, c.s);
       fork();
+      launch_colsum(colh, Bp / 64, 2 * L, 2 * L, gr + d.off[MUB], gr + d.off[LVB], L, w.s);
       gemm_to<T>(w, c.t(l.dH), L2r, L2r, c.t(l.A[2]), H, H, 2 * L, H, Bp, gr + d.off[MUW], gr + d.off[LVW], L, H, 0,
                  0);
       S = dx_pre_bn(c.t(l.dH), L2r, c.t(l.sHD), H, (int)d.K2L, 2);
@@ -516,7 +557,7 @@ template <typename T>
 void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr, float* bn, const float* scal,
                double* loss, void* ws, void* st) {
   Ctx<T> c(lo, ws, st);
-  forward<T>(c, b, prm, bn, 1, 1, scal, loss, gr);
+  forward<T>(c, b, prm, bn, 1, 1, scal, loss, gr, nullptr, 0, nullptr, 0.5f, true);
   backward<T>(c, b, prm, gr, scal);
 }
 
@@ -582,8 +623,12 @@ int gm2_grad_norm(const gm2_dims* d, int prec, const float* params, const float*
     const int nb = grad_stats_blocks(n);
     double* part = (double*)((char*)ws + lo.gradpart);
     float* clip = (float*)((char*)ws + lo.clip);
-    launch_grad_stats(params, grads, n, scalars, part, nb, (hipStream_t)stream);
-    launch_grad_finalize(part, nb, scalars, clip, loss + 3, (hipStream_t)stream);  // loss[3], loss[4]
+    NormAhead na;
+    na.hdr = (const int*)((char*)ws + lo.nahdr);
+    na.sq = (const double*)((char*)ws + lo.nasq);
+    na.lo0 = lo.d.off[E0W], na.hi0 = lo.d.off[E0B], na.lo9 = lo.d.off[D9W], na.hi9 = lo.d.off[D9B];
+    launch_grad_stats(params, grads, n, scalars, part, nb, na, (hipStream_t)stream);
+    launch_grad_finalize(part, nb, scalars, clip, loss + 3, na, (hipStream_t)stream);  // loss[3], loss[4]
   });
 }
 
@@ -835,6 +880,7 @@ int gm2_set_option(int key, int value) {
         break;
       case GM2_OPT_SMALL_SPLIT: set_small_split(value); break;
       case GM2_OPT_BN_EPILOGUE: set_bn_epilogue(value); break;
+      case GM2_OPT_SMALL_WAVES: set_small_waves(value); break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });
@@ -848,6 +894,7 @@ int gm2_get_option(int key, int* value) {
       case GM2_OPT_RECON_TILE: *value = get_recon_tile(); break;
       case GM2_OPT_SMALL_SPLIT: *value = get_small_split(); break;
       case GM2_OPT_BN_EPILOGUE: *value = get_bn_epilogue(); break;
+      case GM2_OPT_SMALL_WAVES: *value = get_small_waves(); break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });

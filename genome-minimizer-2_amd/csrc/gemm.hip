@@ -62,6 +62,9 @@ using Small = Cfg<128, 128, 2, 2>;
 // ~0.2 us of MFMA each, against ~1 us from global_load_lds issue to landing): a 4-stage ring keeps
 // three K-steps in flight instead of one.
 using SmallDeep = Cfg<128, 128, 2, 2, 4>;
+// The same tile with 8 waves (2x4, 64x32 each): two waves per SIMD, so one's LDS reads and waits
+// hide behind the other's MFMAs (GM2_OPT_SMALL_WAVES = 8)
+using SmallDeep8 = Cfg<128, 128, 2, 4, 4>;
 
 struct TileXY {
   int m0, n0, split, t;
@@ -439,6 +442,10 @@ __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_
 //           (sum do, sum (y - mean) do).
 // The store loop visits 4 fixed columns per thread, so the sums stay in registers and the threads
 // of a column are combined through LDS once at the end.
+__device__ __forceinline__ double sq4(float a, float b, float c, float d) {
+  return ((double)a * a + (double)b * b) + ((double)c * c + (double)d * d);
+}
+
 template <class C, typename T, bool AK, bool BK, bool PP>
 __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __restrict__ C0, float* __restrict__ C1,
                                                     int msplit, int64_t ldc, int64_t slab,
@@ -480,6 +487,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
                         (((uintptr_t)C0) & 3) == 0;
   const int e_base = (int)(((uintptr_t)(C0 + (int64_t)tl.m0 * ldc + tl.n0) >> 2) & 3), l3 = (int)(ldc & 3);
   float bb[4], sa[4], sb[4], sh[4], bmean[4], balpha[4], bbeta[4];
+  double sqa = 0.0;  // sum of squares of the stored values (bn.sq), fp64 like the re-reading pass
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     bb[u] = (bias && n + u < g.N) ? bias[n + u] : 0.f;
@@ -516,10 +524,14 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
         float* dst = C0 + (int64_t)nn * ldc + m;
         if (vec && m + 3 < g.M) {
           *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+          sqa += sq4(v[0], v[1], v[2], v[3]);
         } else {
 #pragma unroll
           for (int u = 0; u < 4; ++u)
-            if (m + u < g.M) dst[u] = v[u];
+            if (m + u < g.M) {
+              dst[u] = v[u];
+              sqa += (double)v[u] * v[u];
+            }
         }
       }
       __syncthreads();
@@ -539,17 +551,24 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
         const int c0 = cq - e;
         if (c0 >= 0 && tl.n0 + c0 + 3 < g.N) {
           *(float4*)(rowp + cq) = w;
+          sqa += sq4(w.x, w.y, w.z, w.w);
         } else {
           const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
           for (int u = 0; u < 4; ++u)
-            if (c0 + u >= 0 && tl.n0 + c0 + u < g.N) rowp[cq + u] = wv[u];
+            if (c0 + u >= 0 && tl.n0 + c0 + u < g.N) {
+              rowp[cq + u] = wv[u];
+              sqa += (double)wv[u] * wv[u];
+            }
         }
         if (cq == 0 && e > 0) {  // the end chunk: positions BN .. BN + e - 1
           const float4 t = *(const float4*)(img + r * pitch + C::BN);
           const float tv[4] = {t.x, t.y, t.z, t.w};
           for (int u = 0; u < e; ++u)
-            if (tl.n0 + C::BN - e + u < g.N) rowp[C::BN + u] = tv[u];
+            if (tl.n0 + C::BN - e + u < g.N) {
+              rowp[C::BN + u] = tv[u];
+              sqa += (double)tv[u] * tv[u];
+            }
         }
         continue;
       }
@@ -558,10 +577,14 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
       float* dst = (m < msplit ? Cz + (int64_t)m * ldc : C1 + (int64_t)(m - msplit) * ldc) + n;
       if (vec && n + 3 < g.N) {
         *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+        sqa += sq4(v[0], v[1], v[2], v[3]);
       } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if (n + u < g.N) dst[u] = v[u];
+          if (n + u < g.N) {
+            dst[u] = v[u];
+            sqa += (double)v[u] * v[u];
+          }
       }
       if (bn.mode == 1) {
 #pragma unroll
@@ -608,6 +631,19 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
           o[u] = make_float2(av[u], qv[u]);
         }
       }
+    }
+  }
+  if (bn.sq) {  // (one K pass: checked on the host) fixed-order block sum, one fp64 per tile
+    double* red = (double*)smem;
+    const double w = wave_sum_d(sqa);
+    __syncthreads();
+    if (lane == 0) red[wid] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k < C::NT / 64; ++k) t += red[k];
+      bn.sq[(tl.m0 / C::BM) * (g.Np / C::BN) + tl.n0 / C::BN] = t;
     }
   }
 #ifdef GM2_STAMPS
@@ -1085,6 +1121,14 @@ static bool pp_enabled() { return pp_flag().load(std::memory_order_relaxed) != 0
 void set_gemm_pp(int on) { pp_flag().store(on ? 1 : 0, std::memory_order_relaxed); }
 int get_gemm_pp() { return pp_flag().load(std::memory_order_relaxed); }
 
+// waves per block of the 128x128 fp32-store GEMM tiles (GM2_OPT_SMALL_WAVES: 4 or 8)
+static std::atomic<int>& small_waves_flag() {
+  static std::atomic<int> v{8};  // 8: step 3.52 -> 3.46 ms (profiles/r02_ab_small_waves.txt)
+  return v;
+}
+void set_small_waves(int w) { small_waves_flag().store(w == 8 ? 8 : 4, std::memory_order_relaxed); }
+int get_small_waves() { return small_waves_flag().load(std::memory_order_relaxed); }
+
 // hipFuncAttributeMaxDynamicSharedMemorySize is per device: remember (device, kernel) pairs
 static void ensure_lds_attr(const void* fn, int bytes) {
   static std::mutex mu;
@@ -1144,20 +1188,49 @@ int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
     return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
   }
   check_gemm(g, 128);
+  if (small_waves_flag().load(std::memory_order_relaxed) == 8)
+    return store_impl<SmallDeep8, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
   return store_impl<SmallDeep, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
 }
 
 template <typename T>
-bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s) {
+int gemm_tiles(const GemmArgs<T>& g) {
+  return use_big(g) ? (g.Mp / Big::BM) * (g.Np / Big::BN) : (g.Mp / SmallDeep::BM) * (g.Np / SmallDeep::BN);
+}
+
+template <typename T>
+bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s) {
   if (plan_gemm(g).splits != 1) return false;
   StoreEpi ep;
-  ep.trans = 1;
+  ep.sq = sq;
   if (use_big(g)) {
     check_gemm(g, 256);
     store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
   } else {
     check_gemm(g, 128);
-    store_impl<SmallDeep, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
+    if (small_waves_flag().load(std::memory_order_relaxed) == 8)
+      store_impl<SmallDeep8, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
+    else
+      store_impl<SmallDeep, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
+  }
+  return true;
+}
+
+template <typename T>
+bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, double* sq) {
+  if (plan_gemm(g).splits != 1) return false;
+  StoreEpi ep;
+  ep.trans = 1;
+  ep.sq = sq;
+  if (use_big(g)) {
+    check_gemm(g, 256);
+    store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
+  } else {
+    check_gemm(g, 128);
+    if (small_waves_flag().load(std::memory_order_relaxed) == 8)
+      store_impl<SmallDeep8, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
+    else
+      store_impl<SmallDeep, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
   }
   return true;
 }
@@ -1178,7 +1251,10 @@ bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bi
   const GemmPlan p = plan_gemm(g);
   if (p.tile != 128 || p.splits != 1 || (bn.mode && (g.N % 4 || bn.ldy % 4))) return false;
   check_gemm(g, 128);
-  store_impl<SmallDeep, T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s);
+  if (small_waves_flag().load(std::memory_order_relaxed) == 8)
+    store_impl<SmallDeep8, T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s);
+  else
+    store_impl<SmallDeep, T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s);
   return true;
 }
 
@@ -1274,7 +1350,9 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
 }
 
 #define GM2_INST(T)                                                                                              \
-  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t);                        \
+  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t, double*);                \
+  template bool launch_gemm_sq<T>(const GemmArgs<T>&, float*, int64_t, double*, hipStream_t);                    \
+  template int gemm_tiles<T>(const GemmArgs<T>&);                        \
   template bool launch_gemm_bn<T>(const GemmArgs<T>&, float*, int64_t, const float*, const StoreEpi&, hipStream_t);   \
   template int launch_gemm_store<T>(const GemmArgs<T>&, int, float*, float*, int, int64_t, int64_t, const float*, \
                                     hipStream_t);                                                                \

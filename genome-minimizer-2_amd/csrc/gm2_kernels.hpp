@@ -47,6 +47,7 @@ enum Scal {
   kScalBeta2 = 7,       // beta2       (exp_avg_sq.mul_(beta2).addcmul_(g, g, value=1 - beta2))
   kScalOneMinusB2 = 8,
   kScalAdamEps = 9,
+  kScalNormAhead = 10,  // != 0: grads are as the last gm2_train_fwd_bwd wrote them (gm2.h GM2_S_NORM_AHEAD)
   kNumScal = 16
 };
 
@@ -90,6 +91,10 @@ struct StoreEpi {
   const float* beta = nullptr;
   int H = 0;
   int trans = 0;  // store C^T: C0[n * ldc + m] (no bias, no statistics, one K pass)
+  // one K pass only: sq[tile] = sum of the squares of the values the tile stored (fp64), tile =
+  // (m0 / BM) * (Np / BN) + n0 / BN -- the clip-norm statistics of a weight gradient taken as it is
+  // written (gm2_grad_norm with GM2_S_NORM_AHEAD)
+  double* sq = nullptr;
 };
 // GEMM + BatchNorm statistics of its output in one launch when the plan allows (one K pass of
 // 128-row tiles); returns false (nothing launched) otherwise
@@ -97,7 +102,14 @@ template <typename T>
 bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const StoreEpi& bn, hipStream_t s);
 // C^T = (P . Q^T)^T into C [N][ldc] in one launch when the plan is one K pass; false otherwise
 template <typename T>
-bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s);
+bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, double* sq = nullptr);
+// C = P . Q^T in one K pass with the per-tile sum of squares of C into sq (see StoreEpi::sq);
+// false (nothing launched) when the plan splits K
+template <typename T>
+bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s);
+// tiles of a one-pass launch of g (the sq entries it writes)
+template <typename T>
+int gemm_tiles(const GemmArgs<T>& g);
 void set_bn_epilogue(int on);
 int get_bn_epilogue();
 // splits < 0: use plan_gemm's split-K factor. Returns the number of slabs written.
@@ -115,6 +127,8 @@ void set_recon_tile(int t);
 int get_recon_tile();
 void set_small_split(int s);
 int get_small_split();
+void set_small_waves(int w);
+int get_small_waves();
 struct GemmPlan {
   int tile, splits;
 };
@@ -186,8 +200,9 @@ void launch_slab_sum(const float* slabs, int S, int64_t slab, int M, int N, floa
                      int64_t ldc, hipStream_t s);
 // forward tail: loss[0..1] = sums of the output-layer tile partials (stride 2), loss[2] = sum of
 // the KL partials; cout[c] (when non-null) = sum over `rows` of cpart[r][c]
+// hdr (when non-null) <- {hv0, hv1}: the norm-ahead header of the training call (NormAhead)
 void launch_fwd_tail(const float* lpart, int nl, const float* kpart, int nk, double* loss, const float* cpart, int rows,
-                     int64_t ld, int64_t n, float* cout, hipStream_t s);
+                     int64_t ld, int64_t n, float* cout, int* hdr, int hv0, int hv1, hipStream_t s);
 
 // ---- masks.hip: consumers of the packed sampled masks ----
 void launch_count_groups(const uint8_t* bits, int64_t n, int64_t ldb, const int32_t* goff, int64_t ngroups,
@@ -222,11 +237,20 @@ template <typename T>
 void launch_adam_fused(const TensorTable& tt, const float* grads, float* params, float* m, float* v, const float* scal,
                        const float* clip, hipStream_t s);
 // sum((g + lambda*sign(p))^2) and sum(|p|) over all params -> partials; then finalize
+// Clip-norm statistics taken in the GEMM epilogues of the training call (StoreEpi::sq): hdr[0] = 1
+// when both big weight gradients (input layer [lo0, hi0), output layer [lo9, hi9) of the flat
+// buffer) were stored in one pass with their per-tile sums of squares in sq[0 .. hdr[1]). Used
+// instead of re-reading those ranges when scal[kScalNormAhead] != 0 and there is no L1 term.
+struct NormAhead {
+  const int* hdr = nullptr;
+  const double* sq = nullptr;
+  int64_t lo0 = 0, hi0 = 0, lo9 = 0, hi9 = 0;
+};
 void launch_grad_stats(const float* params, const float* grads, int64_t n, const float* scal, double* part,
-                       int nblocks, hipStream_t s);
+                       int nblocks, const NormAhead& na, hipStream_t s);
 // clip coefficient / norm -> clip_out[0..1]; loss_slots (when non-null) [0] = sum |theta|, [1] = norm
 void launch_grad_finalize(const double* part, int nblocks, const float* scal, float* clip_out,
-                          double* loss_slots, hipStream_t s);
+                          double* loss_slots, const NormAhead& na, hipStream_t s);
 
 int grad_stats_blocks(int64_t n);
 

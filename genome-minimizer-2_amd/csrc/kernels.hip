@@ -13,14 +13,24 @@ constexpr double kBnEps = 1e-5;       // nn.BatchNorm1d default eps
 constexpr double kBnMomentum = 0.1;   // nn.BatchNorm1d default momentum
 
 // ---------------------------------------------------------------------------------------------
-// gather: X[r][c] = data[rows[r]][c] (u8 0/1 -> T) and the row-major target bits of the loss
-// epilogue (bit c%32 of word c/32 of row r). A wave streams one strain row at a time, 16 bytes per
-// lane = 1 KiB of contiguous columns per load instruction (2 KiB / 4 KiB per store), four rows
-// per wave in flight; a block = 4 waves x 4 rows x 1024 columns. Each lane's 16 columns give a
-// 16-bit piece of one target word, the even lane of each pair writes the word. Rows and X stream
-// (non-temporal loads / stores: read once here, X re-read from HBM by the input-layer GEMMs).
+// gather: X[r][c] = data[rows[r]][c] (u8, nonzero -> 1, as T) and the row-major target bits of the
+// loss epilogue (bit c%32 of word c/32 of row r). A wave streams 8 strain rows: 8 bytes per lane =
+// 512 contiguous bytes per load instruction, all 8 rows' loads in flight, then one lane-contiguous
+// store per row (1 KiB bf16 / 2 KiB f32 per instruction); block = 4 waves x 8 rows x 512 columns.
+// Each lane's 8 columns are one byte of a target word; lane 4j writes word j of its 128-column
+// group. Rows and X stream (non-temporal: read once here, X re-read by the input-layer GEMMs).
 // ---------------------------------------------------------------------------------------------
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+
+// bytes -> 0x00 / 0x01 (nonzero -> 1): OR-fold each byte into its bit 0 (no cross-byte leaks
+// reach bit 0: every shift source of bit 0 of byte k is a bit of byte k)
+__device__ __forceinline__ uint32_t bytes_to_01(uint32_t x) {
+  x |= x >> 4;
+  x |= x >> 2;
+  x |= x >> 1;
+  return x & 0x01010101u;
+}
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data, int64_t ld_data,
@@ -28,46 +38,47 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data
                                               T* __restrict__ X, int64_t ldx, uint32_t* __restrict__ xbits,
                                               int64_t ldxb) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int c = blockIdx.x * 1024 + lane * 16;
-  const int rbase = blockIdx.y * 16 + wid * 4;
-  if (c >= Gp) return;  // Gp % 128 == 0: whole 16-column chunks
-  uint4 v[4];
+  const int c = blockIdx.x * 512 + lane * 8;
+  const int rbase = blockIdx.y * 32 + wid * 8;
+  const bool in = c < Gp;  // Gp % 128 == 0: whole 4-lane word groups are in or out
+  u32x2 v[8];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 8; ++k) {
     const int r = rbase + k;
-    v[k] = make_uint4(0, 0, 0, 0);
-    if (r < B) {
+    v[k] = u32x2{0u, 0u};
+    if (in && r < B) {
       const int64_t src = rows ? (int64_t)rows[r] : (int64_t)r;
-      const u32x4 t = __builtin_nontemporal_load((const u32x4*)(data + src * ld_data + c));
-      v[k] = make_uint4(t[0], t[1], t[2], t[3]);
+      v[k] = __builtin_nontemporal_load((const u32x2*)(data + src * ld_data + c));
     }
   }
+  // columns >= G read as zero (the resident matrix's pad is zero already; this keeps X's pad zero
+  // whatever ld_data holds there)
+  const uint32_t keep0 = c + 4 <= G ? 0xFFFFFFFFu : (c >= G ? 0u : (0xFFFFFFFFu >> (8 * (c + 4 - G))));
+  const uint32_t keep1 = c + 8 <= G ? 0xFFFFFFFFu : (c + 4 >= G ? 0u : (0xFFFFFFFFu >> (8 * (c + 8 - G))));
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 8; ++k) {
     const int r = rbase + k;
-    uint8_t b[16];
-    *(uint4*)b = v[k];
-    uint32_t bits = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if (c + i >= G) b[i] = 0;
-      bits |= (b[i] ? 1u : 0u) << i;
-    }
-    T* dst = X + (int64_t)r * ldx + c;
-    if constexpr (sizeof(T) == 2) {
-      uint32_t w[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) w[i] = (b[2 * i] ? 0x3F80u : 0u) | ((b[2 * i + 1] ? 0x3F80u : 0u) << 16);
-      __builtin_nontemporal_store(u32x4{w[0], w[1], w[2], w[3]}, (u32x4*)dst);
-      __builtin_nontemporal_store(u32x4{w[4], w[5], w[6], w[7]}, (u32x4*)(dst + 8));
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        *(float4*)(dst + 4 * i) = make_float4((float)b[4 * i], (float)b[4 * i + 1], (float)b[4 * i + 2], (float)b[4 * i + 3]);
+    const uint32_t t0 = bytes_to_01(v[k][0]) & keep0, t1 = bytes_to_01(v[k][1]) & keep1;
+    if (in) {
+      T* dst = X + (int64_t)r * ldx + c;
+      if constexpr (sizeof(T) == 2) {
+        // (b1 << 16 | b0) * 0x3F80 = the two bf16 values (1.0 = 0x3F80), no carries for b in {0,1}
+        const uint32_t w0 = __builtin_amdgcn_perm(0u, t0, 0x0c010c00u) * 0x3F80u;
+        const uint32_t w1 = __builtin_amdgcn_perm(0u, t0, 0x0c030c02u) * 0x3F80u;
+        const uint32_t w2 = __builtin_amdgcn_perm(0u, t1, 0x0c010c00u) * 0x3F80u;
+        const uint32_t w3 = __builtin_amdgcn_perm(0u, t1, 0x0c030c02u) * 0x3F80u;
+        __builtin_nontemporal_store(u32x4{w0, w1, w2, w3}, (u32x4*)dst);
+      } else {
+        *(float4*)dst = make_float4((float)(t0 & 1), (float)((t0 >> 8) & 1), (float)((t0 >> 16) & 1), (float)(t0 >> 24));
+        *(float4*)(dst + 4) = make_float4((float)(t1 & 1), (float)((t1 >> 8) & 1), (float)((t1 >> 16) & 1), (float)(t1 >> 24));
+      }
     }
     if (xbits) {
-      const uint32_t hi = __shfl_down(bits, 1, 64);
-      if ((lane & 1) == 0) xbits[(int64_t)r * ldxb + (c >> 5)] = bits | (hi << 16);
+      // byte b_i (0/1) at bit 8i -> bit i: (t * 0x01020408) >> 24 collects them without carries
+      const uint32_t b8 = ((t0 * 0x01020408u) >> 24 & 0xFu) | (((t1 * 0x01020408u) >> 24 & 0xFu) << 4);
+      const uint32_t w = b8 | (__shfl_down(b8, 1, 64) << 8) | (__shfl_down(b8, 2, 64) << 16) |
+                         (__shfl_down(b8, 3, 64) << 24);
+      if (in && (lane & 3) == 0) xbits[(int64_t)r * ldxb + (c >> 5)] = w;
     }
   }
 }
@@ -399,10 +410,15 @@ __global__ __launch_bounds__(256) void k_sigmoid_bwd(const float* __restrict__ p
 // output-layer bias gradient column sums in k_colsum2's order (rows = strain tiles).
 __global__ __launch_bounds__(256) void k_fwd_tail(const float* __restrict__ lpart, int nl, const float* __restrict__ kpart,
                                                 int nk, double* __restrict__ loss, const float* __restrict__ cpart,
-                                                int rows, int64_t ld, int64_t n, float* __restrict__ cout) {
+                                                int rows, int64_t ld, int64_t n, float* __restrict__ cout,
+                                                int* __restrict__ hdr, int hv0, int hv1) {
   __shared__ double red[4];
   __shared__ float redf[4][64];
   if (blockIdx.x == 0) {
+    if (hdr && threadIdx.x == 0) {
+      hdr[0] = hv0;
+      hdr[1] = hv1;
+    }
     for (int k = 0; k < 3; ++k) {
       const float* part = k < 2 ? lpart + k : kpart;
       const int cnt = k < 2 ? nl : nk, stride = k < 2 ? 2 : 1;
@@ -488,9 +504,34 @@ __device__ __forceinline__ void ntstore4(float* p, const float (&v)[4]) {
   __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, (f32x4*)p);
 }
 
+// sum of g[i]^2 over [a, b), grid-stride (16-B loads between the scalar head and tail)
+__device__ __forceinline__ double seg_sumsq(const float* __restrict__ g, int64_t a, int64_t b) {
+  double ss = 0.0;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, stride = (int64_t)gridDim.x * 256;
+  if (a >= b) return ss;
+  const int64_t va = (a + 3) & ~(int64_t)3, vb = b & ~(int64_t)3;
+  if (va >= vb) {
+    for (int64_t i = a + t; i < b; i += stride) ss += (double)g[i] * g[i];
+    return ss;
+  }
+  for (int64_t i = va / 4 + t; i < vb / 4; i += stride) {
+    const float4 gv = ntload4(g + 4 * i);
+    ss += (double)gv.x * gv.x + (double)gv.y * gv.y + (double)gv.z * gv.z + (double)gv.w * gv.w;
+  }
+  if (t < va - a) ss += (double)g[a + t] * g[a + t];
+  if (t < b - vb) ss += (double)g[vb + t] * g[vb + t];
+  return ss;
+}
+
+// the GEMM-epilogue statistics are used when the caller vouches for them (scal[kScalNormAhead]),
+// the last training call recorded them (hdr[0]) and there is no L1 term (which needs sign(theta))
+__device__ __forceinline__ bool use_ahead(const NormAhead& na, const float* scal) {
+  return na.hdr && scal[kScalNormAhead] != 0.f && scal[kScalLambda] == 0.f && na.hdr[0] != 0;
+}
+
 __global__ __launch_bounds__(256) void k_grad_stats(const float* __restrict__ p, const float* __restrict__ g,
                                                   int64_t n, const float* __restrict__ scal,
-                                                  double* __restrict__ part) {
+                                                  double* __restrict__ part, NormAhead na) {
   __shared__ double red[2][4];
   const float lam = scal[kScalLambda];
   double ss = 0.0, ab = 0.0;
@@ -509,6 +550,8 @@ __global__ __launch_bounds__(256) void k_grad_stats(const float* __restrict__ p,
       ss += (double)a * a;
       ab += fabs((double)p[i]);
     }
+  } else if (use_ahead(na, scal)) {  // the two big weight gradients were summed as they were written
+    ss = seg_sumsq(g, 0, na.lo0) + seg_sumsq(g, na.hi0, na.lo9) + seg_sumsq(g, na.hi9, n);
   } else {  // no L1 term (v0): gradients only, half the traffic
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
       const float4 gv = ntload4(g + 4 * i);
@@ -529,10 +572,12 @@ __global__ __launch_bounds__(256) void k_grad_stats(const float* __restrict__ p,
 
 __global__ __launch_bounds__(256) void k_grad_finalize(const double* __restrict__ part, int nb,
                                                      const float* __restrict__ scal, float* __restrict__ clip,
-                                                     double* __restrict__ l1abs) {
+                                                     double* __restrict__ l1abs, NormAhead na) {
   __shared__ double red[2][4];
   double ss = 0.0, ab = 0.0;
   for (int i = threadIdx.x; i < nb; i += 256) { ss += part[2 * i]; ab += part[2 * i + 1]; }
+  if (use_ahead(na, scal))
+    for (int i = threadIdx.x; i < na.hdr[1]; i += 256) ss += na.sq[i];
   ss = wave_sum_d(ss);
   ab = wave_sum_d(ab);
   if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = ss; red[1][threadIdx.x >> 6] = ab; }
@@ -941,7 +986,7 @@ void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* row
                         int Gp, int Bp, uint32_t* xbits, int64_t ldxb, hipStream_t s) {
   if (Gp % 128 || Bp % 64 || ld_data % 16 || ld_data < Gp || ((uintptr_t)data & 15) || (xbits && ldxb * 32 < Gp))
     throw Gm2Error("gather: bad layout (Gp=%d Bp=%d ld=%lld)", Gp, Bp, (long long)ld_data);
-  hipLaunchKernelGGL(k_gather<T>, dim3((Gp + 1023) / 1024, Bp / 16), dim3(256), 0, s, data, ld_data, rows, B, G, Gp, X,
+  hipLaunchKernelGGL(k_gather<T>, dim3((Gp + 511) / 512, Bp / 32), dim3(256), 0, s, data, ld_data, rows, B, G, Gp, X,
                      ldx, xbits, ldxb);
   GM2_CHECK_LAUNCH();
 }
@@ -1037,10 +1082,10 @@ void launch_transpose(const T* src, int64_t lds_, int R, int Cn, T* dst, int64_t
 }
 
 void launch_fwd_tail(const float* lpart, int nl, const float* kpart, int nk, double* loss, const float* cpart, int rows,
-                     int64_t ld, int64_t n, float* cout, hipStream_t s) {
+                     int64_t ld, int64_t n, float* cout, int* hdr, int hv0, int hv1, hipStream_t s) {
   const int64_t cb = cout ? (n + 63) / 64 : 0;
   hipLaunchKernelGGL(k_fwd_tail, dim3((unsigned)(1 + cb)), dim3(256), 0, s, lpart, nl, kpart, nk, loss, cpart, rows, ld,
-                     n, cout);
+                     n, cout, hdr, hv0, hv1);
   GM2_CHECK_LAUNCH();
 }
 
@@ -1077,14 +1122,16 @@ void launch_slab_sum(const float* slabs, int S, int64_t slab, int M, int N, floa
 int grad_stats_blocks(int64_t n) { return (int)std::min<int64_t>(2048, std::max<int64_t>(1, (n + 255) / 256)); }
 
 void launch_grad_stats(const float* params, const float* grads, int64_t n, const float* scal, double* part,
-                       int nblocks, hipStream_t s) {
-  hipLaunchKernelGGL(k_grad_stats, dim3(nblocks), dim3(256), 0, s, params, grads, n, scal, part);
+                       int nblocks, const NormAhead& na, hipStream_t s) {
+  if (na.hdr && !(0 <= na.lo0 && na.lo0 <= na.hi0 && na.hi0 <= na.lo9 && na.lo9 <= na.hi9 && na.hi9 <= n))
+    throw Gm2Error("grad_stats: bad skip ranges");
+  hipLaunchKernelGGL(k_grad_stats, dim3(nblocks), dim3(256), 0, s, params, grads, n, scal, part, na);
   GM2_CHECK_LAUNCH();
 }
 
 void launch_grad_finalize(const double* part, int nblocks, const float* scal, float* clip_out, double* l1abs,
-                          hipStream_t s) {
-  hipLaunchKernelGGL(k_grad_finalize, dim3(1), dim3(256), 0, s, part, nblocks, scal, clip_out, l1abs);
+                          const NormAhead& na, hipStream_t s) {
+  hipLaunchKernelGGL(k_grad_finalize, dim3(1), dim3(256), 0, s, part, nblocks, scal, clip_out, l1abs, na);
   GM2_CHECK_LAUNCH();
 }
 

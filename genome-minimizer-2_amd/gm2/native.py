@@ -22,6 +22,7 @@ LOSS_SLOTS = 8
 # scalar block indices (gm2.h GM2_S_*)
 S_BETA, S_WGAMMA, S_LAMBDA, S_NEG_STEP, S_BC2_SQRT, S_MAX_NORM = 0, 1, 2, 3, 4, 5
 S_ONE_MINUS_B1, S_BETA2, S_ONE_MINUS_B2, S_ADAM_EPS = 6, 7, 8, 9
+S_NORM_AHEAD = 10
 
 EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_offsets",
            "gm2_workspace_size", "gm2_workspace_init", "gm2_sync_shadows", "gm2_train_fwd_bwd",
@@ -30,7 +31,7 @@ EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_of
            "gm2_mask_row_offsets", "gm2_mask_compact", "gm2_recon_counts",
            "gm2_gemm", "gm2_grad_bucket_bounds", "gm2_wait_grad_bucket", "gm2_set_option", "gm2_get_option", "gm2_timing_begin", "gm2_timing_end"]
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
-OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE, OPT_SMALL_SPLIT, OPT_BN_EPILOGUE = 1, 2, 3, 4, 5
+OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE, OPT_SMALL_SPLIT, OPT_BN_EPILOGUE, OPT_SMALL_WAVES = 1, 2, 3, 4, 5, 6
 
 
 class Dims(C.Structure):

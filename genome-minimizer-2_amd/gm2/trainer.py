@@ -191,8 +191,10 @@ class VAETrainer:
             return torch.randn(n, L).to(self.device)
         return torch.randn(n, L, device=self.device)
 
-    def _scalar_row(self, sc, adam_step=None):
+    def _scalar_row(self, sc, adam_step=None, norm_ahead=False):
         v = np.zeros(native.NUM_SCALARS, dtype=np.float64)
+        # single process, fused step: grads go from gm2_train_fwd_bwd to gm2_grad_norm untouched
+        v[native.S_NORM_AHEAD] = 1.0 if norm_ahead else 0.0
         v[native.S_BETA] = sc["beta"]
         v[native.S_WGAMMA] = sc["wgamma"]
         v[native.S_LAMBDA] = sc["lambda"]
@@ -306,7 +308,7 @@ class VAETrainer:
         for bi in range(nb):
             sc, per = self.loss_tracker.batch_scalars(epoch)
             pers.append(per)
-            srows.append(self._scalar_row(sc, self.optimizer.step_count + bi + 1))
+            srows.append(self._scalar_row(sc, self.optimizer.step_count + bi + 1, norm_ahead=dist is None))
         scal = self._upload(srows)
         ws = model.workspace(model.precision, (loader.batch_size + world - 1) // world)
         rec = torch.zeros(max(nb, 1), native.LOSS_SLOTS, dtype=torch.float64, device=self.device)

@@ -69,7 +69,12 @@ enum {
   GM2_S_ONE_MINUS_B1 = 6,
   GM2_S_BETA2 = 7,
   GM2_S_ONE_MINUS_B2 = 8,
-  GM2_S_ADAM_EPS = 9
+  GM2_S_ADAM_EPS = 9,
+  GM2_S_NORM_AHEAD = 10    /* != 0: `grads` reaches gm2_grad_norm exactly as the last
+                              gm2_train_fwd_bwd on this workspace wrote it (one process, no
+                              exchange or edit in between); the clip statistics of the two big
+                              weight gradients are then taken from that call's GEMM epilogues
+                              instead of a second pass over 2*H*G floats. 0 = always re-read. */
 };
 
 /* loss record (fp64[GM2_LOSS_SLOTS], device) filled per call:
@@ -221,13 +226,16 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       hidden layers).
  *   GM2_OPT_BN_EPILOGUE 1 = BatchNorm batch statistics (forward) and backward partial sums taken
  *                       in the producing GEMM's store epilogue where the plan allows (default),
- *                       0 = always a separate statistics pass. */
+ *                       0 = always a separate statistics pass.
+ *   GM2_OPT_SMALL_WAVES waves per workgroup (4 or 8) of the 128x128 fp32-store GEMM tiles (the
+ *                       hidden-layer GEMMs). */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
   GM2_OPT_RECON_TILE = 3,
   GM2_OPT_SMALL_SPLIT = 4,
-  GM2_OPT_BN_EPILOGUE = 5
+  GM2_OPT_BN_EPILOGUE = 5,
+  GM2_OPT_SMALL_WAVES = 6
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of libgm2 tuning options on the C2 step shape, interleaved rounds in one process; reports the
 output-layer loss kernel's HIP-event time (KC_RECON_LOSS) and the step time.
-Usage: python3 tools/recon_ab.py OPTION v1 v2 ...   (OPTION = recon_tile | small_split | gemm_pp | bn_epilogue | side_stream)"""
+Usage: python3 tools/recon_ab.py OPTION v1 v2 ...   (OPTION = recon_tile | small_split | gemm_pp | bn_epilogue | side_stream | small_waves)"""
 import os
 import sys
 import time
@@ -40,7 +40,8 @@ def step(i):
 
 
 KEYS = {"recon_tile": native.OPT_RECON_TILE, "small_split": native.OPT_SMALL_SPLIT, "gemm_pp": native.OPT_GEMM_PP,
-        "bn_epilogue": native.OPT_BN_EPILOGUE, "side_stream": native.OPT_SIDE_STREAM}
+        "bn_epilogue": native.OPT_BN_EPILOGUE, "side_stream": native.OPT_SIDE_STREAM,
+        "small_waves": native.OPT_SMALL_WAVES}
 
 
 def main():

@@ -1,5 +1,6 @@
 #!/bin/bash
-# kernel trace of a short default bench (one rocprofv3 pass, csv)
+# kernel trace of a short default bench (one rocprofv3 pass, csv); extra env (e.g. GM2_SIDE_STREAM=0)
+# is inherited from the caller
 cd "$GRAFT_REPO_ROOT" || exit 2
 mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
