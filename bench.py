@@ -78,6 +78,7 @@ def parse():
     ap.add_argument("--sample-genomes", type=int, default=1000000)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-f32-line", action="store_true")
+    ap.add_argument("--no-prefetch", action="store_true", help="gather each batch inside its own step")
     return ap.parse_args()
 
 
@@ -204,14 +205,17 @@ def main():
     tab[:, native.S_NORM_AHEAD] = 1.0 if dist is None else 0.0
     scal = torch.tensor(tab, dtype=torch.float32, device=dev)
     g = torch.Generator().manual_seed(100 + rank)
-    rows = torch.cat([torch.randperm(a.strains, generator=g)[:B] for _ in range(nsteps)]).to(torch.int32).to(dev)
+    rows = torch.cat([torch.randperm(a.strains, generator=g)[:B] for _ in range(nsteps + 1)]).to(torch.int32).to(dev)
     loss = torch.zeros(nsteps, native.LOSS_SLOTS, dtype=torch.float64, device=dev)
     torch.cuda.manual_seed(1)
     sync = GradSync(dist, model, grads) if dist is not None else None
 
     def step(i):
         eps = torch.randn(B, L, device=dev)
-        batch = native.make_batch(mat.data, mat.ld, rows[i * B:(i + 1) * B], B, eps)
+        # the next step's rows are staged during this step's tail (gm2_batch.next; the last timed step
+        # stages one batch nobody uses, so the timed region holds K gathers)
+        nxt = None if a.no_prefetch else native.make_batch(mat.data, mat.ld, rows[(i + 1) * B:(i + 2) * B], B, None)
+        batch = native.make_batch(mat.data, mat.ld, rows[i * B:(i + 1) * B], B, eps, next=nxt)
         native.train_fwd_bwd(ws, batch, model.params, grads, model.bn, scal[i], loss[i])
         if sync is not None:
             sync.after_backward()  # bucketed SUM all-reduce overlapped with the backward

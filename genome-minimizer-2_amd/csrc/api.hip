@@ -89,6 +89,7 @@ struct Layout {
   int64_t bnpart, colpart, colpart_cap, losspart, losspart_cap, klpart, gradpart, clip, scal0, total;
   int64_t colbwd, colbwd_cap;  // per-layer bias-gradient partials of the backward (summed on the side stream)
   int64_t nahdr, nasq;         // norm-ahead header int[4] and per-tile sums of squares (NormAhead)
+  int64_t X1, XB1;             // second input slot: the next batch's rows, staged under this step's tail
 };
 
 Layout make_layout(const gm2_dims* gd, int prec) {
@@ -147,6 +148,8 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.nasq = take(2 * (d.Gp / kTile + 1) * (H / kTile + 1) * 8);
   o.clip = take(64);
   o.scal0 = take(GM2_NUM_SCALARS * 4);
+  o.X1 = take(Bm * d.Gp * es);
+  o.XB1 = take(Bm * (d.Gp / 32) * 4);
   o.total = cur;
   return o;
 }
@@ -158,12 +161,16 @@ struct Ctx {
   hipStream_t s;
   const Dims& d;
   int64_t slab_off, slab_cap;  // split-K scratch of this stream
+  int64_t xo, xbo;             // input slot of this call: gathered rows X [Bm][Gp] (T), target bits
   Ctx(const Layout& l, void* w, void* st)
-      : lo(l), ws((char*)w), s((hipStream_t)st), d(l.d), slab_off(l.slabs), slab_cap(l.slab_cap) {}
+      : lo(l), ws((char*)w), s((hipStream_t)st), d(l.d), slab_off(l.slabs), slab_cap(l.slab_cap), xo(l.X),
+        xbo(l.XB) {}
   Ctx side(hipStream_t st) const {
     Ctx c(lo, ws, st);
     c.slab_off = lo.side_slabs;
     c.slab_cap = lo.side_cap;
+    c.xo = xo;
+    c.xbo = xbo;
     return c;
   }
   T* t(int64_t off) const { return (T*)(ws + off); }
@@ -284,7 +291,7 @@ BigGrads<T> big_grads(const Ctx<T>& c, int Bp) {
   const Layout& l = c.lo;
   const int H = (int)c.d.H, G = (int)c.d.G, Gp = (int)c.d.Gp;
   BigGrads<T> r{{c.t(l.AT5), Bp, c.t(l.dL), Gp, H, G, Bp, H, Gp, 0, 1, 0},
-                {c.t(l.dYT0), Bp, c.t(l.X), Gp, H, G, Bp, H, Gp, 0, 1, 0}, false, 0, 0};
+                {c.t(l.dYT0), Bp, c.t(c.xo), Gp, H, G, Bp, H, Gp, 0, 1, 0}, false, 0, 0};
   r.direct = plan_gemm<T>(r.g9).splits == 1 && plan_gemm<T>(r.g0).splits == 1;
   r.n9 = gemm_tiles<T>(r.g9);
   r.n0 = gemm_tiles<T>(r.g0);
@@ -368,7 +375,7 @@ TensorTable make_table(const Ctx<T>& c, int kind = 0) {
 template <typename T>
 void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, int train, int with_grad,
              const float* scal, double* loss, float* grads, float* probs = nullptr, int64_t ld_probs = 0,
-             int* counts = nullptr, float thr = 0.5f, bool norm_hdr = false) {
+             int* counts = nullptr, float thr = 0.5f, bool norm_hdr = false, bool staged = false) {
   const Dims& d = c.d;
   const Layout& l = c.lo;
   const int B = (int)b->n;
@@ -377,11 +384,12 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   if (!b->data) throw Gm2Error("null data");
   const int Bp = (int)round_up(B, kTile);
   const int H = (int)d.H, L = (int)d.L;
-  // 1) strain rows -> X [Bp][Gp] (T) + bit-packed target
-  launch_gather_rows<T>(b->data, b->ld_data, b->rows, B, (int)d.G, c.t(l.X), d.Gp, (int)d.Gp, Bp,
-                        (uint32_t*)(c.ws + l.XB), d.Gp / 32, c.s);
+  // 1) strain rows -> X [Bp][Gp] (T) + bit-packed target (unless a previous training call staged them)
+  if (!staged)
+    launch_gather_rows<T>(b->data, b->ld_data, b->rows, B, (int)d.G, c.t(c.xo), d.Gp, (int)d.Gp, Bp,
+                          (uint32_t*)(c.ws + c.xbo), d.Gp / 32, c.s);
   // 2) encoder blocks, heads + reparameterisation, decoder blocks (all NT GEMMs)
-  const T* in = c.t(l.X);
+  const T* in = c.t(c.xo);
   int64_t ldin = d.Gp;
   int Kin = (int)d.Gp;
   const int64_t shadow_in[6] = {l.sE0, l.sE1, l.sE2, l.sD0, l.sD1, l.sD2};
@@ -407,12 +415,12 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
                           // per-strain (TP, FP, FN) of (p > thr) vs the strain's genes; no loss
     GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, B, (int)d.G, H, Bp, (int)d.Gp, 0};
     launch_gemm_mask<T>(g, prm + d.off[D9B], nullptr, 0, probs, ld_probs, c.s, nullptr, 0, counts,
-                        (const uint32_t*)(c.ws + l.XB), d.Gp / 32, thr);
+                        (const uint32_t*)(c.ws + c.xbo), d.Gp / 32, thr);
     return;
   }
   // 3) output layer + reconstruction loss (+ dlogits), computed as logit^T: genes x strains
   GemmArgs<T> g{c.t(l.sD3), H, c.t(l.A[5]), H, (int)d.G, B, H, (int)d.Gp, Bp, 0};
-  launch_gemm_recon_loss<T>(g, prm + d.off[D9B], (const uint32_t*)(c.ws + l.XB), d.Gp / 32, with_grad, scal, c.t(l.dL),
+  launch_gemm_recon_loss<T>(g, prm + d.off[D9B], (const uint32_t*)(c.ws + c.xbo), d.Gp / 32, with_grad, scal, c.t(l.dL),
                             d.Gp, c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
   int na_ok = 0, na_n = 0;
   if (norm_hdr) {  // the training call: record whether its backward takes the clip statistics
@@ -428,9 +436,17 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
 // Backward. Every operand is read in the layout its producer wrote: weight gradients use MN-major P
 // and Q (dW[out][in] = sum_b dY[b][out] * in[b][in]), input gradients an MN-major weight
 // (dX[b][in] = sum_out dY[b][out] * W[out][in]); no transposed copy exists anywhere.
+// The next training batch's gather, staged into the other input slot (gm2_batch.next)
+struct NextStage {
+  const gm2_batch* b = nullptr;
+  int64_t xo = 0, xbo = 0;
+  hipEvent_t done = nullptr;
+};
+
 template <typename T>
 void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, const float* scal,
-              const float* dmu_ext = nullptr, const float* dlv_ext = nullptr, int train = 1) {
+              const float* dmu_ext = nullptr, const float* dlv_ext = nullptr, int train = 1,
+              const NextStage* nx = nullptr) {
   const Dims& d = c.d;
   const Layout& l = c.lo;
   const int B = (int)b->n, Bp = (int)round_up(B, kTile);
@@ -504,8 +520,18 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       if (sr) order(sr, w.s, c.s);  // join: every hidden-layer weight gradient is final
       HIP_OK(hipEventRecord(be->ev[1], c.s));
       if (!bg.direct || !launch_gemm_sq<T>(bg.g0, gr + d.off[E0W], G, nasq + bg.n9, c.s))
-        gemm_to<T>(c, c.t(l.dYT0), Bp, H, c.t(l.X), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0);
+        gemm_to<T>(c, c.t(l.dYT0), Bp, H, c.t(c.xo), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0);
       HIP_OK(hipEventRecord(be->ev[2], c.s));
+      if (nx) {  // the next batch's rows -> the other input slot, on the side stream after dWe0 (beside
+                 // it, it only slows the GEMM down by its own length): under the data-parallel exchange
+                 // of the input-layer gradient, or beside the clip / Adam passes on one GPU
+        const hipStream_t gs = sr ? w.s : c.s;
+        if (sr) order(sr, c.s, w.s);  // placed after dWe0 (that slot's readers, the previous step, are earlier)
+        const int Bn = (int)nx->b->n;
+        launch_gather_rows<T>(nx->b->data, nx->b->ld_data, nx->b->rows, Bn, G, c.t(nx->xo), Gp, Gp,
+                              (int)round_up(Bn, kTile), (uint32_t*)(c.ws + nx->xbo), Gp / 32, gs);
+        HIP_OK(hipEventRecord(nx->done, gs));
+      }
       be->recorded = true;
       break;
     }
@@ -553,12 +579,75 @@ void decode_chain(const Ctx<T>& c, const float* prm, float* bn, int n, uint8_t* 
   launch_gemm_mask<T>(g, prm + d.off[D9B], mask, ldm, probs, ldpr, c.s, bits, ldb);
 }
 
+// Per-workspace input-slot state. A training call whose batch carries `next` gathers next's rows
+// into the other slot during its own tail; the following training call finds them there (same
+// data / ld / rows / n) and starts straight at the input-layer GEMM. Every other call that uses an
+// input slot first waits for a pending stage and drops it (it writes slot 0).
+struct SlotState {
+  bool staged = false;
+  int slot = 0;  // slot of the staged batch
+  const uint8_t* data = nullptr;
+  int64_t ld = 0, n = 0, total = 0;
+  const int32_t* rows = nullptr;
+  int prec = -1;
+  hipEvent_t done = nullptr;
+};
+
+SlotState& slot_state(void* ws) {
+  static std::map<void*, SlotState> m;
+  SlotState& st = m[ws];
+  if (!st.done) HIP_OK(hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
+  return st;
+}
+std::mutex& slot_mutex() {
+  static std::mutex mu;
+  return mu;
+}
+
+// make `s` wait for a pending stage on `ws` and forget it (the caller is about to write slot 0)
+void drop_stage(void* ws, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(slot_mutex());
+  SlotState& st = slot_state(ws);
+  if (st.staged) HIP_OK(hipStreamWaitEvent(s, st.done, 0));
+  st.staged = false;
+}
+
 template <typename T>
 void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr, float* bn, const float* scal,
                double* loss, void* ws, void* st) {
   Ctx<T> c(lo, ws, st);
-  forward<T>(c, b, prm, bn, 1, 1, scal, loss, gr, nullptr, 0, nullptr, 0.5f, true);
-  backward<T>(c, b, prm, gr, scal);
+  std::lock_guard<std::mutex> lk(slot_mutex());
+  SlotState& ss = slot_state(ws);
+  const bool hit = ss.staged && ss.prec == lo.prec && ss.total == lo.total && ss.data == b->data &&
+                   ss.ld == b->ld_data && ss.rows == b->rows && ss.n == b->n;
+  if (ss.staged) HIP_OK(hipStreamWaitEvent(c.s, ss.done, 0));
+  const int slot = hit ? ss.slot : 0;
+  c.xo = slot ? lo.X1 : lo.X;
+  c.xbo = slot ? lo.XB1 : lo.XB;
+  ss.staged = false;
+  NextStage nx;
+  const gm2_batch* nb = b->next;
+  if (nb) {
+    if (nb->n <= 0 || nb->n > lo.d.Bm || !nb->data) throw Gm2Error("next batch: rows %lld outside (0, batch_max]", (long long)nb->n);
+    if (nb->ld_data % 16 || nb->ld_data < lo.d.Gp || ((uintptr_t)nb->data & 15))
+      throw Gm2Error("next batch: bad data layout");
+    nx.b = nb;
+    nx.xo = slot ? lo.X : lo.X1;
+    nx.xbo = slot ? lo.XB : lo.XB1;
+    nx.done = ss.done;
+  }
+  forward<T>(c, b, prm, bn, 1, 1, scal, loss, gr, nullptr, 0, nullptr, 0.5f, true, hit);
+  backward<T>(c, b, prm, gr, scal, nullptr, nullptr, 1, nb ? &nx : nullptr);
+  if (nb) {
+    ss.staged = true;
+    ss.slot = slot ^ 1;
+    ss.data = nb->data;
+    ss.ld = nb->ld_data;
+    ss.rows = nb->rows;
+    ss.n = nb->n;
+    ss.prec = lo.prec;
+    ss.total = lo.total;
+  }
 }
 
 }  // namespace
@@ -653,6 +742,7 @@ int gm2_eval_forward(const gm2_dims* d, int prec, const gm2_batch* batch, const 
                      const float* bn_running, const float* scalars, double* loss, void* ws, void* stream) {
   return guarded([&] {
     const Layout lo = make_layout(d, prec);
+    drop_stage(ws, (hipStream_t)stream);  // these write input slot 0
     float* bn = const_cast<float*>(bn_running);  // eval mode never writes running stats
     if (prec == GM2_F32) {
       Ctx<float> c(lo, ws, stream);
@@ -724,6 +814,7 @@ int gm2_recon_counts(const gm2_dims* d, int prec, const gm2_batch* batch, const 
                      float threshold, int32_t* counts, void* ws, void* stream) {
   return guarded([&] {
     const Layout lo = make_layout(d, prec);
+    drop_stage(ws, (hipStream_t)stream);  // these write input slot 0
     if (!batch->eps) throw Gm2Error("recon_counts: eps required (model(x) samples z)");
     if (!counts) throw Gm2Error("recon_counts: counts required");
     HIP_OK(hipMemsetAsync(counts, 0, (size_t)batch->n * 3 * 4, (hipStream_t)stream));
@@ -742,6 +833,7 @@ int gm2_encode(const gm2_dims* d, int prec, const gm2_batch* batch, const float*
                float* mu, float* logvar, void* ws, void* stream) {
   return guarded([&] {
     const Layout lo = make_layout(d, prec);
+    drop_stage(ws, (hipStream_t)stream);  // these write input slot 0
     gm2_batch b = *batch;
     auto run = [&](auto tag) {
       using T = decltype(tag);
@@ -806,6 +898,7 @@ int gm2_forward(const gm2_dims* d, int prec, const gm2_batch* batch, const float
                 int train, float* probs, int64_t ld_probs, float* mu, float* logvar, void* ws, void* stream) {
   return guarded([&] {
     const Layout lo = make_layout(d, prec);
+    drop_stage(ws, (hipStream_t)stream);  // these write input slot 0
     if (!probs || ld_probs < lo.d.G) throw Gm2Error("forward: probs required, ld_probs >= G");
     if (!batch->eps) throw Gm2Error("forward: eps required (model.py:102 draws it)");
     auto run = [&](auto tag) {
@@ -827,6 +920,7 @@ int gm2_backward_outputs(const gm2_dims* d, int prec, const gm2_batch* batch, co
                          const float* dlogvar, float* grads, void* ws, void* stream) {
   return guarded([&] {
     const Layout lo = make_layout(d, prec);
+    drop_stage(ws, (hipStream_t)stream);  // these write input slot 0
     if (!probs || !dprobs || ld_probs < lo.d.G) throw Gm2Error("backward_outputs: probs / dprobs required");
     auto run = [&](auto tag) {
       using T = decltype(tag);

@@ -39,8 +39,11 @@ class Dims(C.Structure):
 
 
 class Batch(C.Structure):
-    _fields_ = [("data", C.c_void_p), ("ld_data", C.c_int64), ("rows", C.c_void_p), ("n", C.c_int64),
-                ("eps", C.c_void_p)]
+    pass
+
+
+Batch._fields_ = [("data", C.c_void_p), ("ld_data", C.c_int64), ("rows", C.c_void_p), ("n", C.c_int64),
+                  ("eps", C.c_void_p), ("next", C.POINTER(Batch))]
 
 
 _lib = None
@@ -91,7 +94,7 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.gm2_abi_version() != 1:
+    if L.gm2_abi_version() != 2:
         raise RuntimeError("libgm2 ABI mismatch")
     _lib = L
     return L
@@ -142,9 +145,14 @@ class Workspace:
               "gm2_workspace_init")
 
 
-def make_batch(data, ld, rows, n, eps) -> Batch:
-    return Batch(data.data_ptr(), int(ld), None if rows is None else rows.data_ptr(), int(n),
-                 None if eps is None else eps.data_ptr())
+def make_batch(data, ld, rows, n, eps, next: "Batch | None" = None) -> Batch:
+    """`next` (training only): the batch the following train_fwd_bwd on the same workspace gets; its
+    rows are gathered during this step's tail (gm2_batch.next). Keep its tensors unchanged until then."""
+    b = Batch(data.data_ptr(), int(ld), None if rows is None else rows.data_ptr(), int(n),
+              None if eps is None else eps.data_ptr())
+    if next is not None:
+        b.next = C.pointer(next)
+    return b
 
 
 def sync_shadows(ws: Workspace, params):

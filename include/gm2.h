@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GM2_ABI_VERSION 1
+#define GM2_ABI_VERSION 2
 #define GM2_NUM_PARAMS 30 /* tensors in model.parameters() */
 #define GM2_NUM_SCALARS 16
 
@@ -55,6 +55,13 @@ typedef struct gm2_batch {
   const int32_t* rows;
   int64_t n;
   const float* eps;
+  /* optional (gm2_train_fwd_bwd only): the batch the NEXT gm2_train_fwd_bwd on this workspace will
+   * be given. Its rows are gathered into the workspace's second input slot on the library's side
+   * stream while this call's input-layer weight-gradient GEMM runs; the next call, given a batch
+   * with the same data / ld_data / rows / n, then skips its own gather. The memory `next` points at
+   * (data, rows) must stay unchanged until that call; eps is not read. Any other call that gathers
+   * rows (eval, encode, forward, recon counts) first waits for and discards a pending stage. */
+  const struct gm2_batch* next;
 } gm2_batch;
 
 /* device scalar block (fp32[GM2_NUM_SCALARS]) read by the kernels, written by the host per step

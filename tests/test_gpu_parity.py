@@ -321,3 +321,51 @@ def test_gather_rows_matches_indexing():
     native.encode(ws, native.make_batch(mat.data, mat.ld, rows.to(torch.int32).cuda(), B, None), m.params, m.bn,
                   mu, None)
     np.testing.assert_array_equal(mu.cpu().numpy(), mu_all.cpu().numpy())
+
+
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+@pytest.mark.parametrize("G,H,L,B", [(517, 128, 16, 130), (8192, 256, 32, 1024)])
+def test_staged_next_batch_bit_identical(prec, G, H, L, B):
+    """gm2_batch.next: a training call gathers the next batch's rows into the second input slot under
+    its own tail. Steps that use a staged batch must be bit-identical to steps that gather their
+    own rows, including a staged batch that is then NOT used (a different batch follows), a ragged
+    last batch, and an eval call between two training calls (which discards the stage)."""
+    P, S = perturb_bn(*oracle_state(G, H, L, 3 * G + B), seed=4)
+    X = synth_x(3 * B, G, 11)
+    pr = native.GM2_F32 if prec == "f32" else native.GM2_BF16
+    gen = torch.Generator().manual_seed(5)
+    sizes = [B, B, B - 37, B, B]
+    rows = [torch.randperm(3 * B, generator=gen)[:n].to(torch.int32).cuda() for n in sizes]
+    other = torch.randperm(3 * B, generator=gen)[:B].to(torch.int32).cuda()
+    eps = [torch.randn(n, L, generator=gen).cuda() for n in sizes]
+    sc = scalars(beta=0.37, wgamma=0.55, lam=0.0)
+
+    def run(staged):
+        m = to_model(P, S, G, H, L, pr)
+        mat = ResidentMatrix(X)
+        ws = m.workspace(pr, B)
+        out = []
+        for i, n in enumerate(sizes):
+            nxt = None
+            if staged and i + 1 < len(sizes):
+                # step 1 stages `other` but step 2 is given its own rows (a miss); step 2 -> 3 is then
+                # interrupted by an eval call
+                nr = other if i == 1 else rows[i + 1]
+                nxt = native.make_batch(mat.data, mat.ld, nr, B if i == 1 else sizes[i + 1], None)
+            grads = torch.zeros_like(m.params)
+            loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+            native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, rows[i], n, eps[i], next=nxt), m.params,
+                                 grads, m.bn, sc, loss)
+            if i == 3:
+                el = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+                native.eval_forward(ws, native.make_batch(mat.data, mat.ld, other, B, eps[0]), m.params, m.bn, sc, el)
+                out.append(el.cpu())
+            out.append(grads.cpu())
+            out.append(loss.cpu())
+        torch.cuda.synchronize()
+        return out
+
+    a, b = run(False), run(True)
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
