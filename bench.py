@@ -79,6 +79,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-f32-line", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true", help="gather each batch inside its own step")
+    ap.add_argument("--grad-exchange", choices=["f32", "bf16"], default="bf16",
+                    help="N>1: dtype the big weight gradients are all-reduced in (gm2.ddp.GradSync)")
+    ap.add_argument("--input-chunks", type=int, choices=[1, 4], default=None,
+                    help="input-layer weight-gradient launches (default: 4 under DDP, else 1)")
     return ap.parse_args()
 
 
@@ -208,7 +212,9 @@ def main():
     rows = torch.cat([torch.randperm(a.strains, generator=g)[:B] for _ in range(nsteps + 1)]).to(torch.int32).to(dev)
     loss = torch.zeros(nsteps, native.LOSS_SLOTS, dtype=torch.float64, device=dev)
     torch.cuda.manual_seed(1)
-    sync = GradSync(dist, model, grads) if dist is not None else None
+    sync = GradSync(dist, model, grads, exchange=a.grad_exchange) if dist is not None else None
+    if a.input_chunks is not None:
+        native.set_option(native.OPT_INPUT_CHUNKS, a.input_chunks)
 
     def step(i):
         eps = torch.randn(B, L, device=dev)
@@ -264,7 +270,12 @@ def main():
         "config": {"workload": "C2: v0 train step (fwd+bwd+clip+Adam), synthetic pan-genome "
                                f"{a.strains}x{G} u8 resident, batch {B}/GPU",
                    "preset": "v0", "genes": G, "hidden": H, "latent": L, "global_batch": B * world,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "grad_exchange": (f"{a.grad_exchange} (decoder.9 / encoder.0 weight buckets; rest f32), RCCL "
+                                     f"SUM all-reduce overlapped with the backward, input-layer gradient in "
+                                     f"{native.get_option(native.OPT_INPUT_CHUNKS)} launch(es)")
+                   if world > 1 else "none (one GPU)",
+                   "input_prefetch": not a.no_prefetch},
         "train_tflops": round(value * train_flops_per_vector(G, H, L) / 1e12, 2),
         "nonfinite_steps": nonfinite,
         "roofline": {"bound": "mfma", "kernel": "k_gemm_recon_loss<bf16>" if prec == native.GM2_BF16

@@ -243,10 +243,21 @@ BucketEvents* bucket_events() {
   return &b;
 }
 
+// first row of quarter q (0..4) of the input-layer weight gradient [H][G]
+int64_t input_quarter_row(const Dims& d, int q) { return (d.H * q) / 4; }
+
 void bucket_bounds(const Dims& d, int64_t* lh) {
   lh[0] = d.off[D9W], lh[1] = d.off[NP];
   lh[2] = d.off[E0B], lh[3] = d.off[D9W];
-  lh[4] = 0, lh[5] = d.off[E0B];
+  for (int q = 0; q < 4; ++q) {
+    lh[4 + 2 * q] = input_quarter_row(d, q) * d.G;
+    lh[5 + 2 * q] = input_quarter_row(d, q + 1) * d.G;
+  }
+}
+
+std::atomic<int>& input_chunks_flag() {
+  static std::atomic<int> v{1};
+  return v;
 }
 
 // GEMM into the fp32 slab scratch (split-K slices summed by the consumer). Returns #slabs.
@@ -286,6 +297,15 @@ struct BigGrads {
   bool direct;
   int n9, n0;
 };
+// the input-layer weight gradient as four row-quarter launches (GM2_OPT_INPUT_CHUNKS = 4): only
+// when each quarter is whole 256-row tiles of a one-pass plan, like the full launch
+template <typename T>
+bool input_chunked(const BigGrads<T>& r, int H) {
+  if (input_chunks_flag().load(std::memory_order_relaxed) != 4 || H % 1024) return false;
+  const GemmPlan p = plan_gemm<T>(r.g0);
+  return p.splits == 1 && p.tile == 256;
+}
+
 template <typename T>
 BigGrads<T> big_grads(const Ctx<T>& c, int Bp) {
   const Layout& l = c.lo;
@@ -296,6 +316,7 @@ BigGrads<T> big_grads(const Ctx<T>& c, int Bp) {
   r.n9 = gemm_tiles<T>(r.g9);
   r.n0 = gemm_tiles<T>(r.g0);
   if ((int64_t)(r.n9 + r.n0) > 2 * (c.d.Gp / kTile + 1) * (c.d.H / kTile + 1)) r.direct = false;
+  if (input_chunked(r, (int)c.d.H)) r.direct = false;  // the quarter launches take no clip statistics
   return r;
 }
 
@@ -519,9 +540,21 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       launch_transpose<T>(dY, H, Bp, H, c.t(l.dYT0), Bp, c.s);
       if (sr) order(sr, w.s, c.s);  // join: every hidden-layer weight gradient is final
       HIP_OK(hipEventRecord(be->ev[1], c.s));
-      if (!bg.direct || !launch_gemm_sq<T>(bg.g0, gr + d.off[E0W], G, nasq + bg.n9, c.s))
-        gemm_to<T>(c, c.t(l.dYT0), Bp, H, c.t(c.xo), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0);
-      HIP_OK(hipEventRecord(be->ev[2], c.s));
+      if (input_chunked(bg, H)) {  // four row-quarter launches, bucket 2 + q final after launch q
+        for (int q = 0; q < 4; ++q) {
+          GemmArgs<T> gq = bg.g0;
+          const int r0 = (int)input_quarter_row(d, q);
+          gq.P = bg.g0.P + (int64_t)r0 * bg.g0.ldp;
+          gq.M = gq.Mp = H / 4;
+          if (!launch_gemm_sq<T>(gq, gr + d.off[E0W] + (int64_t)r0 * G, G, nullptr, c.s, true))
+            throw Gm2Error("input-layer quarter GEMM: not a one-pass plan");
+          HIP_OK(hipEventRecord(be->ev[2 + q], c.s));
+        }
+      } else {
+        if (!bg.direct || !launch_gemm_sq<T>(bg.g0, gr + d.off[E0W], G, nasq + bg.n9, c.s))
+          gemm_to<T>(c, c.t(l.dYT0), Bp, H, c.t(c.xo), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0);
+        for (int q = 0; q < 4; ++q) HIP_OK(hipEventRecord(be->ev[2 + q], c.s));
+      }
       if (nx) {  // the next batch's rows -> the other input slot, on the side stream after dWe0 (beside
                  // it, it only slows the GEMM down by its own length): under the data-parallel exchange
                  // of the input-layer gradient, or beside the clip / Adam passes on one GPU
@@ -975,6 +1008,10 @@ int gm2_set_option(int key, int value) {
       case GM2_OPT_SMALL_SPLIT: set_small_split(value); break;
       case GM2_OPT_BN_EPILOGUE: set_bn_epilogue(value); break;
       case GM2_OPT_SMALL_WAVES: set_small_waves(value); break;
+      case GM2_OPT_INPUT_CHUNKS:
+        if (value != 1 && value != 4) throw Gm2Error("input chunks %d: 1 or 4", value);
+        input_chunks_flag().store(value);
+        break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });
@@ -989,6 +1026,7 @@ int gm2_get_option(int key, int* value) {
       case GM2_OPT_SMALL_SPLIT: *value = get_small_split(); break;
       case GM2_OPT_BN_EPILOGUE: *value = get_bn_epilogue(); break;
       case GM2_OPT_SMALL_WAVES: *value = get_small_waves(); break;
+      case GM2_OPT_INPUT_CHUNKS: *value = input_chunks_flag().load(); break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });

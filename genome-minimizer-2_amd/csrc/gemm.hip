@@ -1199,11 +1199,15 @@ int gemm_tiles(const GemmArgs<T>& g) {
 }
 
 template <typename T>
-bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s) {
-  if (plan_gemm(g).splits != 1) return false;
+bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s, bool force_big) {
+  // force_big: a one-pass 256x256-tile launch even where the plan would pick 128 tiles (a row
+  // slice of a big-tile GEMM, same per-element results as the whole)
+  const bool big = force_big ? (g.Mp % 256 == 0 && g.Np % 256 == 0) : use_big(g);
+  if (!force_big && plan_gemm(g).splits != 1) return false;
+  if (force_big && !big) return false;
   StoreEpi ep;
   ep.sq = sq;
-  if (use_big(g)) {
+  if (big) {
     check_gemm(g, 256);
     store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
   } else {
@@ -1351,7 +1355,7 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
 
 #define GM2_INST(T)                                                                                              \
   template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t, double*);                \
-  template bool launch_gemm_sq<T>(const GemmArgs<T>&, float*, int64_t, double*, hipStream_t);                    \
+  template bool launch_gemm_sq<T>(const GemmArgs<T>&, float*, int64_t, double*, hipStream_t, bool);              \
   template int gemm_tiles<T>(const GemmArgs<T>&);                        \
   template bool launch_gemm_bn<T>(const GemmArgs<T>&, float*, int64_t, const float*, const StoreEpi&, hipStream_t);   \
   template int launch_gemm_store<T>(const GemmArgs<T>&, int, float*, float*, int, int64_t, int64_t, const float*, \

@@ -106,7 +106,7 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
 // C = P . Q^T in one K pass with the per-tile sum of squares of C into sq (see StoreEpi::sq);
 // false (nothing launched) when the plan splits K
 template <typename T>
-bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s);
+bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s, bool force_big = false);
 // tiles of a one-pass launch of g (the sq entries it writes)
 template <typename T>
 int gemm_tiles(const GemmArgs<T>& g);

@@ -8,7 +8,8 @@ Semantics:
   * the gradient buffer is SUM-all-reduced in GM2_GRAD_BUCKETS contiguous buckets, each started on a
     communication stream as soon as libgm2 has finalised it (gm2_wait_grad_bucket: a device-side
     wait on the bucket's event), so the output-layer bucket's exchange runs under the rest of the
-    backward; L1, clip statistics and Adam then run on the reduced gradient, identically on every
+    backward and the input-layer weight gradient's four row quarters (GM2_OPT_INPUT_CHUNKS = 4:
+    one launch each) are exchanged under the launches that follow them; L1, clip statistics and Adam then run on the reduced gradient, identically on every
     rank (the losses are sum-reductions, so the reduced gradient is the global-batch gradient
     except that train-mode BatchNorm normalises with each rank's own shard statistics, the
     standard non-synchronised DDP BatchNorm);
@@ -46,14 +47,29 @@ def rank_slice(n, rank, world):
 
 
 class GradSync:
-    """Bucketed SUM all-reduce of the flat gradient buffer, overlapped with the backward."""
+    """Bucketed SUM all-reduce of the flat gradient buffer, overlapped with the backward.
 
-    def __init__(self, dist, model, grads):
+    exchange="f32" (default) all-reduces the fp32 gradient as it is. exchange="bf16" sends the two
+    big weight gradients (buckets 0 and 2..5: decoder.9 and encoder.0, ~96 % of the bytes of v0) as
+    bf16 and sums them in bf16 over the ranks (half the bytes on xGMI; each element carries the
+    rounding of its per-rank values and of the ring's partial sums, ~2^-9 relative per addition);
+    the hidden/BN bucket stays fp32. The result is identical on every rank, and clip / L1 / Adam run
+    on it in fp32 as before."""
+
+    def __init__(self, dist, model, grads, exchange="f32"):
+        if exchange not in ("f32", "bf16"):
+            raise ValueError(f"gradient exchange {exchange!r}: 'f32' or 'bf16'")
         self.dist = dist
         self.grads = grads
+        self.exchange = exchange
+        self.buf = torch.empty(grads.numel(), dtype=torch.bfloat16, device=grads.device) \
+            if exchange == "bf16" else None
         self.bounds = native.grad_bucket_bounds(native.dims(model.input_dim, model.hidden_dim,
                                                             model.latent_dim, 1))
         self.stream = torch.cuda.Stream(device=grads.device)
+        # the input-layer weight gradient (half the bytes) as four launches, so the exchange of its
+        # first quarters runs under the GEMM of the later ones (bit-identical results)
+        native.set_option(native.OPT_INPUT_CHUNKS, 4)
 
     def after_backward(self, ran=True):
         """Enqueue the bucket all-reduces behind the backward just launched (ran=True), or behind
@@ -65,7 +81,13 @@ class GradSync:
             for b, (lo, hi) in enumerate(self.bounds):
                 if ran:
                     native.wait_grad_bucket(b, self.stream)
-                self.dist.all_reduce(self.grads[lo:hi])
+                if self.buf is not None and b != 1:
+                    t = self.buf[lo:hi]
+                    t.copy_(self.grads[lo:hi])
+                    self.dist.all_reduce(t)
+                    self.grads[lo:hi].copy_(t)
+                else:
+                    self.dist.all_reduce(self.grads[lo:hi])
         cur.wait_stream(self.stream)
 
 

@@ -118,12 +118,15 @@ int gm2_train_fwd_bwd(const gm2_dims* d, int precision, const gm2_batch* batch, 
 
 /* Data-parallel gradient exchange. The flat gradient buffer is cut into
  * GM2_GRAD_BUCKETS contiguous ranges in the order gm2_train_fwd_bwd finalises them:
- *   0 = decoder.9.{weight,bias}, 1 = encoder.0.bias .. decoder.7.bias, 2 = encoder.0.weight.
+ *   0 = decoder.9.{weight,bias}, 1 = encoder.0.bias .. decoder.7.bias,
+ *   2..5 = encoder.0.weight rows in four contiguous quarters (of H rows each rounded to whole
+ *          rows; with GM2_OPT_INPUT_CHUNKS = 4 each quarter is final after its own launch, so the
+ *          exchange of the first quarters runs under the GEMM of the later ones).
  * gm2_grad_bucket_bounds writes [lo, hi) element offsets per bucket (lo_hi[2*GM2_GRAD_BUCKETS]).
  * gm2_wait_grad_bucket makes `stream` wait (device-side, no host sync) until that bucket of the
  * most recent gm2_train_fwd_bwd on the current device is written, so a caller can start the
  * all-reduce of bucket b on a communication stream while the rest of the backward still runs. */
-#define GM2_GRAD_BUCKETS 3
+#define GM2_GRAD_BUCKETS 6
 int gm2_grad_bucket_bounds(const gm2_dims* d, int64_t* lo_hi);
 int gm2_wait_grad_bucket(int bucket, void* stream);
 
@@ -235,14 +238,18 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       in the producing GEMM's store epilogue where the plan allows (default),
  *                       0 = always a separate statistics pass.
  *   GM2_OPT_SMALL_WAVES waves per workgroup (4 or 8) of the 128x128 fp32-store GEMM tiles (the
- *                       hidden-layer GEMMs). */
+ *                       hidden-layer GEMMs).
+ *   GM2_OPT_INPUT_CHUNKS 1 (default) or 4: launches of the input-layer weight-gradient GEMM, one
+ *                       per gradient bucket 2..5 (when H/4 is a multiple of 256; else 1). Same
+ *                       results bit for bit; 4 lets a data-parallel exchange start early. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
   GM2_OPT_RECON_TILE = 3,
   GM2_OPT_SMALL_SPLIT = 4,
   GM2_OPT_BN_EPILOGUE = 5,
-  GM2_OPT_SMALL_WAVES = 6
+  GM2_OPT_SMALL_WAVES = 6,
+  GM2_OPT_INPUT_CHUNKS = 7
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);

@@ -173,3 +173,53 @@ def test_two_rank_trainer_epoch(tmp_path):
     assert n_b == 3
     for k, v in zip(["reconstruction", "gene_abundance", "kl_divergence"], vs):
         assert abs(va[k] - v / N_VAL) <= 1e-5 * abs(v / N_VAL) + 1e-7, (k, va[k], v / N_VAL)
+
+
+def _exchange_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gm2 import native
+    from gm2.data import ResidentMatrix
+    from gm2.ddp import GradSync
+    from gm2.model import VAE
+
+    Gx, Hx, Lx, Bx = 20000, 1024, 32, 128
+    x = synth_x(Bx, Gx, 20 + rank)  # each rank its own rows
+    torch.manual_seed(SEED)
+    m = VAE(Gx, Hx, Lx, precision=native.GM2_BF16)
+    ws = m.workspace(native.GM2_BF16, Bx)
+    mat = ResidentMatrix(x)
+    eps = torch.randn(Bx, Lx, generator=torch.Generator().manual_seed(rank)).cuda()
+    sc = torch.zeros(native.NUM_SCALARS, dtype=torch.float32, device="cuda")
+    sc[native.S_BETA] = 0.5
+    res = {}
+    for ex in ("f32", "bf16"):
+        grads = torch.zeros_like(m.params)
+        loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+        sync = GradSync(dist, m, grads, exchange=ex)
+        native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, Bx, eps), m.params, grads, m.bn, sc, loss)
+        sync.after_backward()
+        torch.cuda.synchronize()
+        res[ex] = grads.cpu().numpy()
+    np.savez(os.path.join(out_dir, f"x{rank}.npz"), **res, bounds=np.array(sync.bounds))
+    dist.destroy_process_group()
+
+
+def test_two_rank_bf16_gradient_exchange(tmp_path):
+    """GradSync(exchange="bf16"): the decoder.9 / encoder.0 weight buckets travel and are summed in
+    bf16, the rest in fp32. Both ranks end with the same gradient; the bf16 buckets are within bf16
+    rounding of the fp32 exchange (a few 2^-9 of the tensor's max |g|), the fp32 bucket identical."""
+    port = _free_port()
+    mp.spawn(_exchange_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = np.load(tmp_path / "x0.npz"), np.load(tmp_path / "x1.npz")
+    np.testing.assert_array_equal(r0["bf16"], r1["bf16"])
+    np.testing.assert_array_equal(r0["f32"], r1["f32"])
+    b = r0["bounds"]
+    for k, (lo, hi) in enumerate(b):
+        ref, got = r0["f32"][lo:hi], r0["bf16"][lo:hi]
+        if k == 1:
+            np.testing.assert_array_equal(got, ref)
+        else:
+            assert np.abs(got - ref).max() <= 4 * 2.0 ** -9 * np.abs(ref).max()

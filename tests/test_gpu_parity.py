@@ -369,3 +369,37 @@ def test_staged_next_batch_bit_identical(prec, G, H, L, B):
     assert len(a) == len(b)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("G,B", [(16384, 256), (16500, 300)])
+def test_input_layer_quarter_launches_bit_identical(G, B):
+    """GM2_OPT_INPUT_CHUNKS = 4: the input-layer weight gradient as four row-quarter launches (one per
+    gradient bucket 2..5, for the data-parallel exchange) gives the same gradient bit for bit as the
+    single launch; the bucket bounds tile encoder.0.weight by quarters of its rows."""
+    H, L = 1024, 32
+    P, S = perturb_bn(*oracle_state(G, H, L, G + B), seed=12)
+    X = synth_x(B, G, 13)
+    eps = torch.randn(B, L, generator=torch.Generator().manual_seed(3)).cuda()
+    sc = scalars(beta=0.37, wgamma=0.0, lam=0.0)
+    old = native.get_option(native.OPT_INPUT_CHUNKS)
+    outs = []
+    try:
+        for chunks in (1, 4):
+            native.set_option(native.OPT_INPUT_CHUNKS, chunks)
+            m = to_model(P, S, G, H, L, native.GM2_BF16)
+            mat = ResidentMatrix(X)
+            ws = m.workspace(native.GM2_BF16, B)
+            grads = torch.zeros_like(m.params)
+            loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+            native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, B, eps), m.params, grads, m.bn, sc,
+                                 loss)
+            native.grad_norm(ws, m.params, grads, sc, loss)
+            torch.cuda.synchronize()
+            outs.append((grads.cpu(), loss.cpu()))
+    finally:
+        native.set_option(native.OPT_INPUT_CHUNKS, old)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])  # incl. the clip norm (statistics re-read when chunked)
+    bounds = native.grad_bucket_bounds(native.dims(G, H, L, B))
+    assert len(bounds) == native.GRAD_BUCKETS == 6
+    assert [b for b in bounds[2:]] == [(q * H // 4 * G, (q + 1) * H // 4 * G) for q in range(4)]
