@@ -538,8 +538,10 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     if (i == 0) {  // input layer: weight gradient only (on the main stream: nothing left to overlap)
       // dWe0[h][g] = sum_b dY0^T[h][b] X[b][g]: dY0^T (K-major copy) x X (MN-major)
       launch_transpose<T>(dY, H, Bp, H, c.t(l.dYT0), Bp, c.s);
-      if (sr) order(sr, w.s, c.s);  // join: every hidden-layer weight gradient is final
-      HIP_OK(hipEventRecord(be->ev[1], c.s));
+      // bucket 1 (every hidden-layer weight gradient) is final when the side stream's queue so far
+      // is; dWe0 starts without waiting for it (the join follows the dWe0 launch: the side stream's
+      // last small GEMM / column sums run beside dWe0's first tiles instead of before them)
+      HIP_OK(hipEventRecord(be->ev[1], w.s));
       if (input_chunked(bg, H)) {  // four row-quarter launches, bucket 2 + q final after launch q
         for (int q = 0; q < 4; ++q) {
           GemmArgs<T> gq = bg.g0;
@@ -555,6 +557,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
           gemm_to<T>(c, c.t(l.dYT0), Bp, H, c.t(c.xo), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0);
         for (int q = 0; q < 4; ++q) HIP_OK(hipEventRecord(be->ev[2 + q], c.s));
       }
+      if (sr) order(sr, w.s, c.s);  // join: the caller's stream sees every weight gradient
       if (nx) {  // the next batch's rows -> the other input slot, on the side stream after dWe0 (beside
                  // it, it only slows the GEMM down by its own length): under the data-parallel exchange
                  // of the input-layer gradient, or beside the clip / Adam passes on one GPU
