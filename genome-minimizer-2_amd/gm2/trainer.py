@@ -16,6 +16,8 @@ statistics are per rank (standard DDP); running statistics are averaged over ran
 """
 from __future__ import annotations
 
+import os
+
 import math
 from dataclasses import dataclass
 from typing import Dict, List, Tuple
@@ -221,7 +223,8 @@ class VAETrainer:
 
     def _grad_sync(self, dist):
         if self._sync is None or self._sync.dist is not dist:
-            self._sync = GradSync(dist, self.model, self.grads)
+            # GM2_GRAD_EXCHANGE=bf16 (main.py --grad-exchange): the big weight buckets in bf16
+            self._sync = GradSync(dist, self.model, self.grads, exchange=os.environ.get("GM2_GRAD_EXCHANGE", "f32"))
         return self._sync
 
     def _epoch_values(self, raw, pers, n_rows):

@@ -56,6 +56,8 @@ def parse_arguments(argv=None):
     p.add_argument("--noise-level", type=float, default=0.1)
     p.add_argument("--project-root", type=str, default=os.environ.get("GM2_PROJECT_ROOT", os.getcwd()))
     p.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
+    p.add_argument("--grad-exchange", choices=["f32", "bf16"], default=None,
+                   help="torchrun / DDP only: dtype of the big weight-gradient all-reduce (default f32)")
     p.add_argument("--mask-dtype", choices=["float64", "uint8", "bits"], default="float64")
     p.add_argument("--no-csv", action="store_true")
     p.add_argument("--genome-path", type=str, default=None,
@@ -272,6 +274,8 @@ def run_genome_minimizer(args):
 
 def main(argv=None):
     args = parse_arguments(argv)
+    if args.grad_exchange:
+        os.environ["GM2_GRAD_EXCHANGE"] = args.grad_exchange  # read by the trainer's gradient exchange
     dist = None
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         # torchrun: one process per GPU; bind the device and join the process group before any
