@@ -78,7 +78,8 @@ def parse():
     ap.add_argument("--sample-genomes", type=int, default=1000000)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-f32-line", action="store_true")
-    ap.add_argument("--no-prefetch", action="store_true", help="gather each batch inside its own step")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="N>1: gather each batch inside its own step (default: staged during the previous step)")
     ap.add_argument("--grad-exchange", choices=["f32", "bf16"], default="bf16",
                     help="N>1: dtype the big weight gradients are all-reduced in (gm2.ddp.GradSync)")
     ap.add_argument("--input-chunks", type=int, choices=[1, 4], default=None,
@@ -215,12 +216,15 @@ def main():
     sync = GradSync(dist, model, grads, exchange=a.grad_exchange) if dist is not None else None
     if a.input_chunks is not None:
         native.set_option(native.OPT_INPUT_CHUNKS, a.input_chunks)
+    # next-batch staging (gm2_batch.next) only under DDP, where the gather fills the wait for the
+    # input-layer exchange; on one GPU it measured ~30 us/step slower (profiles/r02_prefetch_ab_*)
+    prefetch = dist is not None and not a.no_prefetch
 
     def step(i):
         eps = torch.randn(B, L, device=dev)
         # the next step's rows are staged during this step's tail (gm2_batch.next; the last timed step
         # stages one batch nobody uses, so the timed region holds K gathers)
-        nxt = None if a.no_prefetch else native.make_batch(mat.data, mat.ld, rows[(i + 1) * B:(i + 2) * B], B, None)
+        nxt = native.make_batch(mat.data, mat.ld, rows[(i + 1) * B:(i + 2) * B], B, None) if prefetch else None
         batch = native.make_batch(mat.data, mat.ld, rows[i * B:(i + 1) * B], B, eps, next=nxt)
         native.train_fwd_bwd(ws, batch, model.params, grads, model.bn, scal[i], loss[i])
         if sync is not None:
@@ -275,7 +279,7 @@ def main():
                                      f"SUM all-reduce overlapped with the backward, input-layer gradient in "
                                      f"{native.get_option(native.OPT_INPUT_CHUNKS)} launch(es)")
                    if world > 1 else "none (one GPU)",
-                   "input_prefetch": not a.no_prefetch},
+                   "input_prefetch": prefetch},
         "train_tflops": round(value * train_flops_per_vector(G, H, L) / 1e12, 2),
         "nonfinite_steps": nonfinite,
         "roofline": {"bound": "mfma", "kernel": "k_gemm_recon_loss<bf16>" if prec == native.GM2_BF16

@@ -567,6 +567,11 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
         launch_gather_rows<T>(nx->b->data, nx->b->ld_data, nx->b->rows, Bn, G, c.t(nx->xo), Gp, Gp,
                               (int)round_up(Bn, kTile), (uint32_t*)(c.ws + nx->xbo), Gp / 32, gs);
         HIP_OK(hipEventRecord(nx->done, gs));
+        // joined back before the call returns: the caller's stream orders every write this call
+        // makes (workspace lifetime, device-wide syncs are not needed); the clip / Adam passes that
+        // follow wait for it, which measured time-neutral (both are HBM-bound) and keeps the gather
+        // beside the data-parallel exchange, which waits on bucket events instead
+        if (sr) order(sr, w.s, c.s);
       }
       be->recorded = true;
       break;
@@ -714,6 +719,7 @@ int gm2_workspace_init(const gm2_dims* d, int prec, void* ws, size_t ws_bytes, v
     const Layout lo = make_layout(d, prec);
     if ((size_t)lo.total > ws_bytes) throw Gm2Error("workspace too small: %zu < %lld", ws_bytes, (long long)lo.total);
     if ((uintptr_t)ws & 255) throw Gm2Error("workspace must be 256-B aligned");
+    drop_stage(ws, (hipStream_t)stream);  // a new (or reused) workspace holds no staged batch
     HIP_OK(hipMemsetAsync(ws, 0, (size_t)lo.total, (hipStream_t)stream));
   });
 }
