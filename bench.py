@@ -179,12 +179,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # (local % device count: lets a 1-GPU box rehearse the N>1 path with GM2_DIST_BACKEND=gloo;
+    # torch.cuda.device_count() does not initialise the GPU)
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("GM2_DIST_BACKEND", "nccl")  # nccl = RCCL; gloo only to rehearse
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from gm2 import native
     from gm2.data import ResidentMatrix, synthetic_pangenome
