@@ -1017,6 +1017,10 @@ int gm2_set_option(int key, int value) {
       case GM2_OPT_SMALL_SPLIT: set_small_split(value); break;
       case GM2_OPT_BN_EPILOGUE: set_bn_epilogue(value); break;
       case GM2_OPT_SMALL_WAVES: set_small_waves(value); break;
+      case GM2_OPT_SMALL_STAGES:
+        if (value != 4 && value != 5) throw Gm2Error("small stages %d: 4 or 5", value);
+        set_small_stages(value);
+        break;
       case GM2_OPT_INPUT_CHUNKS:
         if (value != 1 && value != 4) throw Gm2Error("input chunks %d: 1 or 4", value);
         input_chunks_flag().store(value);
@@ -1036,6 +1040,7 @@ int gm2_get_option(int key, int* value) {
       case GM2_OPT_BN_EPILOGUE: *value = get_bn_epilogue(); break;
       case GM2_OPT_SMALL_WAVES: *value = get_small_waves(); break;
       case GM2_OPT_INPUT_CHUNKS: *value = input_chunks_flag().load(); break;
+      case GM2_OPT_SMALL_STAGES: *value = get_small_stages(); break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });

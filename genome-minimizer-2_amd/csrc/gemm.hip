@@ -65,6 +65,9 @@ using SmallDeep = Cfg<128, 128, 2, 2, 4>;
 // The same tile with 8 waves (2x4, 64x32 each): two waves per SIMD, so one's LDS reads and waits
 // hide behind the other's MFMAs (GM2_OPT_SMALL_WAVES = 8)
 using SmallDeep8 = Cfg<128, 128, 2, 4, 4>;
+// Five stages (the whole 160 KB LDS): four K-steps in flight (GM2_OPT_SMALL_STAGES = 5)
+using SmallDeep5 = Cfg<128, 128, 2, 2, 5>;
+using SmallDeep85 = Cfg<128, 128, 2, 4, 5>;
 
 struct TileXY {
   int m0, n0, split, t;
@@ -184,8 +187,9 @@ __device__ __forceinline__ f32x4 frag_f32(const char* tile, int r0, int s, int l
 // Wait until at most `r` (0 <= r <= NS - 2; negative = 0) later stages' loads are in flight.
 template <class C>
 __device__ __forceinline__ void wait_stages(int r) {
-  static_assert(C::NS <= 4 && 2 * C::LPS <= 63, "vmcnt range");
-  if (C::NS >= 4 && r >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C::LPS) : "memory");
+  static_assert(C::NS <= 5 && 3 * C::LPS <= 63, "vmcnt range");
+  if (C::NS >= 5 && r >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * C::LPS) : "memory");
+  else if (C::NS >= 4 && r >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C::LPS) : "memory");
   else if (C::NS >= 3 && r >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::LPS) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -1129,6 +1133,22 @@ static std::atomic<int>& small_waves_flag() {
 void set_small_waves(int w) { small_waves_flag().store(w == 8 ? 8 : 4, std::memory_order_relaxed); }
 int get_small_waves() { return small_waves_flag().load(std::memory_order_relaxed); }
 
+// LDS ring depth of those tiles (GM2_OPT_SMALL_STAGES: 4 or 5)
+static std::atomic<int>& small_stages_flag() {
+  static std::atomic<int> v{4};
+  return v;
+}
+void set_small_stages(int n) { small_stages_flag().store(n == 5 ? 5 : 4, std::memory_order_relaxed); }
+int get_small_stages() { return small_stages_flag().load(std::memory_order_relaxed); }
+
+// call f(Cfg{}) with the 128x128 fp32-store tile configuration the options select
+template <class F>
+static auto small_cfg(F&& f) {
+  const bool w8 = small_waves_flag().load(std::memory_order_relaxed) == 8;
+  if (small_stages_flag().load(std::memory_order_relaxed) == 5) return w8 ? f(SmallDeep85{}) : f(SmallDeep5{});
+  return w8 ? f(SmallDeep8{}) : f(SmallDeep{});
+}
+
 // hipFuncAttributeMaxDynamicSharedMemorySize is per device: remember (device, kernel) pairs
 static void ensure_lds_attr(const void* fn, int bytes) {
   static std::mutex mu;
@@ -1188,9 +1208,7 @@ int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
     return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
   }
   check_gemm(g, 128);
-  if (small_waves_flag().load(std::memory_order_relaxed) == 8)
-    return store_impl<SmallDeep8, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
-  return store_impl<SmallDeep, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
+  return small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s); });
 }
 
 template <typename T>
@@ -1212,10 +1230,7 @@ bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hip
     store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
   } else {
     check_gemm(g, 128);
-    if (small_waves_flag().load(std::memory_order_relaxed) == 8)
-      store_impl<SmallDeep8, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
-    else
-      store_impl<SmallDeep, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
+    small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s); });
   }
   return true;
 }
@@ -1231,10 +1246,7 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
     store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
   } else {
     check_gemm(g, 128);
-    if (small_waves_flag().load(std::memory_order_relaxed) == 8)
-      store_impl<SmallDeep8, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
-    else
-      store_impl<SmallDeep, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
+    small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s); });
   }
   return true;
 }
@@ -1255,10 +1267,7 @@ bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bi
   const GemmPlan p = plan_gemm(g);
   if (p.tile != 128 || p.splits != 1 || (bn.mode && (g.N % 4 || bn.ldy % 4))) return false;
   check_gemm(g, 128);
-  if (small_waves_flag().load(std::memory_order_relaxed) == 8)
-    store_impl<SmallDeep8, T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s);
-  else
-    store_impl<SmallDeep, T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s);
+  small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s); });
   return true;
 }
 

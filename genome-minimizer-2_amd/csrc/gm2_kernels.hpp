@@ -129,6 +129,8 @@ void set_small_split(int s);
 int get_small_split();
 void set_small_waves(int w);
 int get_small_waves();
+void set_small_stages(int n);
+int get_small_stages();
 struct GemmPlan {
   int tile, splits;
 };

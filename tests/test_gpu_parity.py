@@ -403,3 +403,38 @@ def test_input_layer_quarter_launches_bit_identical(G, B):
     bounds = native.grad_bucket_bounds(native.dims(G, H, L, B))
     assert len(bounds) == native.GRAD_BUCKETS == 6
     assert [b for b in bounds[2:]] == [(q * H // 4 * G, (q + 1) * H // 4 * G) for q in range(4)]
+
+
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+@pytest.mark.parametrize("waves", [4, 8])
+def test_small_tile_ring_depth_bit_identical(prec, waves):
+    """GM2_OPT_SMALL_STAGES: the 5-stage LDS ring of the 128x128 tiles (four K-steps in flight, the
+    whole 160 KB) changes only when operands arrive, not the arithmetic: the step is bit-identical
+    to the 4-stage ring, for both wave counts of those tiles."""
+    G, H, L, B = 1000, 256, 32, 300
+    P, S = perturb_bn(*oracle_state(G, H, L, G + B), seed=21)
+    X = synth_x(B, G, 22)
+    eps = torch.randn(B, L, generator=torch.Generator().manual_seed(23)).cuda()
+    pr = native.GM2_F32 if prec == "f32" else native.GM2_BF16
+    sc = scalars(beta=0.37, wgamma=0.55, lam=0.01)
+    olds, oldw = native.get_option(native.OPT_SMALL_STAGES), native.get_option(native.OPT_SMALL_WAVES)
+    outs = []
+    try:
+        native.set_option(native.OPT_SMALL_WAVES, waves)
+        for st in (4, 5):
+            native.set_option(native.OPT_SMALL_STAGES, st)
+            m = to_model(P, S, G, H, L, pr)
+            mat = ResidentMatrix(X)
+            ws = m.workspace(pr, B)
+            grads = torch.zeros_like(m.params)
+            loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+            native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, B, eps), m.params, grads, m.bn, sc,
+                                 loss)
+            native.grad_norm(ws, m.params, grads, sc, loss)
+            torch.cuda.synchronize()
+            outs.append((grads.cpu(), loss.cpu(), m.bn.cpu()))
+    finally:
+        native.set_option(native.OPT_SMALL_STAGES, olds)
+        native.set_option(native.OPT_SMALL_WAVES, oldw)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
