@@ -82,6 +82,8 @@ def parse():
                     help="N>1: gather each batch inside its own step (default: staged during the previous step)")
     ap.add_argument("--grad-exchange", choices=["f32", "bf16"], default="bf16",
                     help="N>1: dtype the big weight gradients are all-reduced in (gm2.ddp.GradSync)")
+    ap.add_argument("--grid-cap", type=int, choices=[0, 1], default=None,
+                    help="capped grid for the output-layer weight-gradient GEMM (GM2_OPT_GRID_CAP)")
     ap.add_argument("--small-stages", type=int, choices=[4, 5], default=None,
                     help="LDS ring depth of the 128x128 hidden-layer GEMM tiles (GM2_OPT_SMALL_STAGES)")
     ap.add_argument("--input-chunks", type=int, choices=[1, 4], default=None,
@@ -227,6 +229,8 @@ def main():
         native.set_option(native.OPT_INPUT_CHUNKS, a.input_chunks)
     if a.small_stages is not None:
         native.set_option(native.OPT_SMALL_STAGES, a.small_stages)
+    if a.grid_cap is not None:
+        native.set_option(native.OPT_GRID_CAP, a.grid_cap)
     # next-batch staging (gm2_batch.next) only under DDP, where the gather fills the wait for the
     # input-layer exchange; on one GPU it measured ~30 us/step slower (profiles/r02_prefetch_ab_*)
     prefetch = dist is not None and not a.no_prefetch

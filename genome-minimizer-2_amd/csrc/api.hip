@@ -454,9 +454,6 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
                   norm_hdr ? (int*)(c.ws + l.nahdr) : nullptr, na_ok, na_n, c.s);
 }
 
-// Backward. Every operand is read in the layout its producer wrote: weight gradients use MN-major P
-// and Q (dW[out][in] = sum_b dY[b][out] * in[b][in]), input gradients an MN-major weight
-// (dX[b][in] = sum_out dY[b][out] * W[out][in]); no transposed copy exists anywhere.
 // The next training batch's gather, staged into the other input slot (gm2_batch.next)
 struct NextStage {
   const gm2_batch* b = nullptr;
@@ -464,6 +461,9 @@ struct NextStage {
   hipEvent_t done = nullptr;
 };
 
+// Backward. Every operand is read in the layout its producer wrote: weight gradients use MN-major P
+// and Q (dW[out][in] = sum_b dY[b][out] * in[b][in]), input gradients an MN-major weight
+// (dX[b][in] = sum_out dY[b][out] * W[out][in]); no transposed copy exists anywhere.
 template <typename T>
 void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, const float* scal,
               const float* dmu_ext = nullptr, const float* dlv_ext = nullptr, int train = 1,
@@ -494,6 +494,8 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   {
     const GemmArgs<T>& g9 = bg.g9;
     if (plan_gemm<T>(g9).splits == 1) {
+      // (A5^T here on the side stream; on the main stream before the fork measured ~35 us/step
+      // slower, profiles/r02_a5t_placement_ab.txt)
       launch_transpose<T>(c.t(l.A[5]), H, Bp, H, c.t(l.AT5), Bp, w.s);
       launch_gemm_trans<T>(g9, gr + d.off[D9W], H, w.s, bg.direct ? nasq : nullptr);
     } else {
@@ -1017,6 +1019,7 @@ int gm2_set_option(int key, int value) {
       case GM2_OPT_SMALL_SPLIT: set_small_split(value); break;
       case GM2_OPT_BN_EPILOGUE: set_bn_epilogue(value); break;
       case GM2_OPT_SMALL_WAVES: set_small_waves(value); break;
+      case GM2_OPT_GRID_CAP: set_grid_cap(value); break;
       case GM2_OPT_SMALL_STAGES:
         if (value != 4 && value != 5) throw Gm2Error("small stages %d: 4 or 5", value);
         set_small_stages(value);
@@ -1041,6 +1044,7 @@ int gm2_get_option(int key, int* value) {
       case GM2_OPT_SMALL_WAVES: *value = get_small_waves(); break;
       case GM2_OPT_INPUT_CHUNKS: *value = input_chunks_flag().load(); break;
       case GM2_OPT_SMALL_STAGES: *value = get_small_stages(); break;
+      case GM2_OPT_GRID_CAP: *value = get_grid_cap(); break;
       default: throw Gm2Error("unknown option %d", key);
     }
   });

@@ -23,6 +23,7 @@
 
 #include <atomic>
 #include <cstdlib>
+#include <map>
 #include <mutex>
 #include <set>
 #include <type_traits>
@@ -451,12 +452,35 @@ __device__ __forceinline__ double sq4(float a, float b, float c, float d) {
 }
 
 template <class C, typename T, bool AK, bool BK, bool PP>
+__device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g, float* __restrict__ C0,
+                                           float* __restrict__ C1, int msplit, int64_t ldc, int64_t slab,
+                                           const float* __restrict__ bias, const StoreEpi& bn, char* smem);
+
+template <class C, typename T, bool AK, bool BK, bool PP>
 __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __restrict__ C0, float* __restrict__ C1,
                                                     int msplit, int64_t ldc, int64_t slab,
                                                     const float* __restrict__ bias, StoreEpi bn) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   GM2_STAMP(0);
-  const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
+  const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
+  if (bn.ntiles == 0) {  // one tile per workgroup
+    store_tile<C, T, AK, BK, PP>(tile_of<C>(tm, tn), g, C0, C1, msplit, ldc, slab, bias, bn, smem);
+    return;
+  }
+  // capped grid (one K pass): workgroup wg takes logical tiles wg, wg + grid, ... (every wave of
+  // the block runs the same trip count; the LDS is reused after a barrier)
+  const int ntile = tm * tn;
+  for (int t = xcd_wg(); t < bn.ntiles; t += gridDim.x) {
+    __syncthreads();
+    store_tile<C, T, AK, BK, PP>(tile_at<C>(t % ntile, tm, tn, t / ntile), g, C0, C1, msplit, ldc, slab, bias, bn,
+                                 smem);
+  }
+}
+
+template <class C, typename T, bool AK, bool BK, bool PP>
+__device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g, float* __restrict__ C0,
+                                           float* __restrict__ C1, int msplit, int64_t ldc, int64_t slab,
+                                           const float* __restrict__ bias, const StoreEpi& bn, char* smem) {
   const int kbeg = tl.split * g.k_per_split;
   const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = (kend - kbeg) / E<T>::KT;
@@ -1149,6 +1173,16 @@ static auto small_cfg(F&& f) {
   return w8 ? f(SmallDeep8{}) : f(SmallDeep{});
 }
 
+// GM2_OPT_GRID_CAP: the output-layer weight-gradient GEMM (side stream, beside the hidden-layer
+// backward chain) on a capped grid -- same rounds, the last round's idle CUs free for the chain
+static std::atomic<int>& big_grid_cap_flag() {
+  static std::atomic<int> v{0};  // 1 measured 20-40 us/step slower: the chain's 256-tile GEMMs get
+                                 // 41 CUs (6 rounds) while dW9 runs (profiles/r02_grid_cap_ab_*)
+  return v;
+}
+void set_grid_cap(int on) { big_grid_cap_flag().store(on ? 1 : 0, std::memory_order_relaxed); }
+int get_grid_cap() { return big_grid_cap_flag().load(std::memory_order_relaxed); }
+
 // hipFuncAttributeMaxDynamicSharedMemorySize is per device: remember (device, kernel) pairs
 static void ensure_lds_attr(const void* fn, int bytes) {
   static std::mutex mu;
@@ -1162,12 +1196,34 @@ static void ensure_lds_attr(const void* fn, int bytes) {
   done.insert({dev, fn});
 }
 
+// compute units of the current device (cached per device)
+static int device_cus() {
+  static std::mutex mu;
+  static std::map<int, int> cus;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) throw Gm2Error("hipGetDevice");
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cus.find(dev);
+  if (it != cus.end()) return it->second;
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    throw Gm2Error("hipDeviceGetAttribute(MultiprocessorCount)");
+  return cus[dev] = std::max(n, 1);
+}
+
 template <class C, typename T, bool AK, bool BK, bool PP>
 static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
                            const float* bias, const StoreEpi& bn, hipStream_t s) {
   ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP>, C::LDS);
-  hipLaunchKernelGGL((k_gemm_store<C, T, AK, BK, PP>), dim3(tiles), dim3(C::NT), C::LDS, s, a, C0, C1 ? C1 : C0,
-                     C1 ? msplit : (1 << 30), ldc, slab, bias, bn);
+  int grid = tiles;
+  StoreEpi ep = bn;
+  if (bn.ntiles) {  // capped grid: the same number of rounds on fewer CUs
+    const int cus = device_cus(), rounds = (tiles + cus - 1) / cus;
+    grid = (tiles + rounds - 1) / rounds;
+    ep.ntiles = grid < tiles ? tiles : 0;
+  }
+  hipLaunchKernelGGL((k_gemm_store<C, T, AK, BK, PP>), dim3(grid), dim3(C::NT), C::LDS, s, a, C0, C1 ? C1 : C0,
+                     C1 ? msplit : (1 << 30), ldc, slab, bias, ep);
 }
 
 template <class C, typename T, bool AK, bool BK>
@@ -1241,6 +1297,7 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
   StoreEpi ep;
   ep.trans = 1;
   ep.sq = sq;
+  ep.ntiles = big_grid_cap_flag().load(std::memory_order_relaxed);  // (the launcher sets the count)
   if (use_big(g)) {
     check_gemm(g, 256);
     store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);

@@ -95,6 +95,10 @@ struct StoreEpi {
   // (m0 / BM) * (Np / BN) + n0 / BN -- the clip-norm statistics of a weight gradient taken as it is
   // written (gm2_grad_norm with GM2_S_NORM_AHEAD)
   double* sq = nullptr;
+  // > 0: the launch has fewer workgroups than tiles and each loops over tiles wg, wg + grid, ...
+  // (grid = ceil(tiles / rounds) for the same number of rounds: the idle CUs of the last round
+  // become free CUs for the other stream's work for the whole launch)
+  int ntiles = 0;
 };
 // GEMM + BatchNorm statistics of its output in one launch when the plan allows (one K pass of
 // 128-row tiles); returns false (nothing launched) otherwise
@@ -131,6 +135,8 @@ void set_small_waves(int w);
 int get_small_waves();
 void set_small_stages(int n);
 int get_small_stages();
+void set_grid_cap(int on);
+int get_grid_cap();
 struct GemmPlan {
   int tile, splits;
 };

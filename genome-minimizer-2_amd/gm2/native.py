@@ -32,7 +32,7 @@ EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_of
            "gm2_gemm", "gm2_grad_bucket_bounds", "gm2_wait_grad_bucket", "gm2_set_option", "gm2_get_option", "gm2_timing_begin", "gm2_timing_end"]
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
 OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE, OPT_SMALL_SPLIT, OPT_BN_EPILOGUE, OPT_SMALL_WAVES = 1, 2, 3, 4, 5, 6
-OPT_INPUT_CHUNKS, OPT_SMALL_STAGES = 7, 8
+OPT_INPUT_CHUNKS, OPT_SMALL_STAGES, OPT_GRID_CAP = 7, 8, 9
 
 
 class Dims(C.Structure):

@@ -438,3 +438,35 @@ def test_small_tile_ring_depth_bit_identical(prec, waves):
         native.set_option(native.OPT_SMALL_WAVES, oldw)
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("G", [20480, 20000])
+def test_capped_grid_bit_identical(G):
+    """GM2_OPT_GRID_CAP: the output-layer weight-gradient GEMM on a capped grid (workgroups loop over
+    tiles: 320 tiles -> 160 workgroups x 2 at G = 20480) gives the same gradient, loss record and
+    clip statistics bit for bit as one workgroup per tile; G = 20000 takes the 128-tile plan."""
+    H, L, B = 1024, 32, 256
+    P, S = perturb_bn(*oracle_state(G, H, L, G + B), seed=31)
+    X = synth_x(B, G, 32)
+    eps = torch.randn(B, L, generator=torch.Generator().manual_seed(33)).cuda()
+    sc = scalars(beta=0.37, wgamma=0.55, lam=0.0)
+    sc[native.S_NORM_AHEAD] = 1.0
+    old = native.get_option(native.OPT_GRID_CAP)
+    outs = []
+    try:
+        for cap in (0, 1):
+            native.set_option(native.OPT_GRID_CAP, cap)
+            m = to_model(P, S, G, H, L, native.GM2_BF16)
+            mat = ResidentMatrix(X)
+            ws = m.workspace(native.GM2_BF16, B)
+            grads = torch.zeros_like(m.params)
+            loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+            native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, B, eps), m.params, grads, m.bn, sc,
+                                 loss)
+            native.grad_norm(ws, m.params, grads, sc, loss)
+            torch.cuda.synchronize()
+            outs.append((grads.cpu(), loss.cpu()))
+    finally:
+        native.set_option(native.OPT_GRID_CAP, old)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
