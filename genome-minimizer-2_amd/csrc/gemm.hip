@@ -1173,14 +1173,16 @@ static auto small_cfg(F&& f) {
   return w8 ? f(SmallDeep8{}) : f(SmallDeep{});
 }
 
-// GM2_OPT_GRID_CAP: the output-layer weight-gradient GEMM (side stream, beside the hidden-layer
-// backward chain) on a capped grid -- same rounds, the last round's idle CUs free for the chain
+// GM2_OPT_GRID_CAP bits: 1 = the output-layer weight-gradient GEMM (side stream, beside the
+// hidden-layer backward chain), 2 = the input-layer one (beside the side stream's last hidden-layer
+// weight gradients) on a capped grid -- same rounds, the last round's idle CUs free for the rest
 static std::atomic<int>& big_grid_cap_flag() {
-  static std::atomic<int> v{0};  // 1 measured 20-40 us/step slower: the chain's 256-tile GEMMs get
-                                 // 41 CUs (6 rounds) while dW9 runs (profiles/r02_grid_cap_ab_*)
+  // 2 (dWe0 only): -18 us/step; bit 1 (dW9) measured 20-40 us/step slower: the chain's 256-tile
+  // GEMMs get 41 CUs (6 rounds) while dW9 runs (profiles/r02_grid_cap_ab_*)
+  static std::atomic<int> v{2};
   return v;
 }
-void set_grid_cap(int on) { big_grid_cap_flag().store(on ? 1 : 0, std::memory_order_relaxed); }
+void set_grid_cap(int bits) { big_grid_cap_flag().store(bits & 3, std::memory_order_relaxed); }
 int get_grid_cap() { return big_grid_cap_flag().load(std::memory_order_relaxed); }
 
 // hipFuncAttributeMaxDynamicSharedMemorySize is per device: remember (device, kernel) pairs
@@ -1281,6 +1283,7 @@ bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hip
   if (force_big && !big) return false;
   StoreEpi ep;
   ep.sq = sq;
+  ep.ntiles = (big_grid_cap_flag().load(std::memory_order_relaxed) & 2) && !force_big;  // dWe0 bit
   if (big) {
     check_gemm(g, 256);
     store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
@@ -1297,7 +1300,7 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
   StoreEpi ep;
   ep.trans = 1;
   ep.sq = sq;
-  ep.ntiles = big_grid_cap_flag().load(std::memory_order_relaxed);  // (the launcher sets the count)
+  ep.ntiles = big_grid_cap_flag().load(std::memory_order_relaxed) & 1;  // dW9 bit (the launcher sets the count)
   if (use_big(g)) {
     check_gemm(g, 256);
     store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);

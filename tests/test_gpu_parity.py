@@ -454,7 +454,7 @@ def test_capped_grid_bit_identical(G):
     old = native.get_option(native.OPT_GRID_CAP)
     outs = []
     try:
-        for cap in (0, 1):
+        for cap in (0, 3):
             native.set_option(native.OPT_GRID_CAP, cap)
             m = to_model(P, S, G, H, L, native.GM2_BF16)
             mat = ResidentMatrix(X)
