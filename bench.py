@@ -82,8 +82,8 @@ def parse():
                     help="N>1: gather each batch inside its own step (default: staged during the previous step)")
     ap.add_argument("--grad-exchange", choices=["f32", "bf16"], default="bf16",
                     help="N>1: dtype the big weight gradients are all-reduced in (gm2.ddp.GradSync)")
-    ap.add_argument("--grid-cap", type=int, choices=[0, 1, 2, 3], default=None,
-                    help="capped grid bits for the output- (1) / input-layer (2) weight-gradient GEMMs")
+    ap.add_argument("--grid-cap", type=int, choices=range(8), default=None,
+                    help="capped grid bits: output- (1) / input-layer (2) weight-gradient GEMMs, recon (4)")
     ap.add_argument("--small-stages", type=int, choices=[4, 5], default=None,
                     help="LDS ring depth of the 128x128 hidden-layer GEMM tiles (GM2_OPT_SMALL_STAGES)")
     ap.add_argument("--input-chunks", type=int, choices=[1, 4], default=None,

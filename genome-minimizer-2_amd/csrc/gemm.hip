@@ -822,16 +822,42 @@ __device__ __forceinline__ void recon_pad_const(float& e0, float& p0) {
 }
 
 template <class C, typename T, bool PP, bool GRAD>
+__device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<T>& g, const float* __restrict__ bias,
+                                                const uint32_t* __restrict__ xbits, int64_t ldxb,
+                                                const float* __restrict__ scal, T* __restrict__ dL, int64_t ldd,
+                                                float* __restrict__ loss_part, float* __restrict__ colpart,
+                                                int64_t ldcol, char* smem);
+
+// ntiles > 0: capped grid, workgroup wg takes tiles wg, wg + grid, ... (GM2_OPT_GRID_CAP bit 4)
+template <class C, typename T, bool PP, bool GRAD>
 __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const float* __restrict__ bias,
                                                          const uint32_t* __restrict__ xbits, int64_t ldxb,
-                                                         int with_grad, const float* __restrict__ scal,
+                                                         int ntiles, const float* __restrict__ scal,
                                                          T* __restrict__ dL, int64_t ldd,
                                                          float* __restrict__ loss_part, float* __restrict__ colpart,
                                                          int64_t ldcol) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr bool FAST = sizeof(T) == 2;
   const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
-  const TileXY tl = tile_of<C>(tm, tn);  // m = genes, n = strains
+  if (ntiles == 0) {
+    recon_loss_tile<C, T, PP, GRAD>(tile_of<C>(tm, tn), g, bias, xbits, ldxb, scal, dL, ldd, loss_part, colpart,
+                                    ldcol, smem);
+    return;
+  }
+  for (int t = xcd_wg(); t < ntiles; t += gridDim.x) {
+    __syncthreads();
+    recon_loss_tile<C, T, PP, GRAD>(tile_at<C>(t, tm, tn, 0), g, bias, xbits, ldxb, scal, dL, ldd, loss_part,
+                                    colpart, ldcol, smem);
+  }
+}
+
+template <class C, typename T, bool PP, bool GRAD>
+__device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<T>& g, const float* __restrict__ bias,
+                                                const uint32_t* __restrict__ xbits, int64_t ldxb,
+                                                const float* __restrict__ scal, T* __restrict__ dL, int64_t ldd,
+                                                float* __restrict__ loss_part, float* __restrict__ colpart,
+                                                int64_t ldcol, char* smem) {
+  constexpr bool FAST = sizeof(T) == 2;
+  // (m = genes, n = strains)
   // LDS: [0, image / staging) | per-row-group dl sums | BCE, sum(p) slots | bias slice
   constexpr int EPC = 16 / sizeof(T);
   constexpr int PR = C::BM + 8;
@@ -1182,7 +1208,7 @@ static std::atomic<int>& big_grid_cap_flag() {
   static std::atomic<int> v{2};
   return v;
 }
-void set_grid_cap(int bits) { big_grid_cap_flag().store(bits & 3, std::memory_order_relaxed); }
+void set_grid_cap(int bits) { big_grid_cap_flag().store(bits & 7, std::memory_order_relaxed); }
 int get_grid_cap() { return big_grid_cap_flag().load(std::memory_order_relaxed); }
 
 // hipFuncAttributeMaxDynamicSharedMemorySize is per device: remember (device, kernel) pairs
@@ -1353,10 +1379,17 @@ static void recon_impl_k(const GemmArgs<T>& g, const float* bias, const uint32_t
   if (ldx * 32 < g.Mp || (ldx & 3)) throw Gm2Error("recon: target bit rows too short");
   constexpr int lds = recon_lds_bytes<C, T>();
   static_assert(lds <= 160 * 1024, "LDS budget");
+  const int tiles = (g.Mp / C::BM) * (g.Np / C::BN);
+  int grid = tiles, ntiles = 0;
+  if (big_grid_cap_flag().load(std::memory_order_relaxed) & 4) {  // same rounds on fewer workgroups
+    const int cus = device_cus(), rounds = (tiles + cus - 1) / cus;
+    grid = (tiles + rounds - 1) / rounds;
+    ntiles = grid < tiles ? tiles : 0;
+  }
   auto go = [&](auto kern) {
     ensure_lds_attr((const void*)kern, lds);
-    hipLaunchKernelGGL(kern, dim3((g.Mp / C::BM) * (g.Np / C::BN)), dim3(C::NT), lds, s, g, bias, X, ldx, with_grad,
-                       scal, dL, ldd, loss_part, colpart, ldcol);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(C::NT), lds, s, g, bias, X, ldx, ntiles, scal, dL, ldd, loss_part,
+                       colpart, ldcol);
   };
   if (with_grad) go(k_gemm_recon_loss<C, T, PP, true>);
   else go(k_gemm_recon_loss<C, T, PP, false>);

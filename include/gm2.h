@@ -240,8 +240,8 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *   GM2_OPT_SMALL_WAVES waves per workgroup (4 or 8) of the 128x128 fp32-store GEMM tiles (the
  *                       hidden-layer GEMMs).
  *   GM2_OPT_SMALL_STAGES LDS ring depth (4 or 5) of those 128x128 tiles: K-steps in flight.
- *   GM2_OPT_GRID_CAP    bit 1 = the output-layer, bit 2 = the input-layer weight-gradient GEMM
- *                       runs on a capped grid (workgroups loop over tiles; same rounds, fewer CUs)
+ *   GM2_OPT_GRID_CAP    bit 1 = the output-layer, bit 2 = the input-layer weight-gradient GEMM,
+ *                       bit 4 = the output-layer loss GEMM runs on a capped grid (workgroups loop over tiles; same rounds, fewer CUs)
  *                       so the work beside it keeps CUs (default 2); 0 = one workgroup per tile.
  *   GM2_OPT_INPUT_CHUNKS 1 (default) or 4: launches of the input-layer weight-gradient GEMM, one
  *                       per gradient bucket 2..5 (when H/4 is a multiple of 256; else 1). Same

@@ -443,9 +443,10 @@ def test_small_tile_ring_depth_bit_identical(prec, waves):
 @pytest.mark.parametrize("G", [20480, 20000])
 def test_capped_grid_bit_identical(G):
     """GM2_OPT_GRID_CAP: the output-layer weight-gradient GEMM on a capped grid (workgroups loop over
-    tiles: 320 tiles -> 160 workgroups x 2 at G = 20480) gives the same gradient, loss record and
-    clip statistics bit for bit as one workgroup per tile; G = 20000 takes the 128-tile plan."""
-    H, L, B = 1024, 32, 256
+    tiles: 320 tiles -> 160 workgroups x 2 at G = 20480), the input-layer one and the output-layer
+    loss GEMM (320 genes x strains tiles) give the same gradient, loss record and clip statistics bit
+    for bit as one workgroup per tile; G = 20000 takes the 128-tile plans."""
+    H, L, B = 1024, 32, 1024
     P, S = perturb_bn(*oracle_state(G, H, L, G + B), seed=31)
     X = synth_x(B, G, 32)
     eps = torch.randn(B, L, generator=torch.Generator().manual_seed(33)).cuda()
@@ -454,7 +455,7 @@ def test_capped_grid_bit_identical(G):
     old = native.get_option(native.OPT_GRID_CAP)
     outs = []
     try:
-        for cap in (0, 3):
+        for cap in (0, 7):
             native.set_option(native.OPT_GRID_CAP, cap)
             m = to_model(P, S, G, H, L, native.GM2_BF16)
             mat = ResidentMatrix(X)
