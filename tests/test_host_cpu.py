@@ -28,6 +28,32 @@ def test_library_exports_every_declared_symbol():
     assert sorted(native.EXPORTS) == names
 
 
+def test_header_constants_match_binding():
+    """The ctypes mirror (gm2/native.py) uses the values include/gm2.h defines: ABI version, gradient
+    bucket count, option keys, the gm2_batch field order (ABI 2 adds `next`); option setters accept
+    and reject values without a GPU, and the bucket bounds tile the gradient buffer in order."""
+    from gm2 import native
+    txt = open(os.path.join(ROOT, "include", "gm2.h")).read()
+    assert int(re.search(r"#define GM2_ABI_VERSION (\d+)", txt).group(1)) == native.lib().gm2_abi_version() == 2
+    assert int(re.search(r"#define GM2_GRAD_BUCKETS (\d+)", txt).group(1)) == native.GRAD_BUCKETS
+    opts = dict((k, int(v)) for k, v in re.findall(r"GM2_OPT_([A-Z_]+) = (\d+)", txt))
+    for k, v in opts.items():
+        assert getattr(native, "OPT_" + k) == v, k
+    assert [f[0] for f in native.Batch._fields_] == ["data", "ld_data", "rows", "n", "eps", "next"]
+    native.set_option(native.OPT_INPUT_CHUNKS, 4)
+    assert native.get_option(native.OPT_INPUT_CHUNKS) == 4
+    native.set_option(native.OPT_INPUT_CHUNKS, 1)
+    with pytest.raises(RuntimeError, match="1 or 4"):
+        native.set_option(native.OPT_INPUT_CHUNKS, 2)
+    with pytest.raises(RuntimeError, match="4 or 5"):
+        native.set_option(native.OPT_SMALL_STAGES, 3)
+    G, H, L = 55039, 1024, 64
+    b = native.grad_bucket_bounds(native.dims(G, H, L, 4096))
+    cover = sorted(b)
+    assert cover[0][0] == 0 and cover[-1][1] == native.param_offsets(G, H, L)[-1]
+    assert all(cover[i][1] == cover[i + 1][0] for i in range(len(cover) - 1))
+
+
 def test_layout_queries_and_errors():
     from gm2 import native
     G, H, L = 55039, 1024, 64
