@@ -16,7 +16,10 @@ lines of `sample_from_model` (extras.py:192-203) and the two `train_test_split` 
 `VAE.decode` / sklearn, exactly as those call sites do.
 
 Every fixture records torch.__version__ and the thread count (1): reference training is
-bit-deterministic only at a fixed thread count.
+bit-deterministic only at a fixed thread count. It also records the CPU model, the
+ATen dispatch level and MKL_CBWR=COMPATIBLE, the MKL code path the fixtures were made on: MKL's
+default path differs between Intel and AMD hosts (1-ulp differences in every GEMM), COMPATIBLE is
+the same on both, and tests/conftest.py selects it for the CPU suite.
 
 Outputs are small .npz files (inputs + expected outputs, i.e. data, no reference source).
 """
@@ -28,9 +31,13 @@ import sys
 import numpy as np
 
 REF = "/root/reference"
-OUT = os.path.dirname(os.path.abspath(__file__))
+OUT = os.environ.get("GM2_GOLDEN_OUT") or os.path.dirname(os.path.abspath(__file__))
 sys.dont_write_bytecode = True
 sys.path.insert(0, REF)
+# MKL picks its sgemm code path per CPU vendor/ISA, so the reference's fp32 bits differ between an
+# Intel and an AMD host by ~1 ulp. The COMPATIBLE branch (conditional numerical reproducibility) is
+# the one MKL honours on every x86 vendor; it must be set before the first MKL call.
+os.environ["MKL_CBWR"] = "COMPATIBLE"
 
 import torch  # noqa: E402
 
@@ -42,8 +49,21 @@ from src.genome_minimizer_2.training.training import loss_components as LC  # no
 from torch.utils.data import DataLoader, TensorDataset  # noqa: E402
 from sklearn.model_selection import train_test_split  # noqa: E402
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 META = {"torch": torch.__version__, "threads": 1, "numpy": np.__version__,
-        "generator": "tests/golden/make_golden.py"}
+        "generator": "tests/golden/make_golden.py", "cpu": _cpu_model(),
+        "aten_cpu_capability": torch.backends.cpu.get_cpu_capability(),
+        "mkl_cbwr": os.environ["MKL_CBWR"]}
 
 PRESET_HP = {
     # experiments.py:42-114 (hyper-parameters only; dims are shrunk for fixtures)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel summary of rocprofv3 runs of bench.py (tools/prof_r2.sh):
+"""Per-kernel summary of rocprofv3 runs of bench.py (tools/prof.sh):
 
   * time per training step by kernel (kernel trace of the timed steps: every dispatch between the
     first and last gm2 recon-loss launch, divided by the number of steps);
