@@ -8,18 +8,25 @@ whole hot path of trainer.py:109-120 on one batch: row gather, encoder/decoder f
 train-mode BatchNorm, reparameterisation, fused BCE/KL epilogues, full backward, gradient norm +
 clip, Adam. N>1 (torchrun): one process per GPU, each rank steps its own 4096 rows, gradients
 SUM-all-reduced over RCCL every step (weak scaling: value = all ranks' rows / max-rank time).
+`python bench.py --gpus N` without a torchrun environment launches the N ranks itself (a child
+`torch.distributed.run` process; this parent never touches the GPU) and exits with its code.
 
 Also reported (extra fields, not `value`): sampling throughput of `--mode sample` for the v1 preset
 (C3: 1e6 genomes/s decoded in exact fp32, thresholded into packed masks, essential genes counted on
 the device, masks + counts copied to pinned host memory), the same training step in the other GEMM
 precision (f32 next to the bf16 headline), the live-timed dominant kernel against the MFMA roofline,
 and the CPU baseline (the oracle = the reference's algorithm on torch-CPU, fp32, all host threads,
-the same v0 step at batch 4096 on the same matrix; plus the C1 batch-64 point).
+the same v0 step at batch 4096 on the same matrix; plus the C1 batch-64 point), and the C5-shaped
+step (configs[4]: v0 on the synthetic 100k-strain x 20k-gene matrix, 4096 rows per GPU, each rank
+holding its 1/8 shard of 12,500 strains) with its own roofline entry. Every timed step must be
+finite (losses and gradient norm): a non-finite step fails the run.
 """
 import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -88,7 +95,27 @@ def parse():
                     help="LDS ring depth of the 128x128 hidden-layer GEMM tiles (GM2_OPT_SMALL_STAGES)")
     ap.add_argument("--input-chunks", type=int, choices=[1, 4], default=None,
                     help="input-layer weight-gradient launches (default: 4 under DDP, else 1)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5-shaped (G=20,000) step line")
+    ap.add_argument("--c5-strains", type=int, default=12500,
+                    help="strains resident per rank for the C5 line (the 1/8 shard of 100,000)")
     return ap.parse_args()
+
+
+def launch_ranks(a):
+    """`--gpus N` outside torchrun: start N ranks through a child torch.distributed.run (one process
+    per GPU, 127.0.0.1 rendezvous) and return its exit code. Nothing here initialises the GPU
+    (torch.cuda.device_count does not), so the parent never holds a device context."""
+    backend = os.environ.get("GM2_DIST_BACKEND", "nccl")
+    if backend == "nccl" and torch.cuda.device_count() < a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but {torch.cuda.device_count()} GPU(s) visible "
+              "(GM2_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs)", file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def cpu_baseline(x_u8, G, H, L, budget_s, batch):
@@ -178,37 +205,20 @@ def scalar_table(nsteps):
     return tab
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # (local % device count: lets a 1-GPU box rehearse the N>1 path with GM2_DIST_BACKEND=gloo;
-    # torch.cuda.device_count() does not initialise the GPU)
-    local = local % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        backend = os.environ.get("GM2_DIST_BACKEND", "nccl")  # nccl = RCCL; gloo only to rehearse
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-
+def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12345):
+    """K timed v0 training steps (after W warm-up steps) of `B` rows per rank, on a resident
+    synthetic pan-genome shard of `strains` x G per rank: gather, forward, fused loss, backward,
+    (bucketed all-reduce when world > 1), clip statistics, Adam. Returns the max-over-ranks wall
+    time of the K steps, the live-timed output-layer loss kernel, and the per-step loss record
+    (every step's losses and gradient norm must be finite)."""
     from gm2 import native
     from gm2.data import ResidentMatrix, synthetic_pangenome
     from gm2.ddp import GradSync
     from gm2.model import VAE
     from gm2.trainer import Adam
 
-    G, H, L, B = a.genes, a.hidden, a.latent, a.batch
-    prec = native.GM2_BF16 if a.precision == "bf16" else native.GM2_F32
-    x = synthetic_pangenome(a.strains, G, seed=12345 + rank)
+    x = synthetic_pangenome(strains, G, seed=seed_base + rank)
     mat = ResidentMatrix(x, device=dev)
-    if not (rank == 0 and world == 1 and not a.no_cpu_baseline):
-        del x
     torch.manual_seed(0)  # identical init on every rank
     model = VAE(G, H, L, device=dev, precision=prec)
     opt = Adam(model, lr=1e-3)
@@ -221,16 +231,19 @@ def main():
     tab[:, native.S_NORM_AHEAD] = 1.0 if dist is None else 0.0
     scal = torch.tensor(tab, dtype=torch.float32, device=dev)
     g = torch.Generator().manual_seed(100 + rank)
-    rows = torch.cat([torch.randperm(a.strains, generator=g)[:B] for _ in range(nsteps + 1)]).to(torch.int32).to(dev)
+    rows = torch.cat([torch.randperm(strains, generator=g)[:B] for _ in range(nsteps + 1)]).to(torch.int32).to(dev)
     loss = torch.zeros(nsteps, native.LOSS_SLOTS, dtype=torch.float64, device=dev)
     torch.cuda.manual_seed(1)
     sync = GradSync(dist, model, grads, exchange=a.grad_exchange) if dist is not None else None
+    if sync is not None:
+        sync.prepare(ws)
+    # tuning switches of this workspace only (A/B measurements)
     if a.input_chunks is not None:
-        native.set_option(native.OPT_INPUT_CHUNKS, a.input_chunks)
+        ws.set_option(native.OPT_INPUT_CHUNKS, a.input_chunks)
     if a.small_stages is not None:
-        native.set_option(native.OPT_SMALL_STAGES, a.small_stages)
+        ws.set_option(native.OPT_SMALL_STAGES, a.small_stages)
     if a.grid_cap is not None:
-        native.set_option(native.OPT_GRID_CAP, a.grid_cap)
+        ws.set_option(native.OPT_GRID_CAP, a.grid_cap)
     # next-batch staging (gm2_batch.next) only under DDP, where the gather fills the wait for the
     # input-layer exchange; on one GPU it measured ~30 us/step slower (profiles/r02_prefetch_ab_*)
     prefetch = dist is not None and not a.no_prefetch
@@ -243,7 +256,7 @@ def main():
         batch = native.make_batch(mat.data, mat.ld, rows[i * B:(i + 1) * B], B, eps, next=nxt)
         native.train_fwd_bwd(ws, batch, model.params, grads, model.bn, scal[i], loss[i])
         if sync is not None:
-            sync.after_backward()  # bucketed SUM all-reduce overlapped with the backward
+            sync.after_backward(ws)  # bucketed SUM all-reduce overlapped with the backward
         native.grad_norm(ws, model.params, grads, scal[i], loss[i])
         native.adam_step(ws, model.params, grads, opt.exp_avg, opt.exp_avg_sq, scal[i])
 
@@ -268,49 +281,105 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     losses = loss.cpu().numpy()
-    # every step must have run (its loss slot written) and the first must be finite. v0 at lr 1e-3
-    # on the random synthetic matrix is not a stable optimisation problem at batch 4096 (logvar
-    # overflows after ~10 steps), so later steps may be non-finite: the work a step
-    # does is the same, and the count is reported
-    if not (losses[:, 0] != 0).all() or not np.isfinite(losses[0, :3]).all():
-        raise RuntimeError("a benchmark step did not run, or the first step's loss is non-finite")
-    nonfinite = int((~np.isfinite(losses[:, :3])).any(axis=1).sum())
-    value = world * B * a.steps / elapsed
-    # dominant kernel: decoder output layer GEMM [B,H]x[H,G] + fused BCE/abundance/dlogits epilogue
+    # every step must have run (its BCE slot written) and be finite: BCE, sum p, KL and the
+    # gradient norm of every warm-up and timed step
+    if not (losses[:, 0] != 0).all():
+        raise RuntimeError("a benchmark step did not run (its loss slot is still zero)")
+    bad = ~np.isfinite(losses[:, [0, 1, 2, 4]]).all(axis=1)
+    if bad.any():
+        raise RuntimeError(f"non-finite loss / gradient norm at step(s) {np.flatnonzero(bad).tolist()}")
+    info = {"prefetch": prefetch, "input_chunks": ws.get_option(native.OPT_INPUT_CHUNKS),
+            "x": x if (rank == 0 and world == 1) else None, "mat": mat}
+    del model, opt, ws, grads, sync
+    return elapsed, k_ms, k_n, info
+
+
+def roofline_entry(a, prec, G, H, B, k_ms, k_n, traffic_key=None):
+    """Output-layer loss GEMM [B,H]x[H,G] + fused BCE/dlogits epilogue against the MFMA roofline:
+    achieved = 2*B*H*G FLOP per launch / its average live-timed launch duration."""
+    from gm2 import native
     k_avg_ms = k_ms / max(k_n, 1)
     k_flops = 2.0 * B * H * G
     achieved = k_flops / (k_avg_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic(a, "k_gemm_recon_loss")
+    peak = PEAK_BF16_TFLOPS if prec == native.GM2_BF16 else PEAK_F32_TFLOPS
+    traffic, traffic_src = pmc_traffic(a, "k_gemm_recon_loss") if traffic_key is None else (None, None)
+    return {"bound": "mfma", "kernel": "k_gemm_recon_loss<bf16>" if prec == native.GM2_BF16
+            else "k_gemm_recon_loss<f32>", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
+            "launch_ms": round(k_avg_ms, 4), "launches": k_n, "flops_per_launch": k_flops}
+
+
+def main():
+    a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}: n_gpus must equal the request")
+    # (local % device count: lets a 1-GPU box rehearse the N>1 path with GM2_DIST_BACKEND=gloo;
+    # torch.cuda.device_count() does not initialise the GPU)
+    local = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        backend = os.environ.get("GM2_DIST_BACKEND", "nccl")  # nccl = RCCL; gloo only to rehearse
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+
+    from gm2 import native
+
+    G, H, L, B = a.genes, a.hidden, a.latent, a.batch
+    prec = native.GM2_BF16 if a.precision == "bf16" else native.GM2_F32
+    elapsed, k_ms, k_n, info = train_leg(a, dev, dist, rank, world, G, H, L, B, a.strains, prec)
+    value = world * B * a.steps / elapsed
     out = {
         "metric": "strain-vectors/sec (train+sample), v0 preset, 1/2/4/8 MI355X vs host CPU",
         "value": round(value, 1), "unit": "strain-vectors/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
         "config": {"workload": "C2: v0 train step (fwd+bwd+clip+Adam), synthetic pan-genome "
-                               f"{a.strains}x{G} u8 resident, batch {B}/GPU",
+                               f"{a.strains}x{G} u8 resident per GPU, batch {B}/GPU",
                    "preset": "v0", "genes": G, "hidden": H, "latent": L, "global_batch": B * world,
                    "parallelism": f"dp{world}",
                    "grad_exchange": (f"{a.grad_exchange} (decoder.9 / encoder.0 weight buckets; rest f32), RCCL "
                                      f"SUM all-reduce overlapped with the backward, input-layer gradient in "
-                                     f"{native.get_option(native.OPT_INPUT_CHUNKS)} launch(es)")
+                                     f"{info['input_chunks']} launch(es)")
                    if world > 1 else "none (one GPU)",
-                   "input_prefetch": prefetch},
+                   "input_prefetch": info["prefetch"]},
         "train_tflops": round(value * train_flops_per_vector(G, H, L) / 1e12, 2),
-        "nonfinite_steps": nonfinite,
-        "roofline": {"bound": "mfma", "kernel": "k_gemm_recon_loss<bf16>" if prec == native.GM2_BF16
-                     else "k_gemm_recon_loss<f32>", "achieved": round(achieved, 1),
-                     "peak": PEAK_BF16_TFLOPS if prec == native.GM2_BF16 else PEAK_F32_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved / (PEAK_BF16_TFLOPS if prec == native.GM2_BF16
-                                                                 else PEAK_F32_TFLOPS), 4),
-                     "traffic": traffic, "traffic_source": traffic_src,
-                     "launch_ms": round(k_avg_ms, 4), "launches": k_n,
-                     "flops_per_launch": k_flops},
+        "nonfinite_steps": 0,
+        # dominant kernel: decoder output layer GEMM [B,H]x[H,G] + fused BCE/abundance/dlogits epilogue
+        "roofline": roofline_entry(a, prec, G, H, B, k_ms, k_n),
     }
+    x = info.pop("x")
+    del info
+    torch.cuda.empty_cache()
+    if not a.no_c5:
+        # C5 (configs[4]): v0 on the synthetic 100k x 20k matrix, each rank its 12,500-strain shard
+        Gc = 20000
+        el5, k5, n5, inf5 = train_leg(a, dev, dist, rank, world, Gc, H, L, B, a.c5_strains, prec, seed_base=777)
+        del inf5
+        torch.cuda.empty_cache()
+        v5 = world * B * a.steps / el5
+        out["c5"] = {"workload": f"C5: v0 train step, synthetic {a.c5_strains}x{Gc} u8 shard per GPU (100,000 x "
+                                 f"20,000 over 8), batch {B}/GPU", "value": round(v5, 1), "unit": "strain-vectors/s",
+                     "n_gpus": world, "ms_per_step": round(el5 / a.steps * 1e3, 3),
+                     "train_tflops": round(v5 * train_flops_per_vector(Gc, H, L) / 1e12, 2),
+                     "roofline": roofline_entry(a, prec, Gc, H, B, k5, n5, traffic_key="c5")}
     if rank == 0 and world == 1 and not a.no_f32_line:
+        from gm2.data import ResidentMatrix
         other = native.GM2_F32 if prec == native.GM2_BF16 else native.GM2_BF16
-        out["precision_line"] = gpu_precision_line(mat, G, H, L, B, other, 5, dev)
-    if rank == 0 and not a.no_sample:
-        out["sample"] = sample_bench(a, dev)
+        out["precision_line"] = gpu_precision_line(ResidentMatrix(x, device=dev), G, H, L, B, other, 5, dev)
+    if not a.no_sample:
+        smp = sample_bench(a, dev, dist, rank, world)
+        if rank == 0:
+            out["sample"] = smp
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(x, G, H, L, a.cpu_seconds, B)
         # C1 (BASELINE.json configs[0]): the reference's CPU plumbing case, v0 at batch 64
@@ -322,14 +391,17 @@ def main():
         dist.destroy_process_group()
 
 
-def sample_bench(a, dev):
+def sample_bench(a, dev, dist=None, rank=0, world=1):
     """C3: v1 preset (hidden 512, latent 32) `--mode sample` of a.sample_genomes genomes (1e6 by
     default) in 65,536-genome chunks: z ~ N(0, I) drawn on the device (extras.py:197), exact-fp32
     decode + threshold into packed masks in HBM (gm2_decode_bits), the essential-gene counts of
     every genome on the device (gm2_mask_count_groups, a synthetic 300-gene essential table), and
     the packed masks + counts copied to pinned host memory on a second stream (overlapping the next
-    chunk's decode). genomes/s = all of that, end to end; the .npy write to disk is excluded."""
+    chunk's decode). genomes/s = all of that, end to end; the .npy write to disk is excluded.
+    world > 1: the genomes are sharded over the ranks (contiguous slices, no collective: z rows are
+    independent); genomes/s = all genomes / max-rank time."""
     from gm2 import native
+    from gm2.ddp import rank_slice
     from gm2.masks import essential_groups
     from gm2.model import VAE
     G, H, L = a.genes, 512, 32
@@ -337,7 +409,9 @@ def sample_bench(a, dev):
     m = VAE(G, H, L, device=dev, precision=native.GM2_F32)
     m.eval()
     chunk = 65536
-    n = a.sample_genomes
+    n_all = a.sample_genomes
+    lo, hi = rank_slice(n_all, rank, world)
+    n = hi - lo
     ldb = native.packed_row_bytes(G)
     rng = np.random.Generator(np.random.PCG64(3))
     ess = {f"e{i}": [int(p) for p in rng.integers(0, G, size=int(rng.integers(1, 4)))] for i in range(300)}
@@ -370,19 +444,28 @@ def sample_bench(a, dev):
     # warm-up on one chunk's worth
     native.decode_bits(ws, m.params, m.bn, torch.randn(chunk, L, device=dev), chunk, dbits[0], ldb)
     torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
     native.timing_begin(native.KC_MASK)
     t0 = time.perf_counter()
     run(True)
+    if dist is not None:
+        dist.barrier()
     dt = time.perf_counter() - t0
     k_ms, k_n = native.timing_end()
-    gps = n / dt
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    gps = n_all / dt
     kflops = 2.0 * chunk * H * G
     ach = kflops / (k_ms / max(k_n, 1) * 1e-3) / 1e12
     # the packed masks that reached the host are the decode's: spot-check the last chunk on device
     last = (n - 1) // chunk * chunk
     assert torch.equal(host_bits[last:n].to(dev), dbits[((n - 1) // chunk) & 1][:n - last])
     traffic, traffic_src = pmc_traffic(a, "k_gemm_mask")
-    return {"genomes_per_s": round(gps, 1), "preset": "v1", "genomes": n, "chunk": chunk, "dtype": "f32",
+    return {"genomes_per_s": round(gps, 1), "preset": "v1", "genomes": n_all, "n_gpus": world, "chunk": chunk,
+            "dtype": "f32",
             "mask_format": "packed bits (numpy packbits, little)", "includes": "z draw, decode, threshold, pack, "
             "essential-gene counts, D2H of packed masks + counts to pinned host memory",
             "decode_tflops": round(gps * decode_flops_per_genome(G, H, L) / 1e12, 2),

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -53,7 +54,11 @@ struct Dims {
   int64_t off[NP + 1];
 };
 
-Dims make_dims(const gm2_dims* d) {
+// gpad: the padding of the gene axis G. The bf16 workspaces pad it to 256 so that every GEMM with a
+// G-wide side (input layer, output layer + loss, their weight gradients) tiles into the 256x256
+// kernels (C5's G = 20,000 would otherwise be 20,096 = 78.5 x 256 and fall to the 128-tiles); the
+// f32 workspaces (sampling decode, parity) keep 128.
+Dims make_dims(const gm2_dims* d, int gpad = kTile) {
   if (!d) throw Gm2Error("null dims");
   Dims x;
   x.G = d->G, x.H = d->H, x.L = d->L;
@@ -61,7 +66,7 @@ Dims make_dims(const gm2_dims* d) {
   if (x.H % kTile) throw Gm2Error("hidden_dim %lld must be a multiple of 128", (long long)x.H);
   if (256 % x.L) throw Gm2Error("latent_dim %lld must divide 256", (long long)x.L);
   x.Bm = round_up(d->batch_max, kTile);
-  x.Gp = round_up(x.G, kTile);
+  x.Gp = round_up(x.G, gpad);
   x.Lp = round_up(x.L, kKPad);
   x.K2L = round_up(2 * x.L, kKPad);
   x.L2r = round_up(2 * x.L, kTile);
@@ -95,7 +100,7 @@ struct Layout {
 Layout make_layout(const gm2_dims* gd, int prec) {
   if (prec != GM2_F32 && prec != GM2_BF16) throw Gm2Error("bad precision %d", prec);
   Layout o;
-  o.d = make_dims(gd);
+  o.d = make_dims(gd, prec == GM2_BF16 ? 2 * kTile : kTile);
   o.prec = prec;
   o.es = prec == GM2_F32 ? 4 : 2;
   const Dims& d = o.d;
@@ -154,6 +159,8 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   return o;
 }
 
+struct WsState;
+
 template <typename T>
 struct Ctx {
   const Layout& lo;
@@ -162,11 +169,12 @@ struct Ctx {
   const Dims& d;
   int64_t slab_off, slab_cap;  // split-K scratch of this stream
   int64_t xo, xbo;             // input slot of this call: gathered rows X [Bm][Gp] (T), target bits
-  Ctx(const Layout& l, void* w, void* st)
-      : lo(l), ws((char*)w), s((hipStream_t)st), d(l.d), slab_off(l.slabs), slab_cap(l.slab_cap), xo(l.X),
-        xbo(l.XB) {}
-  Ctx side(hipStream_t st) const {
-    Ctx c(lo, ws, st);
+  WsState* st;                 // host-side state of the workspace
+  Ctx(const Layout& l, void* w, void* strm, WsState* state = nullptr)
+      : lo(l), ws((char*)w), s((hipStream_t)strm), d(l.d), slab_off(l.slabs), slab_cap(l.slab_cap), xo(l.X),
+        xbo(l.XB), st(state) {}
+  Ctx side(hipStream_t strm) const {
+    Ctx c(lo, ws, strm, st);
     c.slab_off = lo.side_slabs;
     c.slab_cap = lo.side_cap;
     c.xo = xo;
@@ -178,69 +186,112 @@ struct Ctx {
 };
 
 // ---------------------------------------------------------------------------------------------
-// side stream for the weight-gradient GEMMs (fork/join through events; capture-safe). One per
-// device, created on first use. GM2_SIDE_STREAM=0 keeps everything on the caller's stream.
+// Host-side state of one workspace (keyed by its device address; created by gm2_workspace_init,
+// dropped by gm2_workspace_release). Nothing here is shared between workspaces: two models, or a
+// training and a sampling workspace, in one process keep their own options, side stream, gradient
+// bucket events and staged input slot. One workspace is used from one host thread at a time.
+//
+//  * side stream for the weight-gradient GEMMs (fork/join through events; capture-safe), created
+//    on first use; GM2_OPT_SIDE_STREAM = 0 keeps everything on the caller's stream.
+//  * gradient buckets (data-parallel exchange): ranges of the flat gradient buffer in the order the
+//    backward finalises them, each with an event recorded when its last gradient is written
+//    (gm2_grad_bucket_bounds / gm2_wait_grad_bucket)
+//      0: decoder.9.weight, decoder.9.bias      (output layer: first off the backward)
+//      1: encoder.0.bias .. decoder.7.bias      (every hidden / head / BN tensor)
+//      2..5: encoder.0.weight row quarters      (input layer: the last weight-gradient GEMM)
+//  * the input-slot stage of gm2_batch.next (SlotState below).
 // ---------------------------------------------------------------------------------------------
-struct SideRes {
+// Per-workspace input-slot state. A training call whose batch carries `next` gathers next's rows
+// into the other slot during its own tail; the following training call finds them there (same
+// data / ld / rows / n) and starts straight at the input-layer GEMM. Every other call that uses an
+// input slot first waits for a pending stage and drops it (it writes slot 0).
+struct SlotState {
+  bool staged = false;
+  int slot = 0;  // slot of the staged batch
+  const uint8_t* data = nullptr;
+  int64_t ld = 0, n = 0, total = 0;
+  const int32_t* rows = nullptr;
+  int prec = -1;
+};
+
+struct WsState {
+  Options opt;
+  int dev = -1;
   hipStream_t side = nullptr;
-  std::vector<hipEvent_t> ev;
+  std::vector<hipEvent_t> ev;  // fork/join ring
   size_t next = 0;
-};
+  hipEvent_t bucket[GM2_GRAD_BUCKETS] = {};
+  bool recorded = false;  // a training backward has recorded the bucket events
+  SlotState slot;
+  hipEvent_t slot_done = nullptr;
 
-std::atomic<int>& side_flag() {
-  static std::atomic<int> on{[] {
-    const char* e = getenv("GM2_SIDE_STREAM");
-    return (e && e[0] == '0') ? 0 : 1;
-  }()};
-  return on;
-}
-
-SideRes* side_res() {
-  if (!side_flag().load(std::memory_order_relaxed)) return nullptr;
-  static std::mutex mu;
-  static std::map<int, SideRes> per_dev;
-  int dev = 0;
-  HIP_OK(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lk(mu);
-  SideRes& r = per_dev[dev];
-  if (!r.side) {
-    HIP_OK(hipStreamCreateWithFlags(&r.side, hipStreamNonBlocking));
-    r.ev.resize(64);
-    for (auto& e : r.ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  void create() {
+    HIP_OK(hipGetDevice(&dev));
+    for (auto& e : bucket) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&slot_done, hipEventDisableTiming));
   }
-  return &r;
-}
-
-// make `to` wait for everything enqueued on `from` so far
-void order(SideRes* r, hipStream_t from, hipStream_t to) {
-  hipEvent_t e = r->ev[r->next++ % r->ev.size()];
-  HIP_OK(hipEventRecord(e, from));
-  HIP_OK(hipStreamWaitEvent(to, e, 0));
-}
-
-// ---------------------------------------------------------------------------------------------
-// gradient buckets (data-parallel exchange): ranges of the flat gradient buffer in the order the
-// backward finalises them, each with a per-device event recorded when its last gradient is
-// written (gm2_grad_bucket_bounds / gm2_wait_grad_bucket)
-//   0: decoder.9.weight, decoder.9.bias      (output layer: first off the backward)
-//   1: encoder.0.bias .. decoder.7.bias      (every hidden / head / BN tensor)
-//   2: encoder.0.weight                      (input layer: the last weight-gradient GEMM)
-// ---------------------------------------------------------------------------------------------
-struct BucketEvents {
-  hipEvent_t ev[GM2_GRAD_BUCKETS] = {};
-  bool recorded = false;
+  void destroy() {
+    if (side) (void)hipStreamDestroy(side);
+    for (auto e : ev) (void)hipEventDestroy(e);
+    for (auto e : bucket)
+      if (e) (void)hipEventDestroy(e);
+    if (slot_done) (void)hipEventDestroy(slot_done);
+    side = nullptr;
+    ev.clear();
+  }
+  // the side stream when GM2_OPT_SIDE_STREAM is on (created on first use), else nullptr
+  hipStream_t side_stream() {
+    if (!opt.side_stream) return nullptr;
+    if (!side) {
+      HIP_OK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+      ev.resize(64);
+      for (auto& e : ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    return side;
+  }
+  // make `to` wait for everything enqueued on `from` so far
+  void order(hipStream_t from, hipStream_t to) {
+    hipEvent_t e = ev[next++ % ev.size()];
+    HIP_OK(hipEventRecord(e, from));
+    HIP_OK(hipStreamWaitEvent(to, e, 0));
+  }
 };
 
-BucketEvents* bucket_events() {
+std::mutex& ws_mutex() {
   static std::mutex mu;
-  static std::map<int, BucketEvents> per_dev;
-  int dev = 0;
-  HIP_OK(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lk(mu);
-  BucketEvents& b = per_dev[dev];
-  if (!b.ev[0])
-    for (auto& e : b.ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  return &b;
+  return mu;
+}
+std::map<void*, std::unique_ptr<WsState>>& ws_map() {
+  static std::map<void*, std::unique_ptr<WsState>> m;
+  return m;
+}
+
+// the state of `ws`; a workspace that was never initialised through gm2_workspace_init (or was
+// released) is an error
+WsState& ws_state(void* ws) {
+  std::lock_guard<std::mutex> lk(ws_mutex());
+  auto it = ws_map().find(ws);
+  if (it == ws_map().end()) throw Gm2Error("workspace %p is not initialised (gm2_workspace_init)", ws);
+  return *it->second;
+}
+
+// (re)initialise the state of `ws`: process-default options, no stage, fresh events
+WsState& ws_reset(void* ws) {
+  std::lock_guard<std::mutex> lk(ws_mutex());
+  auto& slot = ws_map()[ws];
+  if (slot) slot->destroy();
+  slot.reset(new WsState());
+  slot->opt = default_options();
+  slot->create();
+  return *slot;
+}
+
+void ws_release(void* ws) {
+  std::lock_guard<std::mutex> lk(ws_mutex());
+  auto it = ws_map().find(ws);
+  if (it == ws_map().end()) return;
+  it->second->destroy();
+  ws_map().erase(it);
 }
 
 // first row of quarter q (0..4) of the input-layer weight gradient [H][G]
@@ -253,11 +304,6 @@ void bucket_bounds(const Dims& d, int64_t* lh) {
     lh[4 + 2 * q] = input_quarter_row(d, q) * d.G;
     lh[5 + 2 * q] = input_quarter_row(d, q + 1) * d.G;
   }
-}
-
-std::atomic<int>& input_chunks_flag() {
-  static std::atomic<int> v{1};
-  return v;
 }
 
 // GEMM into the fp32 slab scratch (split-K slices summed by the consumer). Returns #slabs.
@@ -301,7 +347,7 @@ struct BigGrads {
 // when each quarter is whole 256-row tiles of a one-pass plan, like the full launch
 template <typename T>
 bool input_chunked(const BigGrads<T>& r, int H) {
-  if (input_chunks_flag().load(std::memory_order_relaxed) != 4 || H % 1024) return false;
+  if (opts().input_chunks != 4 || H % 1024) return false;
   const GemmPlan p = plan_gemm<T>(r.g0);
   return p.splits == 1 && p.tile == 256;
 }
@@ -389,6 +435,14 @@ TensorTable make_table(const Ctx<T>& c, int kind = 0) {
   return tt;
 }
 
+// the resident matrix rows of a batch: 16-B aligned rows of at least roundup(G, 128) bytes (gm2.h)
+void check_batch_data(const gm2_batch* b, const Dims& d, const char* what) {
+  if (!b->data) throw Gm2Error("%s: null data", what);
+  if (b->ld_data % 16 || b->ld_data < round_up(d.G, kTile) || ((uintptr_t)b->data & 15))
+    throw Gm2Error("%s: data rows must be 16-B aligned with ld_data (%lld) a multiple of 16 and >= roundup(G, 128)",
+                   what, (long long)b->ld_data);
+}
+
 // ---------------------------------------------------------------------------------------------
 // forward (train or eval). Fills A_l (+A_l^T when train), Y_l, save_l, HD, Z, ZT and runs the
 // fused reconstruction-loss epilogue (dL, dL^T when with_grad).
@@ -402,7 +456,7 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   const int B = (int)b->n;
   if (B <= 0 || B > d.Bm) throw Gm2Error("batch rows %d outside (0, batch_max=%lld]", B, (long long)d.Bm);
   if (train && B < 2) throw Gm2Error("Expected more than 1 value per channel when training (batch of 1)");
-  if (!b->data) throw Gm2Error("null data");
+  check_batch_data(b, d, "batch");
   const int Bp = (int)round_up(B, kTile);
   const int H = (int)d.H, L = (int)d.L;
   // 1) strain rows -> X [Bp][Gp] (T) + bit-packed target (unless a previous training call staged them)
@@ -475,12 +529,13 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   const int Gp = (int)d.Gp, Lr = (int)d.Lr, L2r = (int)d.L2r;
   // weight gradients go to a side stream: they are off the critical path (dY -> dX -> BN -> ...)
   // and fill the tails of its launches; the join at the end orders them before the caller's work
-  SideRes* sr = side_res();
-  const Ctx<T> w = sr ? c.side(sr->side) : c;
+  WsState& st = *c.st;
+  const hipStream_t side = st.side_stream();
+  const bool sr = side != nullptr;
+  const Ctx<T> w = sr ? c.side(side) : c;
   auto fork = [&] {
-    if (sr) order(sr, c.s, w.s);
+    if (sr) st.order(c.s, w.s);
   };
-  BucketEvents* be = bucket_events();
   // output layer: dW9[g][h] = sum_b dL[b][g] A5[b][h] ; dA5[b][h] = sum_g dL[b][g] W9[g][h]
   // (its bias gradient was summed in the forward's recon epilogue, before the fork)
   // Written as dW9^T[h][g] = sum_b A5^T[h][b] dL[b][g] with A5^T K-major (a transposed copy made
@@ -502,7 +557,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
     }
   }
-  HIP_OK(hipEventRecord(be->ev[0], w.s));
+  HIP_OK(hipEventRecord(st.bucket[0], w.s));
   // dA_j = dY . W (K-major dY, MN-major W) into the slab area; when the plan allows, the GEMM's
   // epilogue also takes BatchNorm j's backward partials (sum do, sum (y-mean) do)
   bool have_part = false;
@@ -543,7 +598,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       // bucket 1 (every hidden-layer weight gradient) is final when the side stream's queue so far
       // is; dWe0 starts without waiting for it (the join follows the dWe0 launch: the side stream's
       // last small GEMM / column sums run beside dWe0's first tiles instead of before them)
-      HIP_OK(hipEventRecord(be->ev[1], w.s));
+      HIP_OK(hipEventRecord(st.bucket[1], w.s));
       if (input_chunked(bg, H)) {  // four row-quarter launches, bucket 2 + q final after launch q
         for (int q = 0; q < 4; ++q) {
           GemmArgs<T> gq = bg.g0;
@@ -552,19 +607,19 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
           gq.M = gq.Mp = H / 4;
           if (!launch_gemm_sq<T>(gq, gr + d.off[E0W] + (int64_t)r0 * G, G, nullptr, c.s, true))
             throw Gm2Error("input-layer quarter GEMM: not a one-pass plan");
-          HIP_OK(hipEventRecord(be->ev[2 + q], c.s));
+          HIP_OK(hipEventRecord(st.bucket[2 + q], c.s));
         }
       } else {
         if (!bg.direct || !launch_gemm_sq<T>(bg.g0, gr + d.off[E0W], G, nasq + bg.n9, c.s))
           gemm_to<T>(c, c.t(l.dYT0), Bp, H, c.t(c.xo), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0);
-        for (int q = 0; q < 4; ++q) HIP_OK(hipEventRecord(be->ev[2 + q], c.s));
+        for (int q = 0; q < 4; ++q) HIP_OK(hipEventRecord(st.bucket[2 + q], c.s));
       }
-      if (sr) order(sr, w.s, c.s);  // join: the caller's stream sees every weight gradient
+      if (sr) st.order(w.s, c.s);  // join: the caller's stream sees every weight gradient
       if (nx) {  // the next batch's rows -> the other input slot, on the side stream after dWe0 (beside
                  // it, it only slows the GEMM down by its own length): under the data-parallel exchange
                  // of the input-layer gradient, or beside the clip / Adam passes on one GPU
         const hipStream_t gs = sr ? w.s : c.s;
-        if (sr) order(sr, c.s, w.s);  // placed after dWe0 (that slot's readers, the previous step, are earlier)
+        if (sr) st.order(c.s, w.s);  // placed after dWe0 (that slot's readers, the previous step, are earlier)
         const int Bn = (int)nx->b->n;
         launch_gather_rows<T>(nx->b->data, nx->b->ld_data, nx->b->rows, Bn, G, c.t(nx->xo), Gp, Gp,
                               (int)round_up(Bn, kTile), (uint32_t*)(c.ws + nx->xbo), Gp / 32, gs);
@@ -573,9 +628,9 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
         // makes (workspace lifetime, device-wide syncs are not needed); the clip / Adam passes that
         // follow wait for it, which measured time-neutral (both are HBM-bound) and keeps the gather
         // beside the data-parallel exchange, which waits on bucket events instead
-        if (sr) order(sr, w.s, c.s);
+        if (sr) st.order(w.s, c.s);
       }
-      be->recorded = true;
+      st.recorded = true;
       break;
     }
     if (i == 3) {  // decoder input layer, then back through the reparameterisation and the heads
@@ -622,48 +677,20 @@ void decode_chain(const Ctx<T>& c, const float* prm, float* bn, int n, uint8_t* 
   launch_gemm_mask<T>(g, prm + d.off[D9B], mask, ldm, probs, ldpr, c.s, bits, ldb);
 }
 
-// Per-workspace input-slot state. A training call whose batch carries `next` gathers next's rows
-// into the other slot during its own tail; the following training call finds them there (same
-// data / ld / rows / n) and starts straight at the input-layer GEMM. Every other call that uses an
-// input slot first waits for a pending stage and drops it (it writes slot 0).
-struct SlotState {
-  bool staged = false;
-  int slot = 0;  // slot of the staged batch
-  const uint8_t* data = nullptr;
-  int64_t ld = 0, n = 0, total = 0;
-  const int32_t* rows = nullptr;
-  int prec = -1;
-  hipEvent_t done = nullptr;
-};
-
-SlotState& slot_state(void* ws) {
-  static std::map<void*, SlotState> m;
-  SlotState& st = m[ws];
-  if (!st.done) HIP_OK(hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
-  return st;
-}
-std::mutex& slot_mutex() {
-  static std::mutex mu;
-  return mu;
-}
-
 // make `s` wait for a pending stage on `ws` and forget it (the caller is about to write slot 0)
-void drop_stage(void* ws, hipStream_t s) {
-  std::lock_guard<std::mutex> lk(slot_mutex());
-  SlotState& st = slot_state(ws);
-  if (st.staged) HIP_OK(hipStreamWaitEvent(s, st.done, 0));
-  st.staged = false;
+void drop_stage(WsState& st, hipStream_t s) {
+  if (st.slot.staged) HIP_OK(hipStreamWaitEvent(s, st.slot_done, 0));
+  st.slot.staged = false;
 }
 
 template <typename T>
 void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr, float* bn, const float* scal,
-               double* loss, void* ws, void* st) {
-  Ctx<T> c(lo, ws, st);
-  std::lock_guard<std::mutex> lk(slot_mutex());
-  SlotState& ss = slot_state(ws);
+               double* loss, void* ws, void* strm, WsState& st) {
+  Ctx<T> c(lo, ws, strm, &st);
+  SlotState& ss = st.slot;
   const bool hit = ss.staged && ss.prec == lo.prec && ss.total == lo.total && ss.data == b->data &&
                    ss.ld == b->ld_data && ss.rows == b->rows && ss.n == b->n;
-  if (ss.staged) HIP_OK(hipStreamWaitEvent(c.s, ss.done, 0));
+  if (ss.staged) HIP_OK(hipStreamWaitEvent(c.s, st.slot_done, 0));
   const int slot = hit ? ss.slot : 0;
   c.xo = slot ? lo.X1 : lo.X;
   c.xbo = slot ? lo.XB1 : lo.XB;
@@ -671,13 +698,12 @@ void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr
   NextStage nx;
   const gm2_batch* nb = b->next;
   if (nb) {
-    if (nb->n <= 0 || nb->n > lo.d.Bm || !nb->data) throw Gm2Error("next batch: rows %lld outside (0, batch_max]", (long long)nb->n);
-    if (nb->ld_data % 16 || nb->ld_data < lo.d.Gp || ((uintptr_t)nb->data & 15))
-      throw Gm2Error("next batch: bad data layout");
+    if (nb->n <= 0 || nb->n > lo.d.Bm) throw Gm2Error("next batch: rows %lld outside (0, batch_max]", (long long)nb->n);
+    check_batch_data(nb, lo.d, "next batch");
     nx.b = nb;
     nx.xo = slot ? lo.X : lo.X1;
     nx.xbo = slot ? lo.XB : lo.XB1;
-    nx.done = ss.done;
+    nx.done = st.slot_done;
   }
   forward<T>(c, b, prm, bn, 1, 1, scal, loss, gr, nullptr, 0, nullptr, 0.5f, true, hit);
   backward<T>(c, b, prm, gr, scal, nullptr, nullptr, 1, nb ? &nx : nullptr);
@@ -691,6 +717,16 @@ void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr
     ss.prec = lo.prec;
     ss.total = lo.total;
   }
+}
+
+// guarded body of a C-ABI call on workspace `ws`: its state, with its options in scope
+template <typename F>
+int with_ws(void* ws, F&& f) {
+  return guarded([&] {
+    WsState& st = ws_state(ws);
+    OptionScope scope(st.opt);
+    f(st);
+  });
 }
 
 }  // namespace
@@ -721,19 +757,19 @@ int gm2_workspace_init(const gm2_dims* d, int prec, void* ws, size_t ws_bytes, v
     const Layout lo = make_layout(d, prec);
     if ((size_t)lo.total > ws_bytes) throw Gm2Error("workspace too small: %zu < %lld", ws_bytes, (long long)lo.total);
     if ((uintptr_t)ws & 255) throw Gm2Error("workspace must be 256-B aligned");
-    drop_stage(ws, (hipStream_t)stream);  // a new (or reused) workspace holds no staged batch
+    ws_reset(ws);  // a new (or reused) workspace: process-default options, no staged batch
     HIP_OK(hipMemsetAsync(ws, 0, (size_t)lo.total, (hipStream_t)stream));
   });
 }
 
 int gm2_sync_shadows(const gm2_dims* d, int prec, const float* params, void* ws, void* stream) {
-  return guarded([&] {
+  return with_ws(ws, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
     if (prec == GM2_F32) {
-      Ctx<float> c(lo, ws, stream);
+      Ctx<float> c(lo, ws, stream, &st);
       launch_shadow_sync<float>(make_table(c), params, c.s);
     } else {
-      Ctx<bf16_t> c(lo, ws, stream);
+      Ctx<bf16_t> c(lo, ws, stream, &st);
       launch_shadow_sync<bf16_t>(make_table(c), params, c.s);
     }
   });
@@ -741,16 +777,16 @@ int gm2_sync_shadows(const gm2_dims* d, int prec, const float* params, void* ws,
 
 int gm2_train_fwd_bwd(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, float* grads,
                       float* bn_running, const float* scalars, double* loss, void* ws, void* stream) {
-  return guarded([&] {
+  return with_ws(ws, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
-    if (prec == GM2_F32) run_train<float>(lo, batch, params, grads, bn_running, scalars, loss, ws, stream);
-    else run_train<bf16_t>(lo, batch, params, grads, bn_running, scalars, loss, ws, stream);
+    if (prec == GM2_F32) run_train<float>(lo, batch, params, grads, bn_running, scalars, loss, ws, stream, st);
+    else run_train<bf16_t>(lo, batch, params, grads, bn_running, scalars, loss, ws, stream, st);
   });
 }
 
 int gm2_grad_norm(const gm2_dims* d, int prec, const float* params, const float* grads, const float* scalars,
                   double* loss, void* ws, void* stream) {
-  return guarded([&] {
+  return with_ws(ws, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
     const int64_t n = lo.d.off[NP];
     const int nb = grad_stats_blocks(n);
@@ -767,16 +803,16 @@ int gm2_grad_norm(const gm2_dims* d, int prec, const float* params, const float*
 
 int gm2_adam_step(const gm2_dims* d, int prec, float* params, const float* grads, float* m, float* v,
                   const float* scalars, void* ws, void* stream) {
-  return guarded([&] {
+  return with_ws(ws, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
     const int64_t n = lo.d.off[NP];
     const float* clip = (const float*)((char*)ws + lo.clip);
     (void)n;
     if (prec == GM2_F32) {
-      Ctx<float> c(lo, ws, stream);
+      Ctx<float> c(lo, ws, stream, &st);
       launch_adam_fused<float>(make_table(c, 1), grads, params, m, v, scalars, clip, c.s);
     } else {
-      Ctx<bf16_t> c(lo, ws, stream);
+      Ctx<bf16_t> c(lo, ws, stream, &st);
       launch_adam_fused<bf16_t>(make_table(c, 1), grads, params, m, v, scalars, clip, c.s);
     }
   });
@@ -784,15 +820,15 @@ int gm2_adam_step(const gm2_dims* d, int prec, float* params, const float* grads
 
 int gm2_eval_forward(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params,
                      const float* bn_running, const float* scalars, double* loss, void* ws, void* stream) {
-  return guarded([&] {
+  return with_ws(ws, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
-    drop_stage(ws, (hipStream_t)stream);  // these write input slot 0
+    drop_stage(st, (hipStream_t)stream);  // these write input slot 0
     float* bn = const_cast<float*>(bn_running);  // eval mode never writes running stats
     if (prec == GM2_F32) {
-      Ctx<float> c(lo, ws, stream);
+      Ctx<float> c(lo, ws, stream, &st);
       forward<float>(c, batch, params, bn, 0, 0, scalars, loss, nullptr);
     } else {
-      Ctx<bf16_t> c(lo, ws, stream);
+      Ctx<bf16_t> c(lo, ws, stream, &st);
       forward<bf16_t>(c, batch, params, bn, 0, 0, scalars, loss, nullptr);
     }
   });
@@ -800,11 +836,11 @@ int gm2_eval_forward(const gm2_dims* d, int prec, const gm2_batch* batch, const 
 
 int gm2_decode_mask(const gm2_dims* d, const float* params, const float* bn_running, const float* z, int64_t n,
                     uint8_t* mask, int64_t ld_mask, float* probs, int64_t ld_probs, void* ws, void* stream) {
-  return guarded([&] {
+  return with_ws(ws, [&](WsState& st) {
     const Layout lo = make_layout(d, GM2_F32);
     if (n <= 0 || n > lo.d.Bm) throw Gm2Error("decode rows %lld outside (0, batch_max]", (long long)n);
     if (ld_mask < lo.d.G || (probs && ld_probs < lo.d.G)) throw Gm2Error("decode: ld < G");
-    Ctx<float> c(lo, ws, stream);
+    Ctx<float> c(lo, ws, stream, &st);
     // z [n][L] -> Z [Bm][Lp] (pad columns stay zero from workspace init)
     HIP_OK(hipMemcpy2DAsync(c.f(lo.Z), lo.d.Lr * 4, z, lo.d.L * 4, lo.d.L * 4, n, hipMemcpyDeviceToDevice, c.s));
     decode_chain<float>(c, params, const_cast<float*>(bn_running), (int)n, mask, ld_mask, probs, ld_probs);
@@ -844,11 +880,11 @@ int gm2_mask_compact(const uint8_t* bits, int64_t n, int64_t ld_bits, const uint
 
 int gm2_decode_bits(const gm2_dims* d, const float* params, const float* bn_running, const float* z, int64_t n,
                     uint8_t* bits, int64_t ld_bits, float* probs, int64_t ld_probs, void* ws, void* stream) {
-  return guarded([&] {
+  return with_ws(ws, [&](WsState& st) {
     const Layout lo = make_layout(d, GM2_F32);
     if (n <= 0 || n > lo.d.Bm) throw Gm2Error("decode rows %lld outside (0, batch_max]", (long long)n);
     if (ld_bits < gm2_packed_row_bytes(lo.d.G) || (probs && ld_probs < lo.d.G)) throw Gm2Error("decode_bits: ld too small");
-    Ctx<float> c(lo, ws, stream);
+    Ctx<float> c(lo, ws, stream, &st);
     HIP_OK(hipMemcpy2DAsync(c.f(lo.Z), lo.d.Lr * 4, z, lo.d.L * 4, lo.d.L * 4, n, hipMemcpyDeviceToDevice, c.s));
     decode_chain<float>(c, params, const_cast<float*>(bn_running), (int)n, nullptr, 0, probs, ld_probs, bits, ld_bits);
   });
@@ -856,16 +892,16 @@ int gm2_decode_bits(const gm2_dims* d, const float* params, const float* bn_runn
 
 int gm2_recon_counts(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, const float* bn_running,
                      float threshold, int32_t* counts, void* ws, void* stream) {
-  return guarded([&] {
+  return with_ws(ws, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
-    drop_stage(ws, (hipStream_t)stream);  // these write input slot 0
+    drop_stage(st, (hipStream_t)stream);  // these write input slot 0
     if (!batch->eps) throw Gm2Error("recon_counts: eps required (model(x) samples z)");
     if (!counts) throw Gm2Error("recon_counts: counts required");
     HIP_OK(hipMemsetAsync(counts, 0, (size_t)batch->n * 3 * 4, (hipStream_t)stream));
     float* bn = const_cast<float*>(bn_running);  // eval mode never writes running stats
     auto run = [&](auto tag) {
       using T = decltype(tag);
-      Ctx<T> c(lo, ws, stream);
+      Ctx<T> c(lo, ws, stream, &st);
       forward<T>(c, batch, params, bn, 0, 0, nullptr, nullptr, nullptr, nullptr, 0, counts, threshold);
     };
     if (prec == GM2_F32) run(float{});
@@ -875,16 +911,17 @@ int gm2_recon_counts(const gm2_dims* d, int prec, const gm2_batch* batch, const 
 
 int gm2_encode(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, const float* bn_running,
                float* mu, float* logvar, void* ws, void* stream) {
-  return guarded([&] {
+  return with_ws(ws, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
-    drop_stage(ws, (hipStream_t)stream);  // these write input slot 0
+    drop_stage(st, (hipStream_t)stream);  // these write input slot 0
     gm2_batch b = *batch;
     auto run = [&](auto tag) {
       using T = decltype(tag);
-      Ctx<T> c(lo, ws, stream);
+      Ctx<T> c(lo, ws, stream, &st);
       const Dims& dd = c.d;
       const int B = (int)b.n, Bp = (int)round_up(B, kTile), H = (int)dd.H, L = (int)dd.L;
       if (B <= 0 || B > dd.Bm) throw Gm2Error("encode rows outside (0, batch_max]");
+      check_batch_data(&b, dd, "encode");
       float* bn = const_cast<float*>(bn_running);
       launch_gather_rows<T>(b.data, b.ld_data, b.rows, B, (int)dd.G, c.t(lo.X), dd.Gp, (int)dd.Gp, Bp, nullptr, 0,
                             c.s);
@@ -940,14 +977,14 @@ int gm2_gemm(int prec, int pk, int qk, const void* P, int64_t ldp, const void* Q
 
 int gm2_forward(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, float* bn_running,
                 int train, float* probs, int64_t ld_probs, float* mu, float* logvar, void* ws, void* stream) {
-  return guarded([&] {
+  return with_ws(ws, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
-    drop_stage(ws, (hipStream_t)stream);  // these write input slot 0
+    drop_stage(st, (hipStream_t)stream);  // these write input slot 0
     if (!probs || ld_probs < lo.d.G) throw Gm2Error("forward: probs required, ld_probs >= G");
     if (!batch->eps) throw Gm2Error("forward: eps required (model.py:102 draws it)");
     auto run = [&](auto tag) {
       using T = decltype(tag);
-      Ctx<T> c(lo, ws, stream);
+      Ctx<T> c(lo, ws, stream, &st);
       forward<T>(c, batch, params, bn_running, train, 0, nullptr, nullptr, nullptr, probs, ld_probs);
       const int64_t L = lo.d.L, B = batch->n;
       if (mu) HIP_OK(hipMemcpy2DAsync(mu, L * 4, c.f(lo.HD), 2 * L * 4, L * 4, B, hipMemcpyDeviceToDevice, c.s));
@@ -962,13 +999,13 @@ int gm2_forward(const gm2_dims* d, int prec, const gm2_batch* batch, const float
 int gm2_backward_outputs(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, int train,
                          const float* probs, int64_t ld_probs, const float* dprobs, const float* dmu,
                          const float* dlogvar, float* grads, void* ws, void* stream) {
-  return guarded([&] {
+  return with_ws(ws, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
-    drop_stage(ws, (hipStream_t)stream);  // these write input slot 0
+    drop_stage(st, (hipStream_t)stream);  // these write input slot 0
     if (!probs || !dprobs || ld_probs < lo.d.G) throw Gm2Error("backward_outputs: probs / dprobs required");
     auto run = [&](auto tag) {
       using T = decltype(tag);
-      Ctx<T> c(lo, ws, stream);
+      Ctx<T> c(lo, ws, stream, &st);
       const Dims& dd = c.d;
       const int B = (int)batch->n, Bp = (int)round_up(B, kTile);
       if (B <= 0 || B > dd.Bm) throw Gm2Error("backward_outputs: rows outside (0, batch_max]");
@@ -998,56 +1035,32 @@ int gm2_grad_bucket_bounds(const gm2_dims* d, int64_t* lo_hi) {
   return guarded([&] { bucket_bounds(make_dims(d), lo_hi); });
 }
 
-int gm2_wait_grad_bucket(int bucket, void* stream) {
-  return guarded([&] {
+int gm2_wait_grad_bucket(void* ws, int bucket, void* stream) {
+  return with_ws(ws, [&](WsState& st) {
     if (bucket < 0 || bucket >= GM2_GRAD_BUCKETS) throw Gm2Error("bucket %d out of range", bucket);
-    BucketEvents* be = bucket_events();
-    if (!be->recorded) throw Gm2Error("no gm2_train_fwd_bwd has run on this device yet");
-    HIP_OK(hipStreamWaitEvent((hipStream_t)stream, be->ev[bucket], 0));
+    if (!st.recorded) throw Gm2Error("no gm2_train_fwd_bwd has run on this workspace yet");
+    HIP_OK(hipStreamWaitEvent((hipStream_t)stream, st.bucket[bucket], 0));
   });
 }
 
 int gm2_set_option(int key, int value) {
-  return guarded([&] {
-    switch (key) {
-      case GM2_OPT_GEMM_PP: set_gemm_pp(value); break;
-      case GM2_OPT_SIDE_STREAM: side_flag().store(value ? 1 : 0); break;
-      case GM2_OPT_RECON_TILE:
-        if (value != 0 && value != 128 && value != 256) throw Gm2Error("recon tile %d: 0, 128 or 256", value);
-        set_recon_tile(value);
-        break;
-      case GM2_OPT_SMALL_SPLIT: set_small_split(value); break;
-      case GM2_OPT_BN_EPILOGUE: set_bn_epilogue(value); break;
-      case GM2_OPT_SMALL_WAVES: set_small_waves(value); break;
-      case GM2_OPT_GRID_CAP: set_grid_cap(value); break;
-      case GM2_OPT_SMALL_STAGES:
-        if (value != 4 && value != 5) throw Gm2Error("small stages %d: 4 or 5", value);
-        set_small_stages(value);
-        break;
-      case GM2_OPT_INPUT_CHUNKS:
-        if (value != 1 && value != 4) throw Gm2Error("input chunks %d: 1 or 4", value);
-        input_chunks_flag().store(value);
-        break;
-      default: throw Gm2Error("unknown option %d", key);
-    }
-  });
+  return guarded([&] { set_default_option(key, value); });
 }
 
 int gm2_get_option(int key, int* value) {
-  return guarded([&] {
-    switch (key) {
-      case GM2_OPT_GEMM_PP: *value = get_gemm_pp(); break;
-      case GM2_OPT_SIDE_STREAM: *value = side_flag().load(); break;
-      case GM2_OPT_RECON_TILE: *value = get_recon_tile(); break;
-      case GM2_OPT_SMALL_SPLIT: *value = get_small_split(); break;
-      case GM2_OPT_BN_EPILOGUE: *value = get_bn_epilogue(); break;
-      case GM2_OPT_SMALL_WAVES: *value = get_small_waves(); break;
-      case GM2_OPT_INPUT_CHUNKS: *value = input_chunks_flag().load(); break;
-      case GM2_OPT_SMALL_STAGES: *value = get_small_stages(); break;
-      case GM2_OPT_GRID_CAP: *value = get_grid_cap(); break;
-      default: throw Gm2Error("unknown option %d", key);
-    }
-  });
+  return guarded([&] { *value = option_get(default_options(), key); });
+}
+
+int gm2_workspace_set_option(void* ws, int key, int value) {
+  return guarded([&] { option_set(ws_state(ws).opt, key, value); });
+}
+
+int gm2_workspace_get_option(void* ws, int key, int* value) {
+  return guarded([&] { *value = option_get(ws_state(ws).opt, key); });
+}
+
+int gm2_workspace_release(void* ws) {
+  return guarded([&] { ws_release(ws); });
 }
 
 int gm2_timing_begin(int kernel_classes) {

@@ -1130,15 +1130,9 @@ static void check_gemm(const GemmArgs<T>& g, int tile) {
 // Tile / split-K plan. Big tiles when they alone fill the chip, or when K is long enough that a
 // split-K slab round trip is cheap next to the work; otherwise the 128-tile, split only when it
 // leaves most CUs idle (and never below 8 K-steps per slice).
-// split-K factor for the 128-tile GEMMs that alone fill the chip with one short-K tile per CU (the
-// hidden-layer GEMMs: 256 tiles, 16 K-steps): > 1 puts that many tiles on each CU so one's loads
-// hide behind another's MFMAs (option GM2_OPT_SMALL_SPLIT; default 1)
-static std::atomic<int>& small_split_flag() {
-  static std::atomic<int> v{1};
-  return v;
-}
-void set_small_split(int s) { small_split_flag().store(std::max(1, std::min(s, 8))); }
-int get_small_split() { return small_split_flag().load(); }
+// (split-K factor for the 128-tile GEMMs that alone fill the chip with one short-K tile per CU, the
+// hidden-layer GEMMs: 256 tiles, 16 K-steps: opts().small_split > 1 puts that many tiles on each
+// CU so one's loads hide behind another's MFMAs; default 1)
 
 template <typename T>
 GemmPlan plan_gemm(const GemmArgs<T>& g) {
@@ -1149,7 +1143,7 @@ GemmPlan plan_gemm(const GemmArgs<T>& g) {
   if (tiles_big >= 256) return {256, 1};
   if (tiles_big > 0 && g.K >= 8192) return {256, cap((256 + tiles_big - 1) / tiles_big)};
   if (tiles_small >= 192) {
-    const int ss = small_split_flag().load(std::memory_order_relaxed);
+    const int ss = opts().small_split;
     return {128, (ss > 1 && tiles_small < 1024 && nk >= 8) ? cap(ss) : 1};
   }
   return {128, cap((256 + tiles_small - 1) / tiles_small)};
@@ -1162,54 +1156,26 @@ static bool use_big(const GemmArgs<T>& g) {
 
 // Main-loop selection for the 256x256 bf16 tiles: the ping-pong loop (default; measured
 // +15-20 % on the long-K GEMMs of the v0 step, profiles/r02_gemm_bench.txt) or the two-stage loop
-// (option GM2_OPT_GEMM_PP = 0, or env GM2_GEMM_PP=0). Read on every launch so a test can switch
-// it in-process (gm2_set_option); both are parity-tested.
-static std::atomic<int>& pp_flag() {
-  static std::atomic<int> on{[] {
-    const char* e = std::getenv("GM2_GEMM_PP");
-    return e && e[0] == '0' ? 0 : 1;
-  }()};
-  return on;
-}
-static bool pp_enabled() { return pp_flag().load(std::memory_order_relaxed) != 0; }
-void set_gemm_pp(int on) { pp_flag().store(on ? 1 : 0, std::memory_order_relaxed); }
-int get_gemm_pp() { return pp_flag().load(std::memory_order_relaxed); }
+// (option GM2_OPT_GEMM_PP = 0, or env GM2_GEMM_PP=0 for the process defaults); both parity-tested.
+static bool pp_enabled() { return opts().gemm_pp != 0; }
 
-// waves per block of the 128x128 fp32-store GEMM tiles (GM2_OPT_SMALL_WAVES: 4 or 8)
-static std::atomic<int>& small_waves_flag() {
-  static std::atomic<int> v{8};  // 8: step 3.52 -> 3.46 ms (profiles/r02_ab_small_waves.txt)
-  return v;
-}
-void set_small_waves(int w) { small_waves_flag().store(w == 8 ? 8 : 4, std::memory_order_relaxed); }
-int get_small_waves() { return small_waves_flag().load(std::memory_order_relaxed); }
-
-// LDS ring depth of those tiles (GM2_OPT_SMALL_STAGES: 4 or 5)
-static std::atomic<int>& small_stages_flag() {
-  static std::atomic<int> v{4};
-  return v;
-}
-void set_small_stages(int n) { small_stages_flag().store(n == 5 ? 5 : 4, std::memory_order_relaxed); }
-int get_small_stages() { return small_stages_flag().load(std::memory_order_relaxed); }
+// waves per block (GM2_OPT_SMALL_WAVES: 4 or 8; 8: step 3.52 -> 3.46 ms, profiles/r02_ab_small_waves.txt)
+// and LDS ring depth (GM2_OPT_SMALL_STAGES: 4 or 5) of the 128x128 fp32-store GEMM tiles
 
 // call f(Cfg{}) with the 128x128 fp32-store tile configuration the options select
 template <class F>
 static auto small_cfg(F&& f) {
-  const bool w8 = small_waves_flag().load(std::memory_order_relaxed) == 8;
-  if (small_stages_flag().load(std::memory_order_relaxed) == 5) return w8 ? f(SmallDeep85{}) : f(SmallDeep5{});
+  const bool w8 = opts().small_waves == 8;
+  if (opts().small_stages == 5) return w8 ? f(SmallDeep85{}) : f(SmallDeep5{});
   return w8 ? f(SmallDeep8{}) : f(SmallDeep{});
 }
 
 // GM2_OPT_GRID_CAP bits: 1 = the output-layer weight-gradient GEMM (side stream, beside the
 // hidden-layer backward chain), 2 = the input-layer one (beside the side stream's last hidden-layer
 // weight gradients) on a capped grid -- same rounds, the last round's idle CUs free for the rest
-static std::atomic<int>& big_grid_cap_flag() {
-  // 2 (dWe0 only): -18 us/step; bit 1 (dW9) measured 20-40 us/step slower: the chain's 256-tile
-  // GEMMs get 41 CUs (6 rounds) while dW9 runs (profiles/r02_grid_cap_ab_*)
-  static std::atomic<int> v{2};
-  return v;
-}
-void set_grid_cap(int bits) { big_grid_cap_flag().store(bits & 7, std::memory_order_relaxed); }
-int get_grid_cap() { return big_grid_cap_flag().load(std::memory_order_relaxed); }
+// (default 2, dWe0 only: -18 us/step; bit 1 (dW9) measured 20-40 us/step slower: the chain's
+// 256-tile GEMMs get 41 CUs (6 rounds) while dW9 runs, profiles/r02_grid_cap_ab_*)
+static int grid_cap_bits() { return opts().grid_cap; }
 
 // hipFuncAttributeMaxDynamicSharedMemorySize is per device: remember (device, kernel) pairs
 static void ensure_lds_attr(const void* fn, int bytes) {
@@ -1309,7 +1275,7 @@ bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hip
   if (force_big && !big) return false;
   StoreEpi ep;
   ep.sq = sq;
-  ep.ntiles = (big_grid_cap_flag().load(std::memory_order_relaxed) & 2) && !force_big;  // dWe0 bit
+  ep.ntiles = (grid_cap_bits() & 2) && !force_big;  // dWe0 bit
   if (big) {
     check_gemm(g, 256);
     store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
@@ -1326,7 +1292,7 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
   StoreEpi ep;
   ep.trans = 1;
   ep.sq = sq;
-  ep.ntiles = big_grid_cap_flag().load(std::memory_order_relaxed) & 1;  // dW9 bit (the launcher sets the count)
+  ep.ntiles = grid_cap_bits() & 1;  // dW9 bit (the launcher sets the count)
   if (use_big(g)) {
     check_gemm(g, 256);
     store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
@@ -1339,17 +1305,12 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
 
 // BatchNorm statistics in the store epilogue (GM2_OPT_BN_EPILOGUE, default on): taken when the
 // plan is one pass of 128-row tiles (the statistics chunk), else the caller runs the separate pass
-static std::atomic<int>& bn_epi_flag() {
-  static std::atomic<int> on{1};
-  return on;
-}
-void set_bn_epilogue(int on) { bn_epi_flag().store(on ? 1 : 0, std::memory_order_relaxed); }
-int get_bn_epilogue() { return bn_epi_flag().load(std::memory_order_relaxed); }
+
 
 template <typename T>
 bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const StoreEpi& bn, hipStream_t s) {
   static_assert(Small::BM == kBnRowChunk, "statistics chunk = row tile");
-  if (!bn_epi_flag().load(std::memory_order_relaxed)) return false;
+  if (!opts().bn_epilogue) return false;
   const GemmPlan p = plan_gemm(g);
   if (p.tile != 128 || p.splits != 1 || (bn.mode && (g.N % 4 || bn.ldy % 4))) return false;
   check_gemm(g, 128);
@@ -1381,7 +1342,7 @@ static void recon_impl_k(const GemmArgs<T>& g, const float* bias, const uint32_t
   static_assert(lds <= 160 * 1024, "LDS budget");
   const int tiles = (g.Mp / C::BM) * (g.Np / C::BN);
   int grid = tiles, ntiles = 0;
-  if (big_grid_cap_flag().load(std::memory_order_relaxed) & 4) {  // same rounds on fewer workgroups
+  if (grid_cap_bits() & 4) {  // same rounds on fewer workgroups
     const int cus = device_cus(), rounds = (tiles + cus - 1) / cus;
     grid = (tiles + rounds - 1) / rounds;
     ntiles = grid < tiles ? tiles : 0;
@@ -1408,16 +1369,11 @@ static void recon_impl(const GemmArgs<T>& g, const float* bias, const uint32_t* 
 
 // the fp32 parity path stays on the 128-tile (a 256-row fp32 dL image would not fit the LDS).
 // GM2_OPT_RECON_TILE: 0 = plan (256 when it fills the chip), 128 / 256 = force (A/B measurements)
-static std::atomic<int>& recon_tile_flag() {
-  static std::atomic<int> v{0};
-  return v;
-}
-void set_recon_tile(int t) { recon_tile_flag().store(t); }
-int get_recon_tile() { return recon_tile_flag().load(); }
+
 
 template <typename T>
 static bool recon_big(const GemmArgs<T>& g) {
-  const int force = recon_tile_flag().load(std::memory_order_relaxed);
+  const int force = opts().recon_tile;
   const bool ok = sizeof(T) == 2 && g.Mp % 256 == 0 && g.Np % 256 == 0;
   if (force == 128) return false;
   if (force == 256) return ok;

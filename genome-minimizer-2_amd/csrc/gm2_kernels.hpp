@@ -66,6 +66,39 @@ struct GemmArgs {
   int pk = 1, qk = 1;
 };
 
+// ---- tuning options (gm2.h GM2_OPT_*): results are bit-identical under every value ----
+// Each workspace carries its own copy (gm2_workspace_set_option); gm2_set_option edits the process
+// defaults that new workspaces and workspace-less calls (gm2_gemm) start from. The launchers read
+// the options of the call in progress through opts(), which an OptionScope sets per C-ABI call.
+struct Options {
+  int gemm_pp = 1;       // GM2_OPT_GEMM_PP      ping-pong main loop of the 256x256 bf16 tiles
+  int side_stream = 1;   // GM2_OPT_SIDE_STREAM  weight-gradient GEMMs on the workspace's side stream
+  int recon_tile = 0;    // GM2_OPT_RECON_TILE   0 plan, 128 / 256 force
+  int small_split = 1;   // GM2_OPT_SMALL_SPLIT  split-K of the chip-filling short-K 128-tile GEMMs
+  int bn_epilogue = 1;   // GM2_OPT_BN_EPILOGUE  BatchNorm statistics in the GEMM store epilogue
+  int small_waves = 8;   // GM2_OPT_SMALL_WAVES  waves of the 128x128 fp32-store tiles (4 or 8)
+  int small_stages = 4;  // GM2_OPT_SMALL_STAGES LDS ring depth of those tiles (4 or 5)
+  int grid_cap = 2;      // GM2_OPT_GRID_CAP     capped grids: 1 dW9, 2 dWe0, 4 recon
+  int input_chunks = 1;  // GM2_OPT_INPUT_CHUNKS launches of the input-layer weight gradient (1 or 4)
+  int defer_output_adam = 0;  // GM2_OPT_DEFER_OUTPUT_ADAM (see gm2.h)
+};
+// validated edit of one option (throws on an unknown key or a bad value)
+void option_set(Options& o, int key, int value);
+int option_get(const Options& o, int key);
+// process defaults: env GM2_GEMM_PP / GM2_SIDE_STREAM read once
+Options default_options();
+void set_default_option(int key, int value);
+// the options of the C-ABI call in progress on this thread
+const Options& opts();
+struct OptionScope {
+  explicit OptionScope(const Options& o);
+  ~OptionScope();
+  OptionScope(const OptionScope&) = delete;
+  OptionScope& operator=(const OptionScope&) = delete;
+  Options saved;
+  int was;
+};
+
 // ---- live per-kernel timing (bench.py): hipEvent pairs around every launch of one class ----
 enum KernelClass { kKcReconLoss = 1, kKcGemmStore = 2, kKcMask = 4 };
 void timing_begin(int classes);
@@ -114,8 +147,7 @@ bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hip
 // tiles of a one-pass launch of g (the sq entries it writes)
 template <typename T>
 int gemm_tiles(const GemmArgs<T>& g);
-void set_bn_epilogue(int on);
-int get_bn_epilogue();
+
 // splits < 0: use plan_gemm's split-K factor. Returns the number of slabs written.
 template <typename T>
 int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, int msplit, int64_t ldc,
@@ -124,19 +156,7 @@ template <typename T>
 int gemm_recon_grid_blocks(const GemmArgs<T>& g);
 template <typename T>
 int gemm_recon_row_tiles(const GemmArgs<T>& g);
-// process-global GEMM main-loop switch (gm2_set_option GM2_OPT_GEMM_PP)
-void set_gemm_pp(int on);
-int get_gemm_pp();
-void set_recon_tile(int t);
-int get_recon_tile();
-void set_small_split(int s);
-int get_small_split();
-void set_small_waves(int w);
-int get_small_waves();
-void set_small_stages(int n);
-int get_small_stages();
-void set_grid_cap(int on);
-int get_grid_cap();
+
 struct GemmPlan {
   int tile, splits;
 };

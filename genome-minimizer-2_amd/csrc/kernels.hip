@@ -41,12 +41,15 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data
   const int c = blockIdx.x * 512 + lane * 8;
   const int rbase = blockIdx.y * 32 + wid * 8;
   const bool in = c < Gp;  // Gp % 128 == 0: whole 4-lane word groups are in or out
+  // reads stop at the lane group holding gene G-1 (ld_data >= roundup(G, 128) is all the caller
+  // promises, while Gp may be padded further, to 256, for the bf16 GEMM tiles)
+  const bool rd = c < G;
   u32x2 v[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int r = rbase + k;
     v[k] = u32x2{0u, 0u};
-    if (in && r < B) {
+    if (rd && r < B) {
       const int64_t src = rows ? (int64_t)rows[r] : (int64_t)r;
       v[k] = __builtin_nontemporal_load((const u32x2*)(data + src * ld_data + c));
     }

@@ -46,6 +46,17 @@ def rank_slice(n, rank, world):
     return (n * rank) // world, (n * (rank + 1)) // world
 
 
+def rank_share(n, rank, world):
+    """Training share [lo, hi) of a global batch of n >= 2 rows: contiguous slices over the first
+    min(world, n // 2) ranks, so every active rank holds >= 2 rows (train-mode BatchNorm needs two,
+    model.py:67) and every row of the batch is trained, as in the reference (trainer.py:109-120).
+    The remaining ranks get an empty share (lo == hi) and contribute zeros to the exchange."""
+    active = max(1, min(world, n // 2))
+    if rank >= active:
+        return n, n
+    return (n * rank) // active, (n * (rank + 1)) // active
+
+
 class GradSync:
     """Bucketed SUM all-reduce of the flat gradient buffer, overlapped with the backward.
 
@@ -67,20 +78,26 @@ class GradSync:
         self.bounds = native.grad_bucket_bounds(native.dims(model.input_dim, model.hidden_dim,
                                                             model.latent_dim, 1))
         self.stream = torch.cuda.Stream(device=grads.device)
-        # the input-layer weight gradient (half the bytes) as four launches, so the exchange of its
-        # first quarters runs under the GEMM of the later ones (bit-identical results)
-        native.set_option(native.OPT_INPUT_CHUNKS, 4)
 
-    def after_backward(self, ran=True):
-        """Enqueue the bucket all-reduces behind the backward just launched (ran=True), or behind
-        whatever the current stream holds (ran=False: this rank contributed zeros)."""
+    @staticmethod
+    def prepare(ws):
+        """The training workspace computes the input-layer weight gradient (half the bytes) as four
+        launches, so the exchange of its first quarters runs under the GEMM of the later ones
+        (bit-identical results). A per-workspace option: nothing else in the process changes."""
+        if ws.get_option(native.OPT_INPUT_CHUNKS) != 4:
+            ws.set_option(native.OPT_INPUT_CHUNKS, 4)
+
+    def after_backward(self, ws, ran=True):
+        """Enqueue the bucket all-reduces behind the backward just launched on workspace `ws`
+        (ran=True), or behind whatever the current stream holds (ran=False: this rank contributed
+        zeros)."""
         cur = torch.cuda.current_stream(self.grads.device)
         with torch.cuda.stream(self.stream):
             if not ran:
                 self.stream.wait_stream(cur)
             for b, (lo, hi) in enumerate(self.bounds):
                 if ran:
-                    native.wait_grad_bucket(b, self.stream)
+                    native.wait_grad_bucket(ws, b, self.stream)
                 if self.buf is not None and b != 1:
                     t = self.buf[lo:hi]
                     t.copy_(self.grads[lo:hi])

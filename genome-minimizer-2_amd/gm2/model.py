@@ -293,8 +293,9 @@ class VAE:
 
 class _Forward(torch.autograd.Function):
     """model(x) on libgm2 with a libgm2 backward (gm2_forward / gm2_backward_outputs). The
-    workspace keeps the forward's activations; a later forward on the same model invalidates them
-    (the backward checks a token and raises)."""
+    workspace keeps the forward's activations; any later call that runs on the same workspace
+    (forward, encode, eval, decode, recon counts, training) invalidates them: the backward checks
+    the workspace's generation counter and raises."""
 
     @staticmethod
     def forward(ctx, params, model, mat, rows, n, eps):
@@ -306,22 +307,22 @@ class _Forward(torch.autograd.Function):
         lv = torch.empty(n, L, device=dev)
         batch = native.make_batch(mat.data, mat.ld, rows, n, eps)
         native.forward(ws, batch, params.detach(), model.bn, int(model.training), probs, G, mu, lv)
-        model._fwd_token = getattr(model, "_fwd_token", 0) + 1
-        ctx.model, ctx.mat, ctx.rows, ctx.n, ctx.token, ctx.train = model, mat, rows, n, model._fwd_token, model.training
+        ctx.model, ctx.mat, ctx.rows, ctx.n, ctx.train = model, mat, rows, n, model.training
+        ctx.ws, ctx.gen = ws, ws.gen
         ctx.save_for_backward(probs, eps)
         return probs, mu, lv
 
     @staticmethod
     def backward(ctx, dprobs, dmu, dlv):
         m = ctx.model
-        if m._fwd_token != ctx.token:
-            raise RuntimeError("VAE.forward activations were overwritten by a later forward of the same model; "
-                               "call backward before the next forward")
+        if m._workspaces.get(m.precision) is not ctx.ws or ctx.ws.gen != ctx.gen:
+            raise RuntimeError("VAE.forward activations were overwritten by a later call on the same model's "
+                               "workspace (forward, encode, eval, decode or training); call backward first")
         probs, eps = ctx.saved_tensors
         if dprobs is None:
             dprobs = torch.zeros_like(probs)
         grads = torch.empty_like(m.params)
-        ws = m.workspace(m.precision, ctx.n)
+        ws = ctx.ws
         batch = native.make_batch(ctx.mat.data, ctx.mat.ld, ctx.rows, ctx.n, eps)
         native.backward_outputs(ws, batch, m.params.detach(), int(ctx.train), probs, m.input_dim,
                                 dprobs.contiguous(), None if dmu is None else dmu.contiguous(),

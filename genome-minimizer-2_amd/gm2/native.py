@@ -29,7 +29,10 @@ EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_of
            "gm2_grad_norm", "gm2_adam_step", "gm2_eval_forward", "gm2_decode_mask", "gm2_encode", "gm2_forward", "gm2_backward_outputs",
            "gm2_reparameterize", "gm2_packed_row_bytes", "gm2_decode_bits", "gm2_mask_count_groups",
            "gm2_mask_row_offsets", "gm2_mask_compact", "gm2_recon_counts",
-           "gm2_gemm", "gm2_grad_bucket_bounds", "gm2_wait_grad_bucket", "gm2_set_option", "gm2_get_option", "gm2_timing_begin", "gm2_timing_end"]
+           "gm2_gemm", "gm2_grad_bucket_bounds", "gm2_wait_grad_bucket", "gm2_set_option", "gm2_get_option",
+           "gm2_workspace_set_option", "gm2_workspace_get_option", "gm2_workspace_release",
+           "gm2_timing_begin", "gm2_timing_end"]
+ABI_VERSION = 3
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
 OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE, OPT_SMALL_SPLIT, OPT_BN_EPILOGUE, OPT_SMALL_WAVES = 1, 2, 3, 4, 5, 6
 OPT_INPUT_CHUNKS, OPT_SMALL_STAGES, OPT_GRID_CAP = 7, 8, 9
@@ -85,9 +88,12 @@ def lib():
         "gm2_recon_counts": (C.c_int, [dp, i32, C.POINTER(Batch), vp, vp, C.c_float, vp, vp, vp]),
         "gm2_gemm": (C.c_int, [i32, i32, i32, vp, i64, vp, i64, vp, i64, i64, i64, i64, i32, vp, vp]),
         "gm2_grad_bucket_bounds": (C.c_int, [dp, C.POINTER(C.c_int64)]),
-        "gm2_wait_grad_bucket": (C.c_int, [i32, vp]),
+        "gm2_wait_grad_bucket": (C.c_int, [vp, i32, vp]),
         "gm2_set_option": (C.c_int, [i32, i32]),
         "gm2_get_option": (C.c_int, [i32, C.POINTER(C.c_int)]),
+        "gm2_workspace_set_option": (C.c_int, [vp, i32, i32]),
+        "gm2_workspace_get_option": (C.c_int, [vp, i32, C.POINTER(C.c_int)]),
+        "gm2_workspace_release": (C.c_int, [vp]),
         "gm2_timing_begin": (C.c_int, [i32]),
         "gm2_timing_end": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     }
@@ -95,8 +101,8 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.gm2_abi_version() != 2:
-        raise RuntimeError("libgm2 ABI mismatch")
+    if L.gm2_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"libgm2 ABI mismatch: library {L.gm2_abi_version()}, binding {ABI_VERSION}")
     _lib = L
     return L
 
@@ -133,7 +139,12 @@ def workspace_size(d: Dims, prec: int) -> int:
 
 
 class Workspace:
-    """Caller-owned device scratch of one (dims, precision) geometry."""
+    """Caller-owned device scratch of one (dims, precision) geometry, with its own tuning options
+    (set_option) and host-side state in libgm2 (released with the buffer).
+
+    `gen` counts the calls that overwrote the workspace's activations (every wrapper below that
+    runs a forward, encode, decode or backward on it), so a holder of activations can check that
+    nobody has used the workspace since (model.py _Forward)."""
 
     def __init__(self, d: Dims, prec: int, device):
         self.d, self.prec = d, prec
@@ -142,8 +153,29 @@ class Workspace:
         base = self.buf.data_ptr()
         self.off = (-base) % 256
         self.ptr = C.c_void_p(base + self.off)
+        self.gen = 0
         check(lib().gm2_workspace_init(C.byref(d), prec, self.ptr, self.nbytes, stream()),
               "gm2_workspace_init")
+        self._lib = lib()
+
+    def set_option(self, key: int, value: int):
+        """Tuning switch of this workspace only (gm2.h GM2_OPT_*)."""
+        check(lib().gm2_workspace_set_option(self.ptr, int(key), int(value)), "gm2_workspace_set_option")
+
+    def get_option(self, key: int) -> int:
+        v = C.c_int()
+        check(lib().gm2_workspace_get_option(self.ptr, int(key), C.byref(v)), "gm2_workspace_get_option")
+        return v.value
+
+    def __del__(self):
+        lb = getattr(self, "_lib", None)
+        if lb is not None and getattr(self, "ptr", None) is not None:
+            try:
+                # the device memory may still be read by queued kernels; the caching allocator
+                # reuses it only in stream order, and only the host-side state goes here
+                lb.gm2_workspace_release(self.ptr)
+            except Exception:
+                pass
 
 
 def make_batch(data, ld, rows, n, eps, next: "Batch | None" = None) -> Batch:
@@ -151,8 +183,12 @@ def make_batch(data, ld, rows, n, eps, next: "Batch | None" = None) -> Batch:
     rows are gathered during this step's tail (gm2_batch.next). Keep its tensors unchanged until then."""
     b = Batch(data.data_ptr(), int(ld), None if rows is None else rows.data_ptr(), int(n),
               None if eps is None else eps.data_ptr())
+    # the tensors the descriptor points at stay alive as long as it does (a staged `next` batch is
+    # matched by address in the following call: its rows must not be freed and reallocated before)
+    b._keep = (data, rows, eps)
     if next is not None:
         b.next = C.pointer(next)
+        b._keep_next = next
     return b
 
 
@@ -161,6 +197,7 @@ def sync_shadows(ws: Workspace, params):
 
 
 def train_fwd_bwd(ws: Workspace, batch: Batch, params, grads, bn, scal, loss):
+    ws.gen += 1
     check(lib().gm2_train_fwd_bwd(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), ptr(grads), ptr(bn),
                                   ptr(scal), ptr(loss), ws.ptr, stream()), "gm2_train_fwd_bwd")
 
@@ -176,26 +213,31 @@ def adam_step(ws: Workspace, params, grads, m, v, scal):
 
 
 def eval_forward(ws: Workspace, batch: Batch, params, bn, scal, loss):
+    ws.gen += 1
     check(lib().gm2_eval_forward(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), ptr(bn), ptr(scal),
                                  ptr(loss), ws.ptr, stream()), "gm2_eval_forward")
 
 
 def decode_mask(ws: Workspace, params, bn, z, n, mask, ld_mask, probs=None, ld_probs=0):
+    ws.gen += 1
     check(lib().gm2_decode_mask(C.byref(ws.d), ptr(params), ptr(bn), ptr(z), int(n), ptr(mask), int(ld_mask),
                                 ptr(probs), int(ld_probs), ws.ptr, stream()), "gm2_decode_mask")
 
 
 def encode(ws: Workspace, batch: Batch, params, bn, mu, logvar):
+    ws.gen += 1
     check(lib().gm2_encode(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), ptr(bn), ptr(mu), ptr(logvar),
                            ws.ptr, stream()), "gm2_encode")
 
 
 def forward(ws: Workspace, batch: Batch, params, bn, train, probs, ld_probs, mu=None, logvar=None):
+    ws.gen += 1
     check(lib().gm2_forward(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), ptr(bn), int(train), ptr(probs),
                             int(ld_probs), ptr(mu), ptr(logvar), ws.ptr, stream()), "gm2_forward")
 
 
 def backward_outputs(ws: Workspace, batch: Batch, params, train, probs, ld_probs, dprobs, dmu, dlogvar, grads):
+    ws.gen += 1
     check(lib().gm2_backward_outputs(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), int(train), ptr(probs),
                                      int(ld_probs), ptr(dprobs), ptr(dmu), ptr(dlogvar), ptr(grads), ws.ptr,
                                      stream()), "gm2_backward_outputs")
@@ -212,6 +254,7 @@ def packed_row_bytes(G: int) -> int:
 
 
 def decode_bits(ws: Workspace, params, bn, z, n, bits, ld_bits, probs=None, ld_probs=0):
+    ws.gen += 1
     check(lib().gm2_decode_bits(C.byref(ws.d), ptr(params), ptr(bn), ptr(z), int(n), ptr(bits), int(ld_bits),
                                 ptr(probs), int(ld_probs), ws.ptr, stream()), "gm2_decode_bits")
 
@@ -232,6 +275,7 @@ def mask_compact(bits, n, ld_bits, keep_bits, offsets, indices):
 
 
 def recon_counts(ws: Workspace, batch: Batch, params, bn, threshold, counts):
+    ws.gen += 1
     check(lib().gm2_recon_counts(C.byref(ws.d), ws.prec, C.byref(batch), ptr(params), ptr(bn), float(threshold),
                                  ptr(counts), ws.ptr, stream()), "gm2_recon_counts")
 
@@ -251,14 +295,15 @@ def grad_bucket_bounds(d: Dims):
     return [(lh[2 * i], lh[2 * i + 1]) for i in range(GRAD_BUCKETS)]
 
 
-def wait_grad_bucket(bucket: int, stream_obj):
+def wait_grad_bucket(ws: Workspace, bucket: int, stream_obj):
     """Make `stream_obj` (a torch.cuda.Stream) wait until gradient bucket `bucket` of the last
-    train_fwd_bwd on this device is final (device-side wait)."""
-    check(lib().gm2_wait_grad_bucket(int(bucket), C.c_void_p(stream_obj.cuda_stream)), "gm2_wait_grad_bucket")
+    backward on workspace `ws` is final (device-side wait)."""
+    check(lib().gm2_wait_grad_bucket(ws.ptr, int(bucket), C.c_void_p(stream_obj.cuda_stream)), "gm2_wait_grad_bucket")
 
 
 def set_option(key: int, value: int):
-    """Process-global tuning switch (gm2.h GM2_OPT_*)."""
+    """Process DEFAULT of a tuning switch (gm2.h GM2_OPT_*): what workspaces created afterwards
+    start with. To change a live workspace use Workspace.set_option."""
     check(lib().gm2_set_option(int(key), int(value)), "gm2_set_option")
 
 

@@ -27,7 +27,7 @@ import torch
 
 from . import native
 from .data import StrainLoader, as_strain_loader
-from .ddp import GradSync, average_running_stats, get_dist, rank_slice, rank_world, reduce_loss_rows
+from .ddp import GradSync, average_running_stats, get_dist, rank_share, rank_slice, rank_world, reduce_loss_rows
 from .loss_components import (GeneAbundanceLoss, KLDivergenceLoss, L1RegularizationLoss, LossComponent,
                               ReconstructionLoss, fused_supported)
 
@@ -316,20 +316,23 @@ class VAETrainer:
         ws = model.workspace(model.precision, (loader.batch_size + world - 1) // world)
         rec = torch.zeros(max(nb, 1), native.LOSS_SLOTS, dtype=torch.float64, device=self.device)
         sync = self._grad_sync(dist) if dist else None
+        if sync:
+            sync.prepare(ws)
         for bi, rows in enumerate(batches):
             n = rows.shape[0]
-            lo, hi = rank_slice(n, rank, world)
+            lo, hi = rank_share(n, rank, world)
             eps = self._eps(n)[lo:hi].contiguous()
-            ran = hi - lo >= 2
+            ran = hi > lo
             if ran:
                 batch = native.make_batch(mat.data, mat.ld, rows[lo:hi], hi - lo, eps)
                 native.train_fwd_bwd(ws, batch, model.params, self.grads, model.bn, scal[bi], rec[bi])
             else:
-                # DDP only: fewer than 2 of this global batch's rows landed on this rank; train-mode
-                # BatchNorm cannot run on them, so this rank contributes a zero gradient
+                # DDP only: a global batch of fewer than 2 rows per rank runs on its first n // 2
+                # ranks (every row is still trained, each active rank with >= 2 rows for train-mode
+                # BatchNorm); this rank contributes a zero gradient and zero loss sums
                 self.grads.zero_()
             if sync:
-                sync.after_backward(ran)
+                sync.after_backward(ws, ran)
             native.grad_norm(ws, model.params, self.grads, scal[bi], rec[bi])
             native.adam_step(ws, model.params, self.grads, self.optimizer.exp_avg, self.optimizer.exp_avg_sq,
                              scal[bi])

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GM2_ABI_VERSION 2
+#define GM2_ABI_VERSION 3
 #define GM2_NUM_PARAMS 30 /* tensors in model.parameters() */
 #define GM2_NUM_SCALARS 16
 
@@ -101,8 +101,14 @@ int gm2_param_count(const gm2_dims* d, int64_t* n_params);
 int gm2_param_offsets(const gm2_dims* d, int64_t* offsets /* [GM2_NUM_PARAMS + 1] */);
 int gm2_workspace_size(const gm2_dims* d, int precision, size_t* bytes);
 
-/* Initialise a workspace (zero it, lay out GEMM shadows and pads). Call once after allocation. */
+/* Initialise a workspace (zero it, lay out GEMM shadows and pads). Call once after allocation.
+ * The library keeps a little host-side state per workspace, keyed by its address: its tuning
+ * options (copied from the process defaults here), its side stream, its gradient-bucket events and
+ * its staged input slot. Nothing is shared between workspaces, so two models (or a training and a
+ * sampling workspace) can be used in one process; one workspace is used from one host thread at a
+ * time. gm2_workspace_release drops that state (call it before freeing the device memory). */
 int gm2_workspace_init(const gm2_dims* d, int precision, void* ws, size_t ws_bytes, void* stream);
+int gm2_workspace_release(void* ws);
 
 /* Re-derive the padded GEMM copies of the Linear weights from `params` (after init,
  * load_state_dict, or any host-side edit). gm2_adam_step keeps them current itself. */
@@ -124,11 +130,12 @@ int gm2_train_fwd_bwd(const gm2_dims* d, int precision, const gm2_batch* batch, 
  *          exchange of the first quarters runs under the GEMM of the later ones).
  * gm2_grad_bucket_bounds writes [lo, hi) element offsets per bucket (lo_hi[2*GM2_GRAD_BUCKETS]).
  * gm2_wait_grad_bucket makes `stream` wait (device-side, no host sync) until that bucket of the
- * most recent gm2_train_fwd_bwd on the current device is written, so a caller can start the
- * all-reduce of bucket b on a communication stream while the rest of the backward still runs. */
+ * most recent gm2_train_fwd_bwd / gm2_backward_outputs on workspace `ws` is written, so a caller
+ * can start the all-reduce of bucket b on a communication stream while the rest of that backward
+ * still runs. Call it after the backward it refers to and before the next one on `ws`. */
 #define GM2_GRAD_BUCKETS 6
 int gm2_grad_bucket_bounds(const gm2_dims* d, int64_t* lo_hi);
-int gm2_wait_grad_bucket(int bucket, void* stream);
+int gm2_wait_grad_bucket(void* ws, int bucket, void* stream);
 
 /* L1 term + clip_grad_norm_ statistics (trainer.py:119; loss_components.py:167-184): computes
  * ||g + lambda*sign(theta)||_2 (loss slot [4]), sum|theta| (slot [3]) and the clip coefficient
@@ -225,12 +232,16 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  * own stream; gm2_timing_end synchronises those events and returns their summed duration and the
  * launch count. Classes: GM2_KC_RECON_LOSS (decoder output layer GEMM + fused BCE / dlogits
  * epilogue), GM2_KC_GEMM_STORE (every other GEMM), GM2_KC_MASK (sampling output layer GEMM). */
-/* Process-global tuning switches (no effect on results' semantics; both paths are parity-tested):
+/* Tuning switches (no effect on results' semantics; every value is parity-tested). Each workspace
+ * has its own set: gm2_workspace_set_option / gm2_workspace_get_option edit / read it and act on
+ * the calls that use that workspace. gm2_set_option / gm2_get_option edit / read the PROCESS
+ * DEFAULTS: the set a workspace receives at gm2_workspace_init, and the one gm2_gemm (no
+ * workspace) runs with.
  *   GM2_OPT_GEMM_PP     1 = ping-pong (4-phase, staggered wave groups) main loop for the 256x256
- *                       bf16 GEMM tiles (default), 0 = two-stage loop. Initial value from env
+ *                       bf16 GEMM tiles (default), 0 = two-stage loop. Process default from env
  *                       GM2_GEMM_PP (0 disables).
- *   GM2_OPT_SIDE_STREAM 1 = weight-gradient GEMMs on a forked side stream (default), 0 = all on
- *                       the caller's stream. Initial value from env GM2_SIDE_STREAM.
+ *   GM2_OPT_SIDE_STREAM 1 = weight-gradient GEMMs on the workspace's forked side stream (default),
+ *                       0 = all on the caller's stream. Process default from env GM2_SIDE_STREAM.
  *   GM2_OPT_RECON_TILE  output-layer loss GEMM tile: 0 = plan (default), 128 or 256 = force.
  *   GM2_OPT_SMALL_SPLIT split-K factor (1..8) of the chip-filling short-K 128-tile GEMMs (the
  *                       hidden layers).
@@ -259,6 +270,8 @@ enum {
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);
+int gm2_workspace_set_option(void* ws, int key, int value);
+int gm2_workspace_get_option(void* ws, int key, int* value);
 
 enum { GM2_KC_RECON_LOSS = 1, GM2_KC_GEMM_STORE = 2, GM2_KC_MASK = 4 };
 int gm2_timing_begin(int kernel_classes);

@@ -15,7 +15,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from gm2.ddp import average_running_stats, rank_slice, reduce_loss_rows
+from gm2.ddp import average_running_stats, rank_share, rank_slice, reduce_loss_rows
 from oracle import vae_oracle as O
 
 G, H, L, B = 40, 16, 4, 27
@@ -87,6 +87,21 @@ def test_rank_slice_partitions():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def test_rank_share_trains_every_row_with_two_per_rank():
+    """Training shares (gm2.ddp.rank_share): contiguous, covering every row of the global batch,
+    every non-empty share >= 2 rows (train-mode BatchNorm), as many ranks active as that allows."""
+    for world in (1, 2, 3, 8):
+        for n in list(range(2, 40)) + [4095, 4096, 100001]:
+            spans = [rank_share(n, r, world) for r in range(world)]
+            rows = [i for lo, hi in spans for i in range(lo, hi)] if n < 5000 else None
+            if rows is not None:
+                assert rows == list(range(n))
+            live = [(lo, hi) for lo, hi in spans if hi > lo]
+            assert all(hi - lo >= 2 for lo, hi in live)
+            assert len(live) == min(world, n // 2)
+            assert sum(hi - lo for lo, hi in live) == n
 
 
 def test_two_rank_step(tmp_path):

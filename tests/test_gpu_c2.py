@@ -1,8 +1,13 @@
-"""Parity at the headline configuration C2's real dimensions (BASELINE.json configs[1]): v0 preset,
-G = 55,039 genes, hidden 1024, latent 64, a batch of 4096 strain rows of the synthetic F4-shaped
-pan-genome matrix. One full libgm2 step (gm2_train_fwd_bwd + gm2_grad_norm) against the oracle's
-explicit gradients (oracle.manual_grads_emulated: the math of the CPU oracle pinned to the
-reference's goldens) evaluated on the device:
+"""Parity at the real dimensions of every single-GPU-sized configuration of BASELINE.json:
+  * C2 (configs[1], the headline): v0 preset, G = 55,039 genes, hidden 1024, latent 64;
+  * C3 (configs[2]): v1 preset (hidden 512, latent 32, gene abundance w*gamma and L1 lambda 0.01),
+    G = 55,039;
+  * C5's per-GPU step (configs[4]): v0 on the 20,000-gene synthetic matrix (G padded to 20,224 =
+    79 x 256 in the bf16 workspace, so every G-wide GEMM takes the 256x256 tiles);
+each on a batch of 4096 strain rows of a synthetic pan-genome matrix. One full libgm2 step
+(gm2_train_fwd_bwd + gm2_grad_norm + gm2_adam_step) against the oracle's explicit gradients
+(oracle.manual_grads_emulated: the math of the CPU oracle pinned to the reference's goldens)
+evaluated on the device:
 
   * EXACT = fp64 (no rounding anywhere): the distance every path is measured from.
   * the reference's own arithmetic: the same math in fp32 (torch fp32 GEMMs) — for the f32 path;
@@ -18,8 +23,13 @@ relative error fro(a) = ||a - EXACT||_2 / ||EXACT||_2 (stable under the element-
 ill-conditioned evaluation; the max-element errors are printed next to it): per tensor,
   fro(libgm2) <= 3 * fro(reference arithmetic) + floor
 (floor 2e-4 for f32, 1e-3 for bf16); losses within rel 1e-5 (f32) / 1e-4 (bf16, vs the emulated
-sums), the clip norm within rel 1e-4 / 2e-2. Pre-BN Linear biases have an exactly-zero true
-gradient (train-mode BatchNorm) and are compared absolutely.
+sums), the clip norm within rel 1e-4 / 2e-2, sum |theta| (C3's L1 term) within rel 1e-6. Pre-BN
+Linear biases have an exactly-zero true gradient (train-mode BatchNorm) and are compared
+absolutely. The Adam step (with C3's L1 sign term and the clip coefficient) is compared with the
+oracle's torch.optim.Adam formula applied on the device to the GPU's own gradients: abs 2e-7.
+
+test_c2_bf16_trajectory follows 20 consecutive C2 training steps (bf16) against the fp32 oracle's
+own 20-step trajectory (see its docstring for the drift bound).
 """
 import numpy as np
 import pytest
@@ -30,8 +40,10 @@ from oracle import vae_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-G, H, L, B = 55039, 1024, 64, 4096
+B = 4096
 BETA = 0.1
+# (name, G, H, L, w*gamma, lambda): v0 / v1 hyper-parameters at epoch 0 (experiments.py:42-73)
+CONFIGS = {"C2": (55039, 1024, 64, 0.0, 0.0), "C3": (55039, 512, 32, 1.0, 0.01), "C5": (20000, 1024, 64, 0.0, 0.0)}
 
 
 def _prebn_bias(name):
@@ -39,36 +51,58 @@ def _prebn_bias(name):
     return p[0] in ("encoder", "decoder") and p[1] in ("0", "3", "6") and p[2] == "bias"
 
 
-@pytest.fixture(scope="module")
-def c2_state():
-    from gm2.data import synthetic_pangenome
-    torch.manual_seed(2024)
-    P = O.init_params(G, H, L)
-    S = O.init_bn_state(H)
-    P, S = perturb_bn(P, S, 99)
-    X = synthetic_pangenome(B, G, seed=12345)
-    torch.manual_seed(5)
-    eps = torch.randn(B, L)
-    return P, S, X, eps
+_STATES = {}
+
+
+def _state(cfg):
+    if cfg not in _STATES:
+        from gm2.data import synthetic_pangenome
+        G, H, L, _, _ = CONFIGS[cfg]
+        torch.manual_seed(2024)
+        P = O.init_params(G, H, L)
+        S = O.init_bn_state(H)
+        P, S = perturb_bn(P, S, 99)
+        X = synthetic_pangenome(B, G, seed=12345)
+        torch.manual_seed(5)
+        eps = torch.randn(B, L)
+        _STATES.clear()  # one configuration's host state at a time
+        _STATES[cfg] = (P, S, X, eps)
+    return _STATES[cfg]
 
 
 @pytest.mark.parametrize("prec", ["f32", "bf16"])
-def test_c2_train_step_real_dims(prec, c2_state):
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C5"])
+def test_train_step_real_dims(cfg, prec):
     from gm2 import native
     from gm2.data import ResidentMatrix
     from gpu_helpers import scalars, to_model
-    P, S, X, eps = c2_state
+    G, H, L, WG, LAM = CONFIGS[cfg]
+    P, S, X, eps = _state(cfg)
     pr = native.GM2_F32 if prec == "f32" else native.GM2_BF16
     m = to_model(P, S, G, H, L, pr)
     mat = ResidentMatrix(X)
     ws = m.workspace(pr, B)
     grads = torch.zeros_like(m.params)
     loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
-    sc = scalars(beta=BETA, wgamma=0.0, lam=0.0)
+    sc = scalars(beta=BETA, wgamma=WG, lam=LAM)
     native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, B, eps.cuda()), m.params, grads, m.bn, sc, loss)
     native.grad_norm(ws, m.params, grads, sc, loss)
+    # the Adam step on the clipped (+L1) gradient, from zero moments (the first step of a run)
+    p0 = m.params.clone()
+    mom = torch.zeros_like(m.params)
+    vel = torch.zeros_like(m.params)
+    native.adam_step(ws, m.params, grads, mom, vel, sc)
     torch.cuda.synchronize()
     lt = loss.cpu().numpy()
+    coef = np.float32(min(1.0, 1.0 / (lt[4] + 1e-6)))
+    gg = (grads + LAM * torch.sign(p0)) * float(coef)
+    st = O.AdamState(lr=1e-3)
+    Pf = {"p": p0.clone()}
+    O.adam_step(Pf, {"p": gg}, st)
+    assert (m.params - Pf["p"]).abs().max().item() <= 2e-7
+    assert (mom - st.m["p"]).abs().max().item() <= 1e-6 * st.m["p"].abs().max().item() + 1e-12
+    assert (vel - st.v["p"]).abs().max().item() <= 1e-6 * st.v["p"].abs().max().item() + 1e-20
+    del p0, mom, vel, gg, Pf, st
     got = grads.cpu().numpy()
     del ws
     # fp64 references on the device
@@ -78,10 +112,10 @@ def test_c2_train_step_real_dims(prec, c2_state):
     x = torch.tensor(X, device=dev)
     ed = eps.to(dev)
     torch.backends.cuda.matmul.allow_tf32 = False
-    exact, sums = O.manual_grads_emulated(Pd, Sd, x, ed, BETA, 0.0)
+    exact, sums = O.manual_grads_emulated(Pd, Sd, x, ed, BETA, WG)
     exact = {k: v.cpu() for k, v in exact.items()}
     rnd = O.bf16_round if prec == "bf16" else None
-    ref32, sums32 = O.manual_grads_emulated(Pd, Sd, x, ed, BETA, 0.0, operand_round=rnd, dtype=torch.float32)
+    ref32, sums32 = O.manual_grads_emulated(Pd, Sd, x, ed, BETA, WG, operand_round=rnd, dtype=torch.float32)
     ref32 = {k: v.cpu().double() for k, v in ref32.items()}
     if prec == "bf16":
         sums = sums32  # the loss of the bf16 arithmetic (rounded operands)
@@ -119,7 +153,110 @@ def test_c2_train_step_real_dims(prec, c2_state):
         if not ok:
             fails.append(msg)
     assert not fails, "\n".join(fails)
-    # clip norm of the data gradient (no L1 in v0)
-    norm = float(np.sqrt(sum((exact[n].double() ** 2).sum().item() for n in exact)))
+    # clip norm of the data gradient + lambda*sign(theta) (L1 only in C3), and sum |theta|
+    norm = float(np.sqrt(sum(((exact[n].double() + LAM * torch.sign(P[n]).double()) ** 2).sum().item()
+                             for n in exact)))
     assert abs(lt[4] - norm) <= (1e-4 if prec == "f32" else 2e-2) * norm, (lt[4], norm)
-    assert lt[3] == 0.0
+    if LAM:
+        l1 = sum(v.double().abs().sum().item() for v in P.values())
+        assert abs(lt[3] - l1) <= 1e-6 * l1, (lt[3], l1)
+    else:
+        assert lt[3] == 0.0
+
+
+def _oracle_trajectory(P, S, xs, epss, operand_round, steps):
+    """The reference's training step (manual_grads_emulated in fp32 on the device: the oracle's
+    explicit gradient of the autograd chain; clip_grad_norm_ max_norm 1; torch.optim.Adam lr 1e-3,
+    trainer.py:109-120) for `steps` batches; operand_round = bf16 rounding emulates the bf16 path's
+    operand storage. Returns the per-step BCE sums and the final parameters."""
+    dev = torch.device("cuda")
+    Pd = {k: v.to(dev).clone() for k, v in P.items()}
+    Sd = {k: v.to(dev) for k, v in S.items()}
+    st = O.AdamState(lr=1e-3)
+    bce = []
+    for i in range(steps):
+        g, sums = O.manual_grads_emulated(Pd, Sd, xs[i], epss[i], BETA, 0.0, operand_round=operand_round,
+                                          dtype=torch.float32)
+        bce.append(sums[0])
+        O.clip_grads(g, 1.0)
+        O.adam_step(Pd, g, st)
+        del g
+    return np.array(bce), Pd
+
+
+def test_c2_bf16_trajectory():
+    """20 consecutive C2 steps (v0, G = 55,039, H = 1024, L = 64, 4096 rows per step drawn from a
+    resident 8,192-strain synthetic matrix): the libgm2 bf16 trajectory against the fp32 oracle's.
+
+    Drift bound, per step k (BCE sum of the step's batch at the step's own parameters):
+        |BCE_libgm2_bf16(k) - BCE_fp32(k)| <= 3 * |BCE_emul_bf16(k) - BCE_fp32(k)| + 1e-4 * BCE_fp32(k)
+    where BCE_emul_bf16 is the oracle trajectory with the bf16 path's operand rounding emulated
+    (the drift the bf16 arithmetic itself causes), and the final parameters satisfy
+        ||theta_libgm2 - theta_fp32|| <= 3 * ||theta_emul - theta_fp32|| + 1e-3 * ||theta_fp32 - theta_0||
+    (over every tensor but the pre-BatchNorm Linear biases, whose gradient is rounding noise).
+    The libgm2 f32 trajectory is held to the fp32 oracle at rel 1e-4 per step. Every step must be
+    finite (bench.py fails on a non-finite step for the same reason)."""
+    from gm2 import native
+    from gm2.data import ResidentMatrix, synthetic_pangenome
+    from gpu_helpers import scalars, to_model
+    G, H, L = 55039, 1024, 64
+    steps = 20
+    torch.manual_seed(77)
+    P = O.init_params(G, H, L)
+    S = O.init_bn_state(H)
+    N = 8192
+    Xall = synthetic_pangenome(N, G, seed=4242)
+    gen = torch.Generator().manual_seed(9)
+    rows = [torch.randperm(N, generator=gen)[:B] for _ in range(steps)]
+    epss = [torch.randn(B, L, generator=gen) for _ in range(steps)]
+    dev = torch.device("cuda")
+    mat = ResidentMatrix(Xall)
+    runs = {}
+    for prec in ("f32", "bf16"):
+        pr = native.GM2_F32 if prec == "f32" else native.GM2_BF16
+        m = to_model(P, S, G, H, L, pr)
+        ws = m.workspace(pr, B)
+        grads = torch.zeros_like(m.params)
+        mom, vel = torch.zeros_like(m.params), torch.zeros_like(m.params)
+        loss = torch.zeros(steps, native.LOSS_SLOTS, dtype=torch.float64, device=dev)
+        for i in range(steps):
+            sc = scalars(beta=BETA, step=i + 1)
+            b = native.make_batch(mat.data, mat.ld, rows[i].to(torch.int32).to(dev), B, epss[i].to(dev))
+            native.train_fwd_bwd(ws, b, m.params, grads, m.bn, sc, loss[i])
+            native.grad_norm(ws, m.params, grads, sc, loss[i])
+            native.adam_step(ws, m.params, grads, mom, vel, sc)
+        torch.cuda.synchronize()
+        lt = loss.cpu().numpy()
+        assert np.isfinite(lt[:, [0, 1, 2, 4]]).all(), f"{prec}: non-finite step"
+        runs[prec] = (lt[:, 0].copy(), m.params.clone())
+        del m, ws, grads, mom, vel
+        torch.cuda.empty_cache()
+    del mat
+    xs = [torch.tensor(Xall[r.numpy()], device=dev) for r in rows]
+    eds = [e.to(dev) for e in epss]
+    ref, Pref = _oracle_trajectory(P, S, xs, eds, None, steps)
+    emu, Pemu = _oracle_trajectory(P, S, xs, eds, O.bf16_round, steps)
+    # parameter distances over every tensor except the pre-BatchNorm Linear biases: their gradient is
+    # pure rounding noise (exactly zero in exact arithmetic) that Adam turns into O(lr) steps of
+    # either sign, and they do not change the model's output (the BatchNorm subtracts them again)
+    names = [n for n, _ in O.param_specs(G, H, L) if not _prebn_bias(n)]
+    off = np.cumsum([0] + [int(np.prod(s)) for _, s in O.param_specs(G, H, L)])
+    spans = [(off[i], off[i + 1]) for i, (n, _) in enumerate(O.param_specs(G, H, L)) if not _prebn_bias(n)]
+    flat = lambda D: torch.cat([D[n].reshape(-1) for n in names])  # noqa: E731
+    sel = lambda t: torch.cat([t[a:b] for a, b in spans])  # noqa: E731
+    th_ref, th_emu = flat(Pref), flat(Pemu)
+    th0 = flat({k: v.to(dev) for k, v in P.items()})
+    f32, th_f32 = runs["f32"][0], sel(runs["f32"][1])
+    bf, th_bf = runs["bf16"][0], sel(runs["bf16"][1])
+    print("step  BCE_fp32_oracle  rel(libgm2 f32)  rel(libgm2 bf16)  rel(emulated bf16)")
+    for k in range(steps):
+        print(f"{k:4d}  {ref[k]:.9e}  {abs(f32[k] - ref[k]) / ref[k]:.3e}  {abs(bf[k] - ref[k]) / ref[k]:.3e}  "
+              f"{abs(emu[k] - ref[k]) / ref[k]:.3e}")
+    assert (np.abs(f32 - ref) <= 1e-4 * ref).all()
+    assert (np.abs(bf - ref) <= 3 * np.abs(emu - ref) + 1e-4 * ref).all()
+    d_bf = (th_bf - th_ref).norm().item()
+    d_emu = (th_emu - th_ref).norm().item()
+    moved = (th_ref - th0).norm().item()
+    print(f"final params: ||bf16 - fp32|| {d_bf:.4g}, ||emulated bf16 - fp32|| {d_emu:.4g}, "
+          f"||fp32 - init|| {moved:.4g}, ||libgm2 f32 - fp32|| {(th_f32 - th_ref).norm().item():.4g}")
+    assert d_bf <= 3 * d_emu + 1e-3 * moved

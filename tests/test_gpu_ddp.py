@@ -11,7 +11,10 @@ gm2_wait_grad_bucket), against the oracle's per-shard math:
   * parameters bit-identical on both ranks after the step (replicas stay in lock step);
   * a 3-batch validation epoch (64 + 64 + 22 rows, each split over the ranks) == the oracle's
     eval-mode losses of the same rows with the GPU's own final parameters (rel 1e-5), i.e. every
-    batch row of the loss record is reduced (the round-1 strided-view bug summed the wrong ones).
+    batch row of the loss record is reduced (the round-1 strided-view bug summed the wrong ones);
+  * a global batch too small to give every rank 2 rows (3 rows on 2 ranks) is trained in full on
+    rank 0 (gm2.ddp.rank_share): the reduced gradient and the epoch losses are the oracle's for
+    all 3 rows, as in the single-device reference (trainer.py:109-120).
 """
 import os
 import socket
@@ -199,8 +202,9 @@ def _exchange_worker(rank, world, port, out_dir):
         grads = torch.zeros_like(m.params)
         loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
         sync = GradSync(dist, m, grads, exchange=ex)
+        sync.prepare(ws)
         native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, Bx, eps), m.params, grads, m.bn, sc, loss)
-        sync.after_backward()
+        sync.after_backward(ws)
         torch.cuda.synchronize()
         res[ex] = grads.cpu().numpy()
     np.savez(os.path.join(out_dir, f"x{rank}.npz"), **res, bounds=np.array(sync.bounds))
@@ -223,3 +227,57 @@ def test_two_rank_bf16_gradient_exchange(tmp_path):
             np.testing.assert_array_equal(got, ref)
         else:
             assert np.abs(got - ref).max() <= 4 * 2.0 ** -9 * np.abs(ref).max()
+
+
+def _ragged_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gm2 import native
+    from gm2.data import ResidentMatrix, StrainLoader
+    from gm2.loss_components import KLDivergenceLoss, ReconstructionLoss
+    from gm2.model import VAE
+    from gm2.trainer import Adam, StepLR, TrainingConfig, VAETrainer
+
+    P, S = _state()
+    m = VAE(G, H, L, precision=native.GM2_F32, init=False)
+    m.load_state_dict({**P, **S})
+    opt = Adam(m, lr=1e-3)
+    tr = VAETrainer(m, opt, StepLR(opt, 20, 0.5), TrainingConfig(n_epochs=N_EPOCHS, max_norm=1.0), eps_rng="cpu")
+    tr.setup_loss_components([ReconstructionLoss(), KLDivergenceLoss(scheduler_type="linear", min_beta=0.1,
+                                                                     max_beta=1.0)])
+    x3 = synth_x(3, G, 5)
+    torch.manual_seed(SEED + 2)
+    losses = tr.train_epoch(StrainLoader(ResidentMatrix(x3), None, BS, shuffle=False), 0)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, f"g{rank}.npz"), grads=tr.grads.cpu().numpy(), params=m.params.cpu().numpy(),
+             rec=np.array([losses["reconstruction"], losses["kl_divergence"]]))
+    dist.destroy_process_group()
+
+
+def test_two_rank_ragged_batch_trains_every_row(tmp_path):
+    port = _free_port()
+    mp.spawn(_ragged_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = np.load(tmp_path / "g0.npz"), np.load(tmp_path / "g1.npz")
+    np.testing.assert_array_equal(r0["params"], r1["params"])
+    np.testing.assert_array_equal(r0["grads"], r1["grads"])
+    P, S = _state()
+    x = torch.tensor(synth_x(3, G, 5), dtype=torch.float32)
+    torch.manual_seed(SEED + 2)
+    torch.empty((), dtype=torch.int64).random_()  # the loader's base seed
+    eps = torch.randn(3, L)
+    beta = O.LossState(O.Preset("t", "linear", 0.1, 1.0), N_EPOCHS).beta(0)
+    g = O.manual_grads(P, S, x, eps, beta, 0.0, 0.0)
+    off = np.cumsum([0] + [int(np.prod(s)) for _, s in O.param_specs(G, H, L)])
+    # the trainer's grads buffer holds the reduced data gradient of the step (before clip / Adam)
+    for i, (name, _) in enumerate(O.param_specs(G, H, L)):
+        parts = name.split(".")
+        if parts[0] in ("encoder", "decoder") and parts[1] in ("0", "3", "6") and parts[2] == "bias":
+            continue
+        ref = g[name].reshape(-1).numpy()
+        got = r0["grads"][off[i]:off[i + 1]]
+        assert np.abs(got - ref).max() <= 1e-4 * max(np.abs(ref).max(), 1e-30), name
+    bce, _, kl = _shard_sums(P, {k: v.clone() for k, v in S.items()}, x, eps, True)
+    assert abs(r0["rec"][0] - bce / 3) <= 1e-5 * abs(bce / 3)
+    assert abs(r0["rec"][1] - np.float32(beta) * (-0.5 * kl) / 3) <= 1e-5 * abs(kl) + 1e-7

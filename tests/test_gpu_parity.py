@@ -445,7 +445,8 @@ def test_capped_grid_bit_identical(G):
     """GM2_OPT_GRID_CAP: the output-layer weight-gradient GEMM on a capped grid (workgroups loop over
     tiles: 320 tiles -> 160 workgroups x 2 at G = 20480), the input-layer one and the output-layer
     loss GEMM (320 genes x strains tiles) give the same gradient, loss record and clip statistics bit
-    for bit as one workgroup per tile; G = 20000 takes the 128-tile plans."""
+    for bit as one workgroup per tile; G = 20000 is padded to 20,224 = 79 x 256 in the bf16 workspace
+    and takes the same 256-tile plans."""
     H, L, B = 1024, 32, 1024
     P, S = perturb_bn(*oracle_state(G, H, L, G + B), seed=31)
     X = synth_x(B, G, 32)
@@ -471,3 +472,59 @@ def test_capped_grid_bit_identical(G):
         native.set_option(native.OPT_GRID_CAP, old)
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_two_workspaces_keep_their_own_options_and_state():
+    """ABI 3: tuning options, side stream, gradient-bucket events and the staged input slot belong to
+    the workspace. Two models trained interleaved in one process, one with the ping-pong main loop,
+    capped grids and four input-layer launches, the other with the two-stage loop, no capped grid
+    and one launch, each read back their own options, and each step is bit-identical to the same
+    step run with that model alone; the process defaults are untouched."""
+    G, H, L, B = 16384, 1024, 32, 512
+    P, S = perturb_bn(*oracle_state(G, H, L, 91), seed=92)
+    X = synth_x(2 * B, G, 93)
+    gen = torch.Generator().manual_seed(94)
+    rows = [torch.randperm(2 * B, generator=gen)[:B].to(torch.int32).cuda() for _ in range(3)]
+    eps = [torch.randn(B, L, generator=gen).cuda() for _ in range(3)]
+    sc = scalars(beta=0.37, wgamma=0.55, lam=0.01)
+    defaults = {k: native.get_option(k) for k in (native.OPT_GEMM_PP, native.OPT_GRID_CAP, native.OPT_INPUT_CHUNKS)}
+    cfg = {"a": {native.OPT_GEMM_PP: 1, native.OPT_GRID_CAP: 7, native.OPT_INPUT_CHUNKS: 4},
+           "b": {native.OPT_GEMM_PP: 0, native.OPT_GRID_CAP: 0, native.OPT_INPUT_CHUNKS: 1}}
+
+    def setup(tag):
+        m = to_model(P, S, G, H, L, native.GM2_BF16)
+        ws = m.workspace(native.GM2_BF16, B)
+        for k, v in cfg[tag].items():
+            ws.set_option(k, v)
+        return m, ws, ResidentMatrix(X)
+
+    def step(state, i):
+        m, ws, mat = state
+        grads = torch.zeros_like(m.params)
+        loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+        native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, rows[i], B, eps[i]), m.params, grads, m.bn, sc,
+                             loss)
+        stream = torch.cuda.Stream()
+        for b in range(native.GRAD_BUCKETS):
+            native.wait_grad_bucket(ws, b, stream)  # this workspace's own bucket events
+        torch.cuda.current_stream().wait_stream(stream)
+        native.grad_norm(ws, m.params, grads, sc, loss)
+        return grads.cpu(), loss.cpu(), m.bn.cpu()
+
+    alone = {}
+    for tag in ("a", "b"):
+        st = setup(tag)
+        alone[tag] = [step(st, i) for i in range(3)]
+    sa, sb = setup("a"), setup("b")
+    inter = {"a": [], "b": []}
+    for i in range(3):
+        inter["a"].append(step(sa, i))
+        inter["b"].append(step(sb, i))
+    torch.cuda.synchronize()
+    for tag, st in (("a", sa), ("b", sb)):
+        for k, v in cfg[tag].items():
+            assert st[1].get_option(k) == v
+        for x, y in zip(alone[tag], inter[tag]):
+            for u, w in zip(x, y):
+                assert torch.equal(u, w)
+    assert {k: native.get_option(k) for k in defaults} == defaults

@@ -98,3 +98,48 @@ def test_sample_train_sample_uses_trained_weights():
         Sn[b + ".running_var"] = m.bn[i, 1].cpu()
     np.testing.assert_allclose(p_after.cpu().numpy(), O.sample_decode(Pn, Sn, z).numpy(), rtol=2e-5, atol=2e-6)
     assert not torch.equal(before, after)
+
+
+def test_c3_million_genomes_properties_and_stratified_oracle():
+    """C3 (BASELINE.json configs[2]): `--mode sample` of 1e6 genomes at v1 dims (G = 55,039,
+    hidden 512, latent 32), z = torch.manual_seed(0); torch.randn(1e6, 32) on the host (SURVEY.md
+    §8d), decoded in 65,536-genome chunks into packed masks on the device (VAE.decode_bits). Every
+    row is checked by size-independent properties against a host recount of the packed rows that
+    reached the host:
+      * genome sizes (PackedMasks.row_sizes, the device popcount + scan) == host popcount per row;
+      * the pad bit beyond G (bit 55,039 of the 6,880-byte row) is zero in every row;
+      * essential-gene counts (PackedMasks.count_groups, a 300-gene table with 1-3 columns each,
+        some negative) == the host's any-of-positions recount of every row;
+    and a stratified subset -- the first and last genome of every chunk -- is decoded by the
+    oracle: bit-exact outside the fp64 rounding band of each logit."""
+    G, H, L, N, chunk = 55039, 512, 32, 1_000_000, 65536
+    P, S = perturb_bn(*oracle_state(G, H, L, 60), seed=61)
+    P["decoder.9.bias"] = torch.linspace(-2.0, 1.0, G)
+    m = to_model(P, S, G, H, L, native.GM2_F32)
+    m.eval()
+    torch.manual_seed(0)
+    z = torch.randn(N, L)
+    pm, _ = m.decode_bits(z.cuda(), chunk=chunk)
+    assert pm.n == N and pm.ld == native.packed_row_bytes(G) == 6880
+    sizes = pm.row_sizes()
+    rng = np.random.Generator(np.random.PCG64(7))
+    ess = {f"e{i}": [int(p) for p in rng.integers(-G, G, size=int(rng.integers(1, 4)))] for i in range(300)}
+    counts = pm.count_groups(ess)
+    host = pm.bits.cpu().numpy()  # [N, 6880] packed rows
+    del pm
+    torch.cuda.empty_cache()
+    assert int((host[:, G // 8] >> (G % 8)).max()) == 0, "pad bits beyond G must be zero"
+    cols = [np.asarray(v) % G for v in ess.values()]
+    for s in range(0, N, chunk):
+        blk = host[s:s + chunk]
+        np.testing.assert_array_equal(np.bitwise_count(blk).sum(axis=1, dtype=np.int64), sizes[s:s + chunk])
+        recount = np.zeros(blk.shape[0], dtype=np.int64)
+        for c in cols:
+            recount += (((blk[:, c // 8] >> (c % 8)) & 1) != 0).any(axis=1)
+        np.testing.assert_array_equal(recount, counts[s:s + chunk])
+    strata = sorted({r for s in range(0, N, chunk) for r in (s, min(s + chunk, N) - 1)})
+    zs = z[strata]
+    mask = np.unpackbits(host[strata], axis=1, count=G, bitorder="little")
+    print(f"mean genome size {sizes.mean():.1f} of {G}; mean essential count {counts.mean():.2f}; "
+          f"{len(strata)} stratified rows")
+    assert _masks_ok(mask, P, S, zs) == 0

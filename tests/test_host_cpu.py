@@ -31,10 +31,20 @@ def test_library_exports_every_declared_symbol():
 def test_header_constants_match_binding():
     """The ctypes mirror (gm2/native.py) uses the values include/gm2.h defines: ABI version, gradient
     bucket count, option keys, the gm2_batch field order (ABI 2 adds `next`); option setters accept
-    and reject values without a GPU, and the bucket bounds tile the gradient buffer in order."""
+    and reject values without a GPU, and the bucket bounds tile the gradient buffer in order. ABI 3:
+    options and bucket events are per workspace; a workspace libgm2 never initialised is refused."""
+    import ctypes
     from gm2 import native
     txt = open(os.path.join(ROOT, "include", "gm2.h")).read()
-    assert int(re.search(r"#define GM2_ABI_VERSION (\d+)", txt).group(1)) == native.lib().gm2_abi_version() == 2
+    assert int(re.search(r"#define GM2_ABI_VERSION (\d+)", txt).group(1)) == native.lib().gm2_abi_version() \
+        == native.ABI_VERSION == 3
+    bogus = ctypes.c_void_p(0x1000)
+    v = ctypes.c_int()
+    assert native.lib().gm2_workspace_set_option(bogus, native.OPT_GRID_CAP, 1) != 0
+    assert "not initialised" in native.lib().gm2_last_error().decode()
+    assert native.lib().gm2_workspace_get_option(bogus, native.OPT_GRID_CAP, ctypes.byref(v)) != 0
+    assert native.lib().gm2_wait_grad_bucket(bogus, 0, None) != 0
+    assert native.lib().gm2_workspace_release(bogus) == 0  # releasing unknown state is a no-op
     assert int(re.search(r"#define GM2_GRAD_BUCKETS (\d+)", txt).group(1)) == native.GRAD_BUCKETS
     opts = dict((k, int(v)) for k, v in re.findall(r"GM2_OPT_([A-Z_]+) = (\d+)", txt))
     for k, v in opts.items():
