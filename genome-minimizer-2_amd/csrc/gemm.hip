@@ -247,6 +247,17 @@ __device__ __forceinline__ void mainloop(const T* __restrict__ P, int64_t ldp, c
         }
       }
     } else {
+      // exact-fp32 path: each K-step's 32 products go into a fresh partial sum that is then added
+      // to the accumulator, so a K-long dot product is a chain of K/32 additions of 32-term blocks
+      // instead of one K-long fma chain. On the long-K GEMMs of the step (K = G = 55,040, the input
+      // layer and the output layer's input gradient) this keeps the rounding error of the train-mode
+      // BatchNorm backward's near-cancelling column sums at the level of the reference's own MKL
+      // arithmetic (tools/diag/c3_chain.py: the single chain was 2.5-6x worse on the hidden layers)
+      f32x4 part[C::FM][C::FN];
+#pragma unroll
+      for (int a = 0; a < C::FM; ++a)
+#pragma unroll
+        for (int b = 0; b < C::FN; ++b) part[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         f32x4 b[C::FN];
@@ -259,9 +270,13 @@ __device__ __forceinline__ void mainloop(const T* __restrict__ P, int64_t ldp, c
           for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int ni = 0; ni < C::FN; ++ni)
-              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[ni][j], acc[mi][ni], 0, 0, 0);
+              part[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[ni][j], part[mi][ni], 0, 0, 0);
         }
       }
+#pragma unroll
+      for (int mi = 0; mi < C::FM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < C::FN; ++ni) acc[mi][ni] += part[mi][ni];
     }
     wait_stages<C>(min(NS - 2, nk - 2 - kt));
     __syncthreads();
@@ -1137,7 +1152,9 @@ static void check_gemm(const GemmArgs<T>& g, int tile) {
 template <typename T>
 GemmPlan plan_gemm(const GemmArgs<T>& g) {
   const int nk = g.K / E<T>::KT;
-  const int tiles_big = (g.Mp % 256 == 0 && g.Np % 256 == 0) ? (g.Mp / 256) * (g.Np / 256) : 0;
+  // (the exact-fp32 path stays on the 128x128 tiles: its K-step partial sums double the accumulator
+  // registers, which the 256x256 tile's 8 waves cannot hold)
+  const int tiles_big = (sizeof(T) == 2 && g.Mp % 256 == 0 && g.Np % 256 == 0) ? (g.Mp / 256) * (g.Np / 256) : 0;
   const int tiles_small = (g.Mp / 128) * (g.Np / 128);
   auto cap = [&](int s) { return std::max(1, std::min({s, 8, std::max(1, nk / 8)})); };
   if (tiles_big >= 256) return {256, 1};
@@ -1253,9 +1270,11 @@ int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
                       const float* bias, hipStream_t s) {
   if (splits < 0) splits = plan_gemm(g).splits;
   const StoreEpi none{};
-  if (use_big(g)) {
-    check_gemm(g, 256);
-    return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
+  if constexpr (sizeof(T) == 2) {  // (256x256 tiles: bf16 only, see plan_gemm)
+    if (use_big(g)) {
+      check_gemm(g, 256);
+      return store_impl<Big, T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s);
+    }
   }
   check_gemm(g, 128);
   return small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s); });
@@ -1270,19 +1289,21 @@ template <typename T>
 bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s, bool force_big) {
   // force_big: a one-pass 256x256-tile launch even where the plan would pick 128 tiles (a row
   // slice of a big-tile GEMM, same per-element results as the whole)
-  const bool big = force_big ? (g.Mp % 256 == 0 && g.Np % 256 == 0) : use_big(g);
+  const bool big = force_big ? (sizeof(T) == 2 && g.Mp % 256 == 0 && g.Np % 256 == 0) : use_big(g);
   if (!force_big && plan_gemm(g).splits != 1) return false;
   if (force_big && !big) return false;
   StoreEpi ep;
   ep.sq = sq;
   ep.ntiles = (grid_cap_bits() & 2) && !force_big;  // dWe0 bit
-  if (big) {
-    check_gemm(g, 256);
-    store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
-  } else {
-    check_gemm(g, 128);
-    small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s); });
+  if constexpr (sizeof(T) == 2) {
+    if (big) {
+      check_gemm(g, 256);
+      store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
+      return true;
+    }
   }
+  check_gemm(g, 128);
+  small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s); });
   return true;
 }
 
@@ -1293,13 +1314,15 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
   ep.trans = 1;
   ep.sq = sq;
   ep.ntiles = grid_cap_bits() & 1;  // dW9 bit (the launcher sets the count)
-  if (use_big(g)) {
-    check_gemm(g, 256);
-    store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
-  } else {
-    check_gemm(g, 128);
-    small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s); });
+  if constexpr (sizeof(T) == 2) {
+    if (use_big(g)) {
+      check_gemm(g, 256);
+      store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
+      return true;
+    }
   }
+  check_gemm(g, 128);
+  small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s); });
   return true;
 }
 

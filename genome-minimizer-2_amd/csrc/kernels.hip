@@ -987,7 +987,8 @@ __global__ __launch_bounds__(256) void k_colsum2(const float* __restrict__ part,
 template <typename T>
 void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* rows, int B, int G, T* X, int64_t ldx,
                         int Gp, int Bp, uint32_t* xbits, int64_t ldxb, hipStream_t s) {
-  if (Gp % 128 || Bp % 64 || ld_data % 16 || ld_data < Gp || ((uintptr_t)data & 15) || (xbits && ldxb * 32 < Gp))
+  // (the gather reads columns < roundup(G, 8) only: ld_data need not cover Gp's extra padding)
+  if (Gp % 128 || Bp % 64 || ld_data % 16 || ld_data < G || ((uintptr_t)data & 15) || (xbits && ldxb * 32 < Gp))
     throw Gm2Error("gather: bad layout (Gp=%d Bp=%d ld=%lld)", Gp, Bp, (long long)ld_data);
   hipLaunchKernelGGL(k_gather<T>, dim3((Gp + 511) / 512, Bp / 32), dim3(256), 0, s, data, ld_data, rows, B, G, Gp, X,
                      ldx, xbits, ldxb);

@@ -268,16 +268,22 @@ def test_two_rank_ragged_batch_trains_every_row(tmp_path):
     torch.empty((), dtype=torch.int64).random_()  # the loader's base seed
     eps = torch.randn(3, L)
     beta = O.LossState(O.Preset("t", "linear", 0.1, 1.0), N_EPOCHS).beta(0)
-    g = O.manual_grads(P, S, x, eps, beta, 0.0, 0.0)
+    # exact (fp64) gradient of all 3 rows, and the reference's own fp32 arithmetic (torch CPU)
+    g64 = O.manual_grads({k: v.double() for k, v in P.items()}, {k: v.double() for k, v in S.items()}, x.double(),
+                         eps.double(), beta, 0.0, 0.0)
+    g32 = O.manual_grads(P, S, x, eps, beta, 0.0, 0.0)
     off = np.cumsum([0] + [int(np.prod(s)) for _, s in O.param_specs(G, H, L)])
-    # the trainer's grads buffer holds the reduced data gradient of the step (before clip / Adam)
+    # the trainer's grads buffer holds the reduced data gradient of the step (before clip / Adam);
+    # bar: the C2 method (norm-wise error vs exact <= 3x the reference arithmetic's + 2e-4)
     for i, (name, _) in enumerate(O.param_specs(G, H, L)):
         parts = name.split(".")
         if parts[0] in ("encoder", "decoder") and parts[1] in ("0", "3", "6") and parts[2] == "bias":
             continue
-        ref = g[name].reshape(-1).numpy()
-        got = r0["grads"][off[i]:off[i + 1]]
-        assert np.abs(got - ref).max() <= 1e-4 * max(np.abs(ref).max(), 1e-30), name
+        ex = g64[name].reshape(-1).numpy()
+        nrm = max(float(np.linalg.norm(ex)), 1e-30)
+        f_gpu = float(np.linalg.norm(r0["grads"][off[i]:off[i + 1]] - ex)) / nrm
+        f_ref = float(np.linalg.norm(g32[name].reshape(-1).double().numpy() - ex)) / nrm
+        assert f_gpu <= 3 * f_ref + 2e-4, (name, f_gpu, f_ref)
     bce, _, kl = _shard_sums(P, {k: v.clone() for k, v in S.items()}, x, eps, True)
     assert abs(r0["rec"][0] - bce / 3) <= 1e-5 * abs(bce / 3)
     assert abs(r0["rec"][1] - np.float32(beta) * (-0.5 * kl) / 3) <= 1e-5 * abs(kl) + 1e-7

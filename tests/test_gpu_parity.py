@@ -1,14 +1,11 @@
 """GPU parity: libgm2 (HIP, gfx950) against the CPU oracle and the golden fixtures.
 
 Tolerances (stated per test):
-  * exact-fp32 path (GM2_F32): losses rel 1e-5, gradients rel 1e-4 of the tensor's max |g|
-    (different summation order than MKL + BN in fp64 vs fp32), updated params abs 1e-6.
-  * bf16 path (GM2_BF16, bf16 MFMA operands, fp32 accumulate): losses rel 2e-3. Hidden-layer
-    gradients of this BatchNorm MLP are intrinsically sensitive: rounding ONLY the weights to bf16
-    in the fp32 reference moves them by 10-35 % (max-normalised) at these shapes. So each bf16
-    gradient tensor must satisfy  err(gpu_bf16, ref) <= max(3e-2, 2.5 * err(ref_bf16W, ref))  and
-    cosine(gpu_bf16, ref) >= 1 - 3 * (1 - cosine(ref_bf16W, ref)) - 1e-3, where ref_bf16W is the
-    oracle's explicit gradient with bf16-rounded weights (the error budget bf16 storage alone implies).
+  * training step (both paths): the C2 method of tests/test_gpu_c2.py -- every gradient tensor's
+    norm-wise error against the EXACT (fp64) oracle gradient is at most 3x the error of the
+    reference arithmetic (f32 path: the oracle's torch-CPU/MKL fp32 evaluation; bf16 path: fp32 with
+    the bf16 operand rounding emulated) + a floor (2e-4 / 1e-3); losses rel 1e-5 / 1e-4 against the
+    sums of the same arithmetic; Adam abs 2e-7 from the GPU's own gradients.
   * sampled masks: bit-exact on every element outside the fp32 rounding band of its logit
     (|logit64| > 1e-3: counted and reported; band elements are reported, not asserted).
 Pre-BN Linear biases have an exactly-zero true gradient (rounding noise on both sides) and are
@@ -187,10 +184,16 @@ def _prebn_bias(name):
                                             # >= 128 256x256 output tiles: the big-tile recon kernel
                                             (8192, 256, 32, 1024, 0.55, 0.01)])
 def test_train_step_vs_oracle(prec, G, H, L, B, wg, lam, gemm_pp, bn_epi):
-    """One fused fwd+bwd (+clip+L1+Adam) against the oracle's explicit gradients and its
-    autograd-driven step (trainer.py:109-120 semantics). The shapes cover both BatchNorm statistics
-    routes under bn_epi=1: one-pass 128-row-tile GEMMs take them in the epilogue, the split-K
-    input layer of the last shape keeps the separate pass."""
+    """One fused fwd+bwd (+clip+L1+Adam) against the oracle (trainer.py:109-120 semantics). The
+    shapes cover both BatchNorm statistics routes under bn_epi=1: one-pass 128-row-tile GEMMs take
+    them in the epilogue, the split-K input layer of the last shape keeps the separate pass.
+
+    Gradient bar (the C2 method, tests/test_gpu_c2.py): per tensor, on the norm-wise relative error
+    against EXACT (the oracle's explicit gradient in fp64 on the device),
+        fro(libgm2) <= 3 * fro(reference arithmetic) + floor,
+    where the reference arithmetic is the oracle's own fp32 evaluation on the CPU (torch + MKL: the
+    reference's arithmetic) for the f32 path, and the same math in fp32 with the bf16 path's operand
+    rounding (manual_grads_emulated) for the bf16 path; floor 2e-4 (f32) / 1e-3 (bf16)."""
     P, S = perturb_bn(*oracle_state(G, H, L, G + B), seed=9)
     X = synth_x(B, G, B)
     torch.manual_seed(1)
@@ -207,50 +210,45 @@ def test_train_step_vs_oracle(prec, G, H, L, B, wg, lam, gemm_pp, bn_epi):
     native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, B, ed), m.params, grads, m.bn, sc, loss)
     native.grad_norm(ws, m.params, grads, sc, loss)
     torch.cuda.synchronize()
-    # --- oracle: explicit data gradients + autograd losses
+    # --- exact reference (fp64, device) and the reference arithmetic of this path
+    dev = torch.device("cuda")
     x = torch.tensor(X, dtype=torch.float32)
-    Gref = O.manual_grads(P, S, x, eps, beta, wg, 0.0)
-    S2 = {k: v.clone() for k, v in S.items()}
-    Pl = {k: v.clone().requires_grad_(True) for k, v in P.items()}
-    recon, mu, lv = O.forward(Pl, S2, x, eps, train=True)
-    bce = torch.nn.functional.binary_cross_entropy(recon, x, reduction="sum").item()
-    klraw = torch.sum(1 + lv - mu.pow(2) - lv.exp()).item()
-    psum = recon.sum().item()
+    Pd = {k: v.to(dev) for k, v in P.items()}
+    Sd = {k: v.to(dev) for k, v in S.items()}
+    exact, sums = O.manual_grads_emulated(Pd, Sd, x.to(dev), ed, beta, wg)
+    if prec == "f32":
+        ref = O.manual_grads(P, S, x, eps, beta, wg, 0.0)  # torch-CPU fp32: the reference's arithmetic
+    else:
+        ref, sums = O.manual_grads_emulated(Pd, Sd, x.to(dev), ed, beta, wg, operand_round=O.bf16_round,
+                                            dtype=torch.float32)
     lt = loss.cpu().numpy()
-    rtol_loss = 1e-5 if prec == "f32" else 2e-3
-    assert abs(lt[0] - bce) <= rtol_loss * abs(bce)
-    assert abs(lt[1] - psum) <= rtol_loss * abs(psum)
-    assert abs(lt[2] - klraw) <= rtol_loss * abs(klraw) + 1e-3 * B * L * (1 if prec == "bf16" else 0.01)
-    # gradients per tensor
-    if prec == "bf16":
-        Pb = {k: (v.bfloat16().float() if v.dim() == 2 else v) for k, v in P.items()}
-        Ginh = O.manual_grads(Pb, S, x, eps, beta, wg, 0.0)
+    rtol_loss = 1e-5 if prec == "f32" else 1e-4
+    assert abs(lt[0] - sums[0]) <= rtol_loss * abs(sums[0]), (lt[0], sums[0])
+    assert abs(lt[1] - sums[1]) <= rtol_loss * abs(sums[1]), (lt[1], sums[1])
+    assert abs(lt[2] - sums[2]) <= 1e-4 * abs(sums[2]) + 1e-3 * B * L * (1 if prec == "bf16" else 0.01)
     off = m.offsets
     fails = []
+    floor = 2e-4 if prec == "f32" else 1e-3
     for i, (name, shp) in enumerate(m.specs):
-        got = grads[off[i]:off[i + 1]].cpu().numpy()
-        ref = Gref[name].reshape(-1).numpy()
+        got = grads[off[i]:off[i + 1]].cpu().double().numpy()
+        ex = exact[name].reshape(-1).cpu().double().numpy()
         if _prebn_bias(name):
-            scale = max(float(np.abs(Gref[name.replace("bias", "weight")].numpy()).max()), 1e-12)
+            scale = max(float(np.abs(exact[name.replace("bias", "weight")].cpu().numpy()).max()), 1e-12)
             if np.abs(got).max() > (1e-3 if prec == "f32" else 2e-2) * scale:
                 fails.append(f"{name}: |g|max {np.abs(got).max():.3g} vs weight scale {scale:.3g}")
             continue
-        e = rel_err(got, ref)
-        cos = float((got * ref).sum() / max(np.linalg.norm(got) * np.linalg.norm(ref), 1e-30))
-        if prec == "f32":
-            ok = e <= 1e-4
-            msg = f"{name}: rel err {e:.3g}"
-        else:
-            inh = Ginh[name].reshape(-1).numpy()
-            e_inh = rel_err(inh, ref)
-            c_inh = float((inh * ref).sum() / max(np.linalg.norm(inh) * np.linalg.norm(ref), 1e-30))
-            ok = e <= max(3e-2, 2.5 * e_inh) and cos >= 1 - 3 * (1 - c_inh) - 1e-3
-            msg = f"{name}: rel err {e:.3g} (bf16-weight budget {e_inh:.3g}), cos {cos:.5f} (budget {c_inh:.5f})"
+        r = ref[name].reshape(-1).cpu().double().numpy()
+        nrm = max(float(np.linalg.norm(ex)), 1e-30)
+        f_gpu = float(np.linalg.norm(got - ex)) / nrm
+        f_ref = float(np.linalg.norm(r - ex)) / nrm
+        msg = f"{name}: libgm2 {prec} vs exact fro {f_gpu:.3g}; reference arithmetic fro {f_ref:.3g}"
         print(msg)
-        if not ok:
+        if not f_gpu <= 3 * f_ref + floor:
             fails.append(msg)
     assert not fails, "\n".join(fails)
-    # BN running statistics (train-mode update, momentum 0.1, unbiased var)
+    # BN running statistics (train-mode update, momentum 0.1, unbiased var) against the fp64 forward
+    S2 = {k: v.double().clone() for k, v in S.items()}
+    O.forward({k: v.double() for k, v in P.items()}, S2, x.double(), eps.double(), train=True)
     bn = m.bn.cpu().numpy()
     for i, b in enumerate(O.BNS):
         np.testing.assert_allclose(bn[i, 0], S2[b + ".running_mean"].numpy(), rtol=1e-3 if prec == "bf16" else 2e-5,
@@ -258,12 +256,12 @@ def test_train_step_vs_oracle(prec, G, H, L, B, wg, lam, gemm_pp, bn_epi):
         np.testing.assert_allclose(bn[i, 1], S2[b + ".running_var"].numpy(), rtol=1e-2 if prec == "bf16" else 2e-5,
                                    atol=1e-3 if prec == "bf16" else 2e-6)
     # L1 statistic and clip norm
-    l1 = sum(v.abs().sum().item() for v in P.values())
+    l1 = sum(v.double().abs().sum().item() for v in P.values())
     if lam:
         assert abs(lt[3] - l1) <= 1e-6 * l1
     else:
         assert lt[3] == 0.0  # no L1 component: the clip pass reads gradients only
-    tot = torch.cat([(Gref[n] + lam * torch.sign(P[n])).reshape(-1) for n in P])
+    tot = torch.cat([(exact[n].cpu().double() + lam * torch.sign(P[n]).double()).reshape(-1) for n in P])
     norm = tot.norm().item()
     assert abs(lt[4] - norm) <= (1e-4 if prec == "f32" else 3e-2) * norm
     # Adam step on the clipped grads: compare with the oracle's update from the GPU's own grads
