@@ -95,6 +95,7 @@ struct Layout {
   int64_t colbwd, colbwd_cap;  // per-layer bias-gradient partials of the backward (summed on the side stream)
   int64_t nahdr, nasq;         // norm-ahead header int[4] and per-tile sums of squares (NormAhead)
   int64_t X1, XB1;             // second input slot: the next batch's rows, staged under this step's tail
+  int64_t syncb;               // SyncBN all-reduce vector: 2H + 2 doubles
 };
 
 Layout make_layout(const gm2_dims* gd, int prec) {
@@ -155,6 +156,7 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.scal0 = take(GM2_NUM_SCALARS * 4);
   o.X1 = take(Bm * d.Gp * es);
   o.XB1 = take(Bm * (d.Gp / 32) * 4);
+  o.syncb = take((2 * H + 2) * 8);
   o.total = cur;
   return o;
 }
@@ -224,6 +226,8 @@ struct WsState {
   bool recorded = false;  // a training backward has recorded the bucket events
   SlotState slot;
   hipEvent_t slot_done = nullptr;
+  gm2_allreduce_fn coll = nullptr;  // SyncBN's all-reduce (gm2_workspace_set_collective)
+  void* coll_user = nullptr;
 
   void create() {
     HIP_OK(hipGetDevice(&dev));
@@ -248,6 +252,12 @@ struct WsState {
       for (auto& e : ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     return side;
+  }
+  // SyncBN: SUM-all-reduce `count` doubles at device pointer `buf` across the ranks, on `s`
+  void allreduce(double* buf, int64_t count, hipStream_t s) {
+    if (!coll) throw Gm2Error("GM2_OPT_SYNC_BN needs a collective (gm2_workspace_set_collective)");
+    const int rc = coll(buf, count, (void*)s, coll_user);
+    if (rc != 0) throw Gm2Error("SyncBN all-reduce failed (%d)", rc);
   }
   // make `to` wait for everything enqueued on `from` so far
   void order(hipStream_t from, hipStream_t to) {
@@ -455,8 +465,11 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   const Layout& l = c.lo;
   const int B = (int)b->n;
   if (B <= 0 || B > d.Bm) throw Gm2Error("batch rows %d outside (0, batch_max=%lld]", B, (long long)d.Bm);
-  if (train && B < 2) throw Gm2Error("Expected more than 1 value per channel when training (batch of 1)");
+  const bool sync = train && c.st && c.st->opt.sync_bn;
+  // (SyncBN: the batch statistics span every rank's rows, so one row here is fine)
+  if (train && B < 2 && !sync) throw Gm2Error("Expected more than 1 value per channel when training (batch of 1)");
   check_batch_data(b, d, "batch");
+  double* syncb = (double*)(c.ws + l.syncb);
   const int Bp = (int)round_up(B, kTile);
   const int H = (int)d.H, L = (int)d.L;
   // 1) strain rows -> X [Bp][Gp] (T) + bit-packed target (unless a previous training call staged them)
@@ -479,9 +492,13 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
     }
     linear_pre_bn<T>(c, in, ldin, Bp, c.t(shadow_in[i]), i == 3 ? d.Lr : Kin, B, H, Kin, prm + d.off[kBlk[i][1]],
                      c.f(l.Y[i]), c.f(l.bnpart), train != 0);
+    if (sync) {  // SyncBN: this rank's column sums -> all-reduce -> the global batch's statistics
+      launch_bn_sync_pack(c.f(l.bnpart), B, H, 0, syncb, c.s);
+      c.st->allreduce(syncb, 2 * H + 2, c.s);
+    }
     launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train, prm + d.off[kBlk[i][2]],
                            prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
-                           c.f(l.save[i]), c.t(l.A[i]), c.s);
+                           c.f(l.save[i]), c.t(l.A[i]), c.s, sync ? syncb : nullptr);
     in = c.t(l.A[i]);
     ldin = H;
     Kin = H;
@@ -586,9 +603,15 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
                             prm + d.off[kBlk[i][3]], B, H, c.f(l.bnpart), sum ? c.f(l.DA) : nullptr, c.s);
     // bias-gradient partials go to this layer's own slice: their column sum runs on the side stream
     float* colp = c.f(l.colbwd) + (int64_t)i * l.colbwd_cap;
+    const bool sync = train && st.opt.sync_bn;
+    double* syncb = (double*)(c.ws + l.syncb);
+    if (sync) {  // SyncBN: the batch-coupling sums of the backward over every rank's rows
+      launch_bn_sync_pack(c.f(l.bnpart), B, H, 1, syncb, c.s);
+      st.allreduce(syncb, 2 * H + 2, c.s);
+    }
     launch_bn_bwd_apply<T>(sum ? c.f(l.DA) : c.f(c.slab_off), c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train,
                            c.f(l.save[i]), prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]], gr + d.off[kBlk[i][2]],
-                           gr + d.off[kBlk[i][3]], c.t(l.dY[i]), colp, c.s);
+                           gr + d.off[kBlk[i][3]], c.t(l.dY[i]), colp, c.s, sync ? syncb : nullptr);
     fork();
     launch_colsum(colp, Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, w.s);
     const T* dY = c.t(l.dY[i]);
@@ -683,9 +706,37 @@ void drop_stage(WsState& st, hipStream_t s) {
   st.slot.staged = false;
 }
 
+// SyncBN, a rank with no rows in this global batch: zero gradient and loss sums, the 12 all-reduces
+// with zero contributions in the order the ranks with rows issue them, and the same running-statistics
+// update (the global batch's); bucket events recorded so a gradient exchange can follow
+void sync_bn_no_rows(const Layout& lo, float* gr, float* bn, double* loss, void* ws, hipStream_t s, WsState& st) {
+  const Dims& d = lo.d;
+  const int64_t H = d.H, n = 2 * H + 2;
+  double* syncb = (double*)((char*)ws + lo.syncb);
+  HIP_OK(hipMemsetAsync(gr, 0, (size_t)d.off[NP] * 4, s));
+  HIP_OK(hipMemsetAsync(loss, 0, 3 * sizeof(double), s));
+  for (int i = 0; i < 6; ++i) {
+    HIP_OK(hipMemsetAsync(syncb, 0, (size_t)n * 8, s));
+    st.allreduce(syncb, n, s);
+    launch_bn_sync_running(syncb, (int)H, bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, s);
+  }
+  for (int i = 5; i >= 0; --i) {
+    HIP_OK(hipMemsetAsync(syncb, 0, (size_t)n * 8, s));
+    st.allreduce(syncb, n, s);
+  }
+  for (auto e : st.bucket) HIP_OK(hipEventRecord(e, s));
+  st.recorded = true;
+}
+
 template <typename T>
 void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr, float* bn, const float* scal,
                double* loss, void* ws, void* strm, WsState& st) {
+  if (b->n == 0 && st.opt.sync_bn) {
+    if (st.slot.staged) HIP_OK(hipStreamWaitEvent((hipStream_t)strm, st.slot_done, 0));
+    st.slot.staged = false;
+    sync_bn_no_rows(lo, gr, bn, loss, ws, (hipStream_t)strm, st);
+    return;
+  }
   Ctx<T> c(lo, ws, strm, &st);
   SlotState& ss = st.slot;
   const bool hit = ss.staged && ss.prec == lo.prec && ss.total == lo.total && ss.data == b->data &&
@@ -1057,6 +1108,14 @@ int gm2_workspace_set_option(void* ws, int key, int value) {
 
 int gm2_workspace_get_option(void* ws, int key, int* value) {
   return guarded([&] { *value = option_get(ws_state(ws).opt, key); });
+}
+
+int gm2_workspace_set_collective(void* ws, gm2_allreduce_fn fn, void* user) {
+  return guarded([&] {
+    WsState& st = ws_state(ws);
+    st.coll = fn;
+    st.coll_user = user;
+  });
 }
 
 int gm2_workspace_release(void* ws) {

@@ -80,7 +80,7 @@ struct Options {
   int small_stages = 4;  // GM2_OPT_SMALL_STAGES LDS ring depth of those tiles (4 or 5)
   int grid_cap = 2;      // GM2_OPT_GRID_CAP     capped grids: 1 dW9, 2 dWe0, 4 recon
   int input_chunks = 1;  // GM2_OPT_INPUT_CHUNKS launches of the input-layer weight gradient (1 or 4)
-  int defer_output_adam = 0;  // GM2_OPT_DEFER_OUTPUT_ADAM (see gm2.h)
+  int sync_bn = 0;       // GM2_OPT_SYNC_BN      train-mode BatchNorm over every rank's rows (collective)
 };
 // validated edit of one option (throws on an unknown key or a bad value)
 void option_set(Options& o, int key, int value);
@@ -196,14 +196,19 @@ void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float
 template <typename T>
 void launch_transpose(const T* src, int64_t lds_, int R, int Cn, T* dst, int64_t ldd, hipStream_t s);
 // BatchNorm finalize (chunk merge per column) + elementwise apply in one launch per layer
+// (sync != nullptr: SyncBN, the global batch's all-reduced sums from launch_bn_sync_pack)
 template <typename T>
 void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
                          const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,
-                         hipStream_t s);
+                         hipStream_t s, const double* sync = nullptr);
 template <typename T>
 void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const float* part, int B, int Bp, int H,
                          int train, const float* save, const float* gamma, const float* beta, float* dgamma,
-                         float* dbeta, T* dY, float* colpart, hipStream_t s);
+                         float* dbeta, T* dY, float* colpart, hipStream_t s, const double* sync = nullptr);
+// SyncBN: this rank's [sum | sum of squares (mode 0) or sum (y-mean)do (mode 1) | rows, 0] (2H + 2 doubles)
+void launch_bn_sync_pack(const float* part, int B, int H, int mode, double* out, hipStream_t s);
+// SyncBN, a rank with no rows: the running-statistics update from the all-reduced sums
+void launch_bn_sync_running(const double* sync, int H, float* rmean, float* rvar, hipStream_t s);
 // reparameterization + KL (model.py:100-104, loss_components.py:77)
 template <typename T>
 void launch_reparam(const float* slabs, int S, int64_t slab, int L, const float* bmu, const float* blv,

@@ -769,19 +769,29 @@ __global__ __launch_bounds__(256) void k_slab_sum(const float* __restrict__ slab
 // Then a vectorised elementwise pass over 64 rows x 256 columns (4 columns per thread).
 // ---------------------------------------------------------------------------------------------
 // forward coefficients (alpha = invstd*gamma, beta' = fma(-mean, alpha, beta)) of column `col`
+// (SyncBN: `sync` holds the all-reduced [sum y | sum y^2 | rows] of every rank's batch, fp64; the
+// statistics are then the global batch's, N = sync[2H] rows)
+__device__ __forceinline__ void bn_sync_stats(const double* __restrict__ sync, int H, int col, double& mean,
+                                              double& var, double& n) {
+  n = sync[2 * H];
+  mean = sync[col] / n;
+  var = fmax(sync[H + col] / n - mean * mean, 0.0);
+}
+
 __device__ __forceinline__ float2 bn_fwd_coef(const float2* __restrict__ part, int B, int H, int train,
                                      const float* __restrict__ gamma, const float* __restrict__ beta, float* rmean,
-                                     float* rvar, float* save, int col, bool own) {
+                                     float* rvar, float* save, int col, bool own, const double* __restrict__ sync) {
   float invstd, meanf;
   if (train) {
-    double mean, var;
-    bn_merge(part, B, H, col, mean, var);
+    double mean, var, n = (double)B;
+    if (sync) bn_sync_stats(sync, H, col, mean, var, n);
+    else bn_merge(part, B, H, col, mean, var);
     invstd = (float)(1.0 / sqrt(var + kBnEps));
     meanf = (float)mean;
     if (own) {
       save[col] = meanf;
       save[H + col] = invstd;
-      const double unb = B > 1 ? var * (double)B / (double)(B - 1) : var;
+      const double unb = n > 1.0 ? var * n / (n - 1.0) : var;
       rmean[col] = (float)(kBnMomentum * mean + (1.0 - kBnMomentum) * (double)rmean[col]);
       rvar[col] = (float)(kBnMomentum * unb + (1.0 - kBnMomentum) * (double)rvar[col]);
     }
@@ -804,7 +814,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_bn_fwd_apply(const float* __restrict__ Y, int64_t ld,
                                                     const float2* __restrict__ part, int B, int H, int train,
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                    float* rmean, float* rvar, float* save, T* __restrict__ A) {
+                                                    float* rmean, float* rvar, float* save, T* __restrict__ A,
+                                                    const double* __restrict__ sync) {
   __shared__ float2 cf[256];
   const int c0 = blockIdx.x * 256;
   const int cl = (threadIdx.x & 63) * 4, rg = threadIdx.x >> 6;
@@ -812,7 +823,7 @@ __global__ __launch_bounds__(256) void k_bn_fwd_apply(const float* __restrict__ 
   const int r0 = blockIdx.y * 64;
   if (c0 + (int)threadIdx.x < H)
     cf[threadIdx.x] = bn_fwd_coef(part, B, H, train, gamma, beta, rmean, rvar, save, c0 + threadIdx.x,
-                                  blockIdx.y == 0);
+                                  blockIdx.y == 0, sync);
   __syncthreads();
   if (c >= H) return;  // H % 128 == 0: the last block may cover only 128 of its 256 columns
   const float2 k0 = cf[cl], k1 = cf[cl + 1], k2 = cf[cl + 2], k3 = cf[cl + 3];
@@ -845,7 +856,8 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
                                                     int train, const float* __restrict__ save,
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                    T* __restrict__ dY, float* __restrict__ colpart) {
+                                                    T* __restrict__ dY, float* __restrict__ colpart,
+                                                    const double* __restrict__ sync) {
   __shared__ float4 cf4[5][64];  // [mean, alpha, beta', grad_mean, proj_scale][column / 4]
   __shared__ float4 red[4][64];
   float* cf = (float*)cf4;
@@ -883,8 +895,11 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
       cf[t] = mean;
       cf[256 + t] = alpha;
       cf[512 + t] = fmaf(-mean, alpha, beta[col]);
-      cf[768 + t] = train ? (float)(s1 / B) : 0.f;
-      cf[1024 + t] = train ? (float)(s2 * (double)invstd * invstd / B) : 0.f;
+      // (SyncBN: the coupling terms use the global batch's sums; dgamma / dbeta above stay this
+      // rank's share, which the gradient all-reduce sums)
+      const double g1 = sync ? sync[col] : s1, g2 = sync ? sync[H + col] : s2, nb = sync ? sync[2 * H] : (double)B;
+      cf[768 + t] = train ? (float)(g1 / nb) : 0.f;
+      cf[1024 + t] = train ? (float)(g2 * (double)invstd * invstd / nb) : 0.f;
     }
   }
   __syncthreads();
@@ -926,6 +941,48 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
     for (int k = 1; k < 4; ++k) { v.x += red[k][cg].x; v.y += red[k][cg].y; v.z += red[k][cg].z; v.w += red[k][cg].w; }
     *(float4*)(colpart + (int64_t)blockIdx.y * H + c) = v;
   }
+}
+
+// SyncBN: this rank's per-column sums of the batch, from the chunk partials, for the all-reduce:
+//   forward  (mode 0): out = [sum y | sum y^2 | rows, 0]  (from the chunk (mean, M2) pairs)
+//   backward (mode 1): out = [sum do | sum (y - mean) do | rows, 0]
+// fp64 throughout (sum y^2 - N mean^2 keeps ~1e-16 * (mean / std)^2 relative error in the variance)
+__global__ __launch_bounds__(256) void k_bn_sync_pack(const float2* __restrict__ part, int B, int H, int mode,
+                                                    double* __restrict__ out) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col == 0) {
+    out[2 * H] = (double)B;
+    out[2 * H + 1] = 0.0;
+  }
+  if (col >= H) return;
+  const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
+  double a = 0.0, b = 0.0;
+  for (int ch = 0; ch < nch; ++ch) {
+    const float2 p = part[(int64_t)ch * H + col];
+    if (mode == 0) {
+      const double nb = (double)min(kBnRowChunk, B - ch * kBnRowChunk), m = (double)p.x;
+      a += nb * m;
+      b += (double)p.y + nb * m * m;
+    } else {
+      a += (double)p.x;
+      b += (double)p.y;
+    }
+  }
+  out[col] = a;
+  out[H + col] = b;
+}
+
+// SyncBN on a rank with no rows this step: the running statistics still follow the global batch
+// (the same update every rank applies in k_bn_fwd_apply)
+__global__ __launch_bounds__(256) void k_bn_sync_running(const double* __restrict__ sync, int H, float* rmean,
+                                                       float* rvar) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= H) return;
+  double mean, var, n;
+  bn_sync_stats(sync, H, col, mean, var, n);
+  const double unb = n > 1.0 ? var * n / (n - 1.0) : var;
+  rmean[col] = (float)(kBnMomentum * mean + (1.0 - kBnMomentum) * (double)rmean[col]);
+  rvar[col] = (float)(kBnMomentum * unb + (1.0 - kBnMomentum) * (double)rvar[col]);
 }
 
 // dst[c][r] = src[r][c] over an R x Cn block (both multiples of 64): 64 x 64 tiles through LDS,
@@ -1061,19 +1118,29 @@ void launch_colsum(const float* part, int rows, int64_t ld, int64_t n, float* ou
 template <typename T>
 void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
                          const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,
-                         hipStream_t s) {
-  if (H % 128 || ld % 4 || Bp % 64) throw Gm2Error("bn_fwd_apply: H %% 128, ld %% 4, Bp %% 64");
+                         hipStream_t s, const double* sync) {
+  if (H % 128 || ld % 4 || Bp % 64 || B <= 0) throw Gm2Error("bn_fwd_apply: H %% 128, ld %% 4, Bp %% 64, B > 0");
   hipLaunchKernelGGL(k_bn_fwd_apply<T>, dim3((H + 255) / 256, Bp / 64), dim3(256), 0, s, Y, ld, (const float2*)part,
-                     B, H, train, gamma, beta, rmean, rvar, save, A);
+                     B, H, train, gamma, beta, rmean, rvar, save, A, sync);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_bn_sync_pack(const float* part, int B, int H, int mode, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_sync_pack, dim3((H + 255) / 256), dim3(256), 0, s, (const float2*)part, B, H, mode, out);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_bn_sync_running(const double* sync, int H, float* rmean, float* rvar, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_sync_running, dim3((H + 255) / 256), dim3(256), 0, s, sync, H, rmean, rvar);
   GM2_CHECK_LAUNCH();
 }
 template <typename T>
 void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const float* part, int B, int Bp, int H,
                          int train, const float* save, const float* gamma, const float* beta, float* dgamma,
-                         float* dbeta, T* dY, float* colpart, hipStream_t s) {
-  if (H % 128 || ld % 4 || Bp % 64) throw Gm2Error("bn_bwd_apply: H %% 128, ld %% 4, Bp %% 64");
+                         float* dbeta, T* dY, float* colpart, hipStream_t s, const double* sync) {
+  if (H % 128 || ld % 4 || Bp % 64 || B <= 0) throw Gm2Error("bn_bwd_apply: H %% 128, ld %% 4, Bp %% 64, B > 0");
   hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3((H + 255) / 256, Bp / 64), dim3(256), 0, s, da, Y, ld,
-                     (const float2*)part, B, H, train, save, gamma, beta, dgamma, dbeta, dY, colpart);
+                     (const float2*)part, B, H, train, save, gamma, beta, dgamma, dbeta, dY, colpart, sync);
   GM2_CHECK_LAUNCH();
 }
 
@@ -1151,10 +1218,10 @@ void launch_grad_finalize(const double* part, int nblocks, const float* scal, fl
                                       float*, hipStream_t);                                                     \
   template void launch_shadow_sync<T>(const TensorTable&, const float*, hipStream_t);                          \
   template void launch_bn_fwd_apply<T>(const float*, int64_t, const float*, int, int, int, int, const float*,   \
-                                       const float*, float*, float*, float*, T*, hipStream_t);                   \
+                                       const float*, float*, float*, float*, T*, hipStream_t, const double*);    \
   template void launch_bn_bwd_apply<T>(const float*, const float*, int64_t, const float*, int, int, int, int,    \
                                        const float*, const float*, const float*, float*, float*, T*, float*,    \
-                                       hipStream_t);                                                            \
+                                       hipStream_t, const double*);                                             \
   template void launch_transpose<T>(const T*, int64_t, int, int, T*, int64_t, hipStream_t);                    \
   template void launch_adam_fused<T>(const TensorTable&, const float*, float*, float*, float*, const float*,    \
                                      const float*, hipStream_t);

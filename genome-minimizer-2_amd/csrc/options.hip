@@ -58,6 +58,7 @@ void option_set(Options& o, int key, int value) {
       if (value != 1 && value != 4) throw Gm2Error("input chunks %d: 1 or 4", value);
       o.input_chunks = value;
       break;
+    case GM2_OPT_SYNC_BN: o.sync_bn = value ? 1 : 0; break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -73,6 +74,7 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_SMALL_STAGES: return o.small_stages;
     case GM2_OPT_GRID_CAP: return o.grid_cap;
     case GM2_OPT_INPUT_CHUNKS: return o.input_chunks;
+    case GM2_OPT_SYNC_BN: return o.sync_bn;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

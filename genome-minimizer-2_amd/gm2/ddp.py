@@ -17,7 +17,11 @@ Semantics:
   * BatchNorm running statistics are averaged over ranks at the end of every training epoch, so
     validation, sampling and the saved checkpoint see one set of statistics on every rank. The
     running-stat update is linear in the batch statistics, so one average per epoch equals the
-    average of per-step averages (up to fp32 rounding).
+    average of per-step averages (up to fp32 rounding);
+  * optional SyncBN (enable_sync_bn, VAETrainer(sync_bn=True), main.py --sync-bn): train-mode
+    BatchNorm over the GLOBAL batch through 12 fp64 all-reduces per step inside libgm2, so the step
+    is the single-device reference's step on the whole batch; running statistics are then identical
+    on every rank and are not averaged.
 """
 from __future__ import annotations
 
@@ -108,6 +112,16 @@ class GradSync:
         cur.wait_stream(self.stream)
 
 
+def enable_sync_bn(dist, ws):
+    """SyncBN on a training workspace (gm2.h GM2_OPT_SYNC_BN): train-mode BatchNorm normalises with
+    the statistics of the global batch, every rank's rows, as the single-device reference does
+    (model.py:67-86), at the price of 12 small fp64 all-reduces (2H + 2 doubles each) per step,
+    issued by libgm2 through this torch.distributed collective on the call's stream."""
+    if ws.get_option(native.OPT_SYNC_BN) != 1:
+        ws.set_option(native.OPT_SYNC_BN, 1)
+        ws.set_collective(lambda t: dist.all_reduce(t))
+
+
 def reduce_loss_rows(dist, rec):
     """SUM over ranks of the per-rank loss sums [BCE, sum p, KL] of every batch row of the epoch's
     loss record (rec [nb][GM2_LOSS_SLOTS] fp64; slots 3-4 are post-reduction values already
@@ -129,6 +143,20 @@ def broadcast_model(dist, model, src=0):
     dist.broadcast(model.params, src)
     dist.broadcast(model.bn, src)
     model.touch()
+
+
+def gather_rows(dist, local, n_total):
+    """Concatenate every rank's contiguous row slice (rank_slice(n_total, r, world)) of a device
+    tensor on every rank: one padded all-gather (slices differ by at most one row). Used by the
+    sharded `--mode sample` to hand rank 0 the full mask set for the reference's output files."""
+    world = dist.get_world_size()
+    spans = [rank_slice(n_total, r, world) for r in range(world)]
+    cap = max(hi - lo for lo, hi in spans)
+    buf = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    buf[: local.shape[0]] = local
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    return torch.cat([parts[r][: hi - lo] for r, (lo, hi) in enumerate(spans)])
 
 
 def shared_seed(dist, src=0):

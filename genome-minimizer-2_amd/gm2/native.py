@@ -31,11 +31,14 @@ EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_of
            "gm2_mask_row_offsets", "gm2_mask_compact", "gm2_recon_counts",
            "gm2_gemm", "gm2_grad_bucket_bounds", "gm2_wait_grad_bucket", "gm2_set_option", "gm2_get_option",
            "gm2_workspace_set_option", "gm2_workspace_get_option", "gm2_workspace_release",
+           "gm2_workspace_set_collective",
            "gm2_timing_begin", "gm2_timing_end"]
 ABI_VERSION = 3
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
 OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE, OPT_SMALL_SPLIT, OPT_BN_EPILOGUE, OPT_SMALL_WAVES = 1, 2, 3, 4, 5, 6
-OPT_INPUT_CHUNKS, OPT_SMALL_STAGES, OPT_GRID_CAP = 7, 8, 9
+OPT_INPUT_CHUNKS, OPT_SMALL_STAGES, OPT_GRID_CAP, OPT_SYNC_BN = 7, 8, 9, 10
+# gm2_allreduce_fn (gm2.h): int (double* buf, int64_t count, void* stream, void* user)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
 
 
 class Dims(C.Structure):
@@ -94,6 +97,7 @@ def lib():
         "gm2_workspace_set_option": (C.c_int, [vp, i32, i32]),
         "gm2_workspace_get_option": (C.c_int, [vp, i32, C.POINTER(C.c_int)]),
         "gm2_workspace_release": (C.c_int, [vp]),
+        "gm2_workspace_set_collective": (C.c_int, [vp, ALLREDUCE_FN, vp]),
         "gm2_timing_begin": (C.c_int, [i32]),
         "gm2_timing_end": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     }
@@ -166,6 +170,30 @@ class Workspace:
         v = C.c_int()
         check(lib().gm2_workspace_get_option(self.ptr, int(key), C.byref(v)), "gm2_workspace_get_option")
         return v.value
+
+    def set_collective(self, fn):
+        """The SUM all-reduce SyncBN calls (gm2_workspace_set_collective): fn(tensor) reduces a
+        float64 device tensor (a view of this workspace) in place on torch's current stream, which
+        is the stream of the libgm2 call in progress. None removes it."""
+        if fn is None:
+            self._coll = None
+            check(lib().gm2_workspace_set_collective(self.ptr, ALLREDUCE_FN(), None), "gm2_workspace_set_collective")
+            return
+        base = self.buf.data_ptr()
+
+        def cb(buf, count, strm, user):
+            try:
+                off = int(buf) - base
+                t = self.buf[off: off + 8 * int(count)].view(torch.float64)
+                with torch.cuda.stream(torch.cuda.ExternalStream(int(strm), device=self.buf.device)):
+                    fn(t)
+                return 0
+            except Exception as e:  # an exception must not cross the C frames
+                import sys
+                print(f"libgm2 collective failed: {e!r}", file=sys.stderr)
+                return 1
+        self._coll = ALLREDUCE_FN(cb)  # kept alive as long as the workspace
+        check(lib().gm2_workspace_set_collective(self.ptr, self._coll, None), "gm2_workspace_set_collective")
 
     def __del__(self):
         lb = getattr(self, "_lib", None)

@@ -27,7 +27,8 @@ import torch
 
 from . import native
 from .data import StrainLoader, as_strain_loader
-from .ddp import GradSync, average_running_stats, get_dist, rank_share, rank_slice, rank_world, reduce_loss_rows
+from .ddp import (GradSync, average_running_stats, enable_sync_bn, get_dist, rank_share, rank_slice, rank_world,
+                  reduce_loss_rows)
 from .loss_components import (GeneAbundanceLoss, KLDivergenceLoss, L1RegularizationLoss, LossComponent,
                               ReconstructionLoss, fused_supported)
 
@@ -164,9 +165,10 @@ class VAETrainer:
     """trainer.py:84-189 on libgm2. `eps_rng`: 'device' draws the reparameterization noise with
     torch's generator on the model's device (what the reference does on a GPU: randn_like on a
     cuda tensor); 'cpu' draws it from the global CPU generator (what the reference does on CPU;
-    used by the parity tests against the CPU oracle)."""
+    used by the parity tests against the CPU oracle). `sync_bn` (data parallel only; default from
+    env GM2_SYNC_BN): train-mode BatchNorm over the global batch (gm2.ddp.enable_sync_bn)."""
 
-    def __init__(self, model, optimizer, scheduler, config: TrainingConfig, eps_rng="device"):
+    def __init__(self, model, optimizer, scheduler, config: TrainingConfig, eps_rng="device", sync_bn=None):
         self.model = model
         self.optimizer = optimizer
         self.scheduler = scheduler
@@ -179,6 +181,7 @@ class VAETrainer:
         self.grads = torch.zeros_like(model.params)
         self.last_grad_norm = None
         self._sync = None
+        self.sync_bn = bool(int(os.environ.get("GM2_SYNC_BN", "0"))) if sync_bn is None else bool(sync_bn)
 
     def setup_loss_components(self, loss_components: List[LossComponent]):
         self.loss_tracker = LossTracker(loss_components)
@@ -316,13 +319,18 @@ class VAETrainer:
         ws = model.workspace(model.precision, (loader.batch_size + world - 1) // world)
         rec = torch.zeros(max(nb, 1), native.LOSS_SLOTS, dtype=torch.float64, device=self.device)
         sync = self._grad_sync(dist) if dist else None
+        sync_bn = dist is not None and self.sync_bn
         if sync:
             sync.prepare(ws)
+        if sync_bn:
+            enable_sync_bn(dist, ws)
         for bi, rows in enumerate(batches):
             n = rows.shape[0]
-            lo, hi = rank_share(n, rank, world)
+            # SyncBN: plain contiguous slices (a rank may get 0 or 1 rows: the statistics are the
+            # global batch's, and a rank with none still joins the 12 all-reduces inside libgm2)
+            lo, hi = rank_slice(n, rank, world) if sync_bn else rank_share(n, rank, world)
             eps = self._eps(n)[lo:hi].contiguous()
-            ran = hi > lo
+            ran = hi > lo or sync_bn
             if ran:
                 batch = native.make_batch(mat.data, mat.ld, rows[lo:hi], hi - lo, eps)
                 native.train_fwd_bwd(ws, batch, model.params, self.grads, model.bn, scal[bi], rec[bi])
@@ -341,7 +349,8 @@ class VAETrainer:
             self._bump_bn()
         if dist:
             reduce_loss_rows(dist, rec)
-            average_running_stats(dist, model.bn)
+            if not sync_bn:  # (SyncBN: every rank applied the same global-batch updates)
+                average_running_stats(dist, model.bn)
         raw = rec.cpu().numpy()  # the epoch's one device->host sync
         if nb:
             self.last_grad_norm = float(raw[nb - 1, 4])

@@ -256,7 +256,18 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       so the work beside it keeps CUs (default 2); 0 = one workgroup per tile.
  *   GM2_OPT_INPUT_CHUNKS 1 (default) or 4: launches of the input-layer weight-gradient GEMM, one
  *                       per gradient bucket 2..5 (when H/4 is a multiple of 256; else 1). Same
- *                       results bit for bit; 4 lets a data-parallel exchange start early. */
+ *                       results bit for bit; 4 lets a data-parallel exchange start early.
+ *   GM2_OPT_SYNC_BN     (workspace option; changes the model's semantics on purpose) 1 = SyncBN for
+ *                       data-parallel training: train-mode BatchNorm normalises with the statistics
+ *                       of the GLOBAL batch (every rank's rows), as the single-device reference does
+ *                       (model.py:67-86), instead of each rank's own rows. Needs a collective
+ *                       (gm2_workspace_set_collective): per training call the library all-reduces
+ *                       (SUM, fp64) 6 forward [sum y | sum y^2 | rows] and 6 backward
+ *                       [sum do | sum (y-mean) do | rows] vectors of 2H+2 doubles, in a fixed order
+ *                       (forward layers encoder.1 .. decoder.7, then backward decoder.7 .. encoder.1).
+ *                       A rank with no rows in a global batch calls gm2_train_fwd_bwd with n = 0: it
+ *                       takes part in the 12 all-reduces with zeros, writes zero gradients and loss
+ *                       slots, and applies the same running-statistics update. Default 0. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -266,12 +277,22 @@ enum {
   GM2_OPT_SMALL_WAVES = 6,
   GM2_OPT_INPUT_CHUNKS = 7,
   GM2_OPT_SMALL_STAGES = 8,
-  GM2_OPT_GRID_CAP = 9
+  GM2_OPT_GRID_CAP = 9,
+  GM2_OPT_SYNC_BN = 10
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);
 int gm2_workspace_set_option(void* ws, int key, int value);
 int gm2_workspace_get_option(void* ws, int key, int* value);
+
+/* The all-reduce SyncBN needs (GM2_OPT_SYNC_BN), supplied by the caller: SUM `count` doubles at the
+ * DEVICE pointer `buf` (inside the workspace) across every rank, in place, ordered on `stream` (the
+ * stream of the libgm2 call in progress: work enqueued on it before the call must be done before
+ * the reduction reads `buf`, and work enqueued after the callback returns must see the result).
+ * Returns 0 on success. Called from inside gm2_train_fwd_bwd on the calling thread. The Python host
+ * binds torch.distributed.all_reduce (RCCL) here (gm2/ddp.py). */
+typedef int (*gm2_allreduce_fn)(double* buf, int64_t count, void* stream, void* user);
+int gm2_workspace_set_collective(void* ws, gm2_allreduce_fn fn, void* user);
 
 enum { GM2_KC_RECON_LOSS = 1, GM2_KC_GEMM_STORE = 2, GM2_KC_MASK = 4 };
 int gm2_timing_begin(int kernel_classes);

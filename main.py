@@ -20,7 +20,10 @@ Return codes follow main.py:647-692: 0 success, 1 failure.
 Multi-GPU (no reference equivalent; the reference is single-device, main.py:37):
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 main.py --mode training ...
 runs strain-row data parallelism over RCCL (gm2/ddp.py): every rank trains its share of each batch,
-rank 0 prints and saves the checkpoint. Other modes run on rank 0 only.
+rank 0 prints and saves the checkpoint (--sync-bn: BatchNorm over the global batch, gm2/ddp.py).
+--mode sample shards the genomes: one broadcast seed, the same z on every rank, each rank decodes its
+contiguous slice on its GPU, rank 0 gathers the packed masks and writes the files. Other modes run
+on rank 0 only.
 
 Additions (no reference equivalent): --precision bf16|f32 for the training GEMMs (sampling always
 decodes in exact fp32), --mask-dtype float64|uint8|bits for the saved masks (the reference writes
@@ -58,6 +61,8 @@ def parse_arguments(argv=None):
     p.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
     p.add_argument("--grad-exchange", choices=["f32", "bf16"], default=None,
                    help="torchrun / DDP only: dtype of the big weight-gradient all-reduce (default f32)")
+    p.add_argument("--sync-bn", action="store_true",
+                   help="torchrun / DDP only: train-mode BatchNorm over the global batch (SyncBN)")
     p.add_argument("--mask-dtype", choices=["float64", "uint8", "bits"], default="float64")
     p.add_argument("--no-csv", action="store_true")
     p.add_argument("--genome-path", type=str, default=None,
@@ -178,12 +183,26 @@ def run_sampling(args):
     model = load_model(input_dim, config.hidden_dim, config.latent_dim, args.model_path)
     print(f"- Architecture: {input_dim} -> {config.hidden_dim} -> {config.latent_dim}")
     print(f"- Samples: {args.num_samples}\n- Mode: {args.sampling_mode}\n- Output: {out_dir}")
+    from gm2.ddp import gather_rows, get_dist, rank_slice, rank_world, shared_seed
+    dist = get_dist()
+    rank, world = rank_world(dist)
+    if dist is not None:
+        # every rank draws the same z from one broadcast seed (the reference's z is one unseeded
+        # draw of the global generator, extras.py:197) and decodes its contiguous slice
+        torch.cuda.manual_seed(shared_seed(dist))
     if args.sampling_mode == "default":
         with torch.no_grad():
             z = torch.randn(args.num_samples, config.latent_dim, device=device)  # extras.py:197
     else:
         z = focused_z(model, config.latent_dim, args.num_samples, args.noise_level, device)
-    packed, _ = model.decode_bits(z)          # masks stay on the GPU, 8 genes per byte
+    lo, hi = rank_slice(args.num_samples, rank, world)
+    packed, _ = model.decode_bits(z[lo:hi])   # masks stay on the GPU, 8 genes per byte
+    if dist is not None:
+        # the ranks' packed slices -> the full set (rank 0 writes the reference's files)
+        from gm2.masks import PackedMasks
+        packed = PackedMasks(gather_rows(dist, packed.bits, args.num_samples), packed.G)
+        if rank != 0:
+            return True
     sizes = packed.row_sizes()                # binary.sum(axis=1)
     ess = count_essential_genes(packed, essential_gene_positions)  # on the device
     print(f"\n✓ Sampling Results:\n- Generated samples: {packed.n}")
@@ -276,11 +295,13 @@ def main(argv=None):
     args = parse_arguments(argv)
     if args.grad_exchange:
         os.environ["GM2_GRAD_EXCHANGE"] = args.grad_exchange  # read by the trainer's gradient exchange
+    if args.sync_bn:
+        os.environ["GM2_SYNC_BN"] = "1"  # read by VAETrainer
     dist = None
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         # torchrun: one process per GPU; bind the device and join the process group before any
         # other GPU work (strain-row data parallelism)
-        if args.mode != "training":
+        if args.mode not in ("training", "sample"):
             if int(os.environ.get("RANK", "0")) != 0:
                 return 0
             print(f"--mode {args.mode} does not shard; running it on rank 0 only")

@@ -287,3 +287,129 @@ def test_two_rank_ragged_batch_trains_every_row(tmp_path):
     bce, _, kl = _shard_sums(P, {k: v.clone() for k, v in S.items()}, x, eps, True)
     assert abs(r0["rec"][0] - bce / 3) <= 1e-5 * abs(bce / 3)
     assert abs(r0["rec"][1] - np.float32(beta) * (-0.5 * kl) / 3) <= 1e-5 * abs(kl) + 1e-7
+
+
+def _syncbn_worker(rank, world, port, out_dir, n_rows):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gm2 import native
+    from gm2.data import ResidentMatrix, StrainLoader
+    from gm2.loss_components import GeneAbundanceLoss, KLDivergenceLoss, ReconstructionLoss
+    from gm2.model import VAE
+    from gm2.trainer import Adam, StepLR, TrainingConfig, VAETrainer
+
+    P, S = _state()
+    m = VAE(G, H, L, precision=native.GM2_F32, init=False)
+    m.load_state_dict({**P, **S})
+    opt = Adam(m, lr=1e-3)
+    tr = VAETrainer(m, opt, StepLR(opt, 20, 0.5), TrainingConfig(n_epochs=N_EPOCHS, max_norm=1.0), eps_rng="cpu",
+                    sync_bn=True)
+    tr.setup_loss_components([ReconstructionLoss(), KLDivergenceLoss(**BETA_KW), GeneAbundanceLoss(**GAMMA_KW)])
+    x = synth_x(n_rows, G, 8)
+    torch.manual_seed(SEED + 3)
+    losses = tr.train_epoch(StrainLoader(ResidentMatrix(x), None, BS, shuffle=False), 0)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, f"s{rank}.npz"), grads=tr.grads.cpu().numpy(), params=m.params.cpu().numpy(),
+             bn=m.bn.cpu().numpy(), rec=np.array([losses["reconstruction"], losses["kl_divergence"],
+                                                 losses["gene_abundance"]]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_rows", [(2, 64), (2, 3), (3, 2)])
+def test_sync_bn_step_equals_full_batch_reference(tmp_path, world, n_rows):
+    """SyncBN (gm2.ddp.enable_sync_bn, GM2_OPT_SYNC_BN): one global batch of n_rows split over
+    `world` ranks (64 rows on 2; 3 rows = 1 + 2; 2 rows on 3 ranks, one rank with NO rows that only
+    joins the all-reduces) gives the single-device reference's step on the WHOLE batch: the reduced
+    gradient against the fp64 full-batch oracle with the C2 method's bar (norm-wise error <= 3x
+    the reference's own fp32 arithmetic + 2e-4), the BatchNorm running statistics equal to the
+    full-batch update on every rank (no averaging), the epoch losses equal to the full-batch sums,
+    all ranks identical."""
+    port = _free_port()
+    mp.spawn(_syncbn_worker, args=(world, port, str(tmp_path), n_rows), nprocs=world, join=True)
+    rs = [np.load(tmp_path / f"s{r}.npz") for r in range(world)]
+    for r in rs[1:]:
+        np.testing.assert_array_equal(rs[0]["params"], r["params"])
+        np.testing.assert_array_equal(rs[0]["grads"], r["grads"])
+        np.testing.assert_array_equal(rs[0]["bn"], r["bn"])
+    P, S = _state()
+    x = torch.tensor(synth_x(n_rows, G, 8), dtype=torch.float32)
+    torch.manual_seed(SEED + 3)
+    torch.empty((), dtype=torch.int64).random_()  # the loader's base seed
+    eps = torch.randn(n_rows, L)
+    ls = O.LossState(O.Preset("t", "cosine", 0.1, 1.0, T=10, gamma_start=1.0, gamma_end=0.1), N_EPOCHS)
+    beta, gamma = ls.beta(0), ls.gamma(0)
+    P64 = {k: v.double() for k, v in P.items()}
+    S64 = {k: v.double() for k, v in S.items()}
+    g64 = O.manual_grads(P64, S64, x.double(), eps.double(), beta, gamma, 0.0)
+    g32 = O.manual_grads(P, S, x, eps, beta, gamma, 0.0)
+    off = np.cumsum([0] + [int(np.prod(s)) for _, s in O.param_specs(G, H, L)])
+    fails = []
+    for i, (name, _) in enumerate(O.param_specs(G, H, L)):
+        parts = name.split(".")
+        if parts[0] in ("encoder", "decoder") and parts[1] in ("0", "3", "6") and parts[2] == "bias":
+            continue
+        ex = g64[name].reshape(-1).numpy()
+        nrm = max(float(np.linalg.norm(ex)), 1e-30)
+        f_gpu = float(np.linalg.norm(rs[0]["grads"][off[i]:off[i + 1]] - ex)) / nrm
+        f_ref = float(np.linalg.norm(g32[name].reshape(-1).double().numpy() - ex)) / nrm
+        if not f_gpu <= 3 * f_ref + 2e-4:
+            fails.append(f"{name}: fro {f_gpu:.3g} vs reference arithmetic {f_ref:.3g}")
+    assert not fails, "\n".join(fails)
+    S2 = {k: v.clone() for k, v in S64.items()}
+    O.forward(P64, S2, x.double(), eps.double(), train=True)
+    for i, b in enumerate(O.BNS):
+        np.testing.assert_allclose(rs[0]["bn"][i, 0], S2[b + ".running_mean"].numpy(), rtol=2e-5, atol=2e-6)
+        np.testing.assert_allclose(rs[0]["bn"][i, 1], S2[b + ".running_var"].numpy(), rtol=2e-5, atol=2e-6)
+    bce, ps, kl = _shard_sums(P64, {k: v.clone() for k, v in S64.items()}, x.double(), eps.double(), True)
+    np.testing.assert_allclose(rs[0]["rec"][0], bce / n_rows, rtol=1e-5)
+    np.testing.assert_allclose(rs[0]["rec"][1], np.float32(beta) * (-0.5 * kl) / n_rows, rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(rs[0]["rec"][2], np.float32(gamma) * ps / n_rows, rtol=1e-5)
+
+
+def _sample_worker(rank, world, port, root, ckpt, pkl, n):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK="0", GM2_DIST_BACKEND="gloo")
+    torch.set_num_threads(1)
+    import main as cli
+    torch.manual_seed(4321)  # rank 0's draw of the shared seed
+    rc = cli.main(["--mode", "sample", "--model-path", ckpt, "--genes-path", pkl, "--num-samples", str(n),
+                   "--project-root", root, "--no-csv"])
+    assert rc == 0
+
+
+def test_two_rank_sharded_sampling_cli(tmp_path):
+    """`--mode sample` under torchrun (2 ranks, gloo, one GPU): one broadcast seed, the same z on
+    both ranks, each rank decodes its contiguous half, rank 0 gathers the packed masks and writes
+    the reference's .npy. The file holds exactly the masks of decoding that z on one device:
+    bit-exact to the fp32 oracle outside the fp64 rounding band of each logit."""
+    import pickle
+    from gm2.data import write_synthetic_csvs
+    root = str(tmp_path)
+    Gs, Hs, Ls, n = 300, 1024, 64, 1001
+    write_synthetic_csvs(root, 50, Gs, seed=6)
+    torch.manual_seed(11)
+    Pq = O.init_params(Gs, Hs, Ls)
+    Sq = O.init_bn_state(Hs)
+    Pq, Sq = perturb_bn(Pq, Sq, 12)
+    Pq["decoder.9.bias"] = torch.linspace(-1.5, 1.0, Gs)
+    sd = {**Pq, **Sq}
+    for b in O.BNS:
+        sd[b + ".num_batches_tracked"] = torch.tensor(0, dtype=torch.long)
+    ckpt = os.path.join(root, "saved_VAE_v0.pt")
+    torch.save(sd, ckpt)
+    pkl = os.path.join(root, "ess.pkl")
+    with open(pkl, "wb") as f:
+        pickle.dump({"a": [0, 3], "b": [299]}, f)
+    port = _free_port()
+    mp.spawn(_sample_worker, args=(2, port, root, ckpt, pkl, n), nprocs=2, join=True)
+    masks = np.load(os.path.join(root, "models", "v0_model", "sampling_results", "v0_binary_samples_default.npy"))
+    assert masks.shape == (n, Gs)
+    torch.manual_seed(4321)
+    seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    torch.cuda.manual_seed(seed)
+    z = torch.randn(n, Ls, device="cuda").cpu()
+    ref = O.sample_decode(Pq, Sq, z).numpy() > 0.5
+    band = np.abs(O.decode_logits64(Pq, Sq, z).numpy()) <= 1e-3
+    assert ((masks.astype(bool) != ref) & ~band).sum() == 0
