@@ -942,7 +942,8 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
     float a = 0.f, b = 0.f;
     for (int w = 0; w < C::NT / 64; ++w) { a += red[w]; b += red[32 + w]; }
     // padded genes of an edge tile: logit exactly 0 -> p = 1/2, x = 0, BCE = -log(1/2) each
-    const int pad_g = max(0, tl.m0 + C::BM - g.M), val_s = min(C::BN, g.N - tl.n0);
+    // (a tile may lie wholly in the padding when Gp - G >= BM: the bf16 workspaces pad G to 256)
+    const int pad_g = min(C::BM, max(0, tl.m0 + C::BM - g.M)), val_s = min(C::BN, g.N - tl.n0);
     if (pad_g > 0) {
       float e0, p0;
       recon_pad_const<FAST>(e0, p0);

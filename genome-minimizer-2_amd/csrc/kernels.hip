@@ -123,14 +123,23 @@ __global__ __launch_bounds__(256) void k_bn_fwd_partial(const float* __restrict_
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] = f4add(v[i], w[u][i]);
   }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = f4add(v[i], b);
+  // the chunk mean from sums of (v - shift), shift = the chunk's first row (a sample of the column):
+  // |v - shift| ~ the column's spread, not its mean, so the fp32 sum keeps the mean accurate to a
+  // few ulps of the spread -- what the backward's near-cancelling sum((y - mean) do) needs (the
+  // GEMM-epilogue statistics use the same shift)
+  if (rg == 0) red[0][cg] = v[0];
+  __syncthreads();
+  const float4 sh = red[0][cg];
+  __syncthreads();
   float4 sum = zero;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int rl = rg + 16 * i;
     if (rl < nrows) {
-      v[i] = f4add(v[i], b);
       *(float4*)(Y + (int64_t)(r0 + rl) * ld + col) = v[i];
-      sum = f4add(sum, v[i]);
+      sum = f4add(sum, make_float4(v[i].x - sh.x, v[i].y - sh.y, v[i].z - sh.z, v[i].w - sh.w));
     }
   }
   red[rg][cg] = sum;
@@ -139,7 +148,8 @@ __global__ __launch_bounds__(256) void k_bn_fwd_partial(const float* __restrict_
 #pragma unroll
   for (int k = 0; k < 16; ++k) tot = f4add(tot, red[k][cg]);
   const float inv = 1.f / (float)nrows;
-  const float4 mean = make_float4(tot.x * inv, tot.y * inv, tot.z * inv, tot.w * inv);
+  const float4 mean = make_float4(fmaf(tot.x, inv, sh.x), fmaf(tot.y, inv, sh.y), fmaf(tot.z, inv, sh.z),
+                                  fmaf(tot.w, inv, sh.w));
   __syncthreads();
   float4 m2 = zero;
 #pragma unroll

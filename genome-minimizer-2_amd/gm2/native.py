@@ -185,7 +185,10 @@ class Workspace:
             try:
                 off = int(buf) - base
                 t = self.buf[off: off + 8 * int(count)].view(torch.float64)
-                with torch.cuda.stream(torch.cuda.ExternalStream(int(strm), device=self.buf.device)):
+                # (the call's stream; NULL = the device's default stream)
+                st = torch.cuda.ExternalStream(int(strm), device=self.buf.device) if strm else \
+                    torch.cuda.default_stream(self.buf.device)
+                with torch.cuda.stream(st):
                     fn(t)
                 return 0
             except Exception as e:  # an exception must not cross the C frames

@@ -3,8 +3,8 @@
 Tolerances (stated per test):
   * training step (both paths): the C2 method of tests/test_gpu_c2.py -- every gradient tensor's
     norm-wise error against the EXACT (fp64) oracle gradient is at most 3x the error of the
-    reference arithmetic (f32 path: the oracle's torch-CPU/MKL fp32 evaluation; bf16 path: fp32 with
-    the bf16 operand rounding emulated) + a floor (2e-4 / 1e-3); losses rel 1e-5 / 1e-4 against the
+    reference arithmetic (the same math in fp32 on the device; for the bf16 path with the bf16 operand
+    rounding emulated) + a floor (2e-4 / 1e-3); losses rel 1e-5 / 1e-4 against the
     sums of the same arithmetic; Adam abs 2e-7 from the GPU's own gradients.
   * sampled masks: bit-exact on every element outside the fp32 rounding band of its logit
     (|logit64| > 1e-3: counted and reported; band elements are reported, not asserted).
@@ -191,9 +191,9 @@ def test_train_step_vs_oracle(prec, G, H, L, B, wg, lam, gemm_pp, bn_epi):
     Gradient bar (the C2 method, tests/test_gpu_c2.py): per tensor, on the norm-wise relative error
     against EXACT (the oracle's explicit gradient in fp64 on the device),
         fro(libgm2) <= 3 * fro(reference arithmetic) + floor,
-    where the reference arithmetic is the oracle's own fp32 evaluation on the CPU (torch + MKL: the
-    reference's arithmetic) for the f32 path, and the same math in fp32 with the bf16 path's operand
-    rounding (manual_grads_emulated) for the bf16 path; floor 2e-4 (f32) / 1e-3 (bf16)."""
+    where the reference arithmetic is the same math evaluated in fp32 on the device (torch fp32
+    GEMMs), with the bf16 path's operand rounding for the bf16 path (manual_grads_emulated); floor
+    2e-4 (f32) / 1e-3 (bf16)."""
     P, S = perturb_bn(*oracle_state(G, H, L, G + B), seed=9)
     X = synth_x(B, G, B)
     torch.manual_seed(1)
@@ -216,11 +216,12 @@ def test_train_step_vs_oracle(prec, G, H, L, B, wg, lam, gemm_pp, bn_epi):
     Pd = {k: v.to(dev) for k, v in P.items()}
     Sd = {k: v.to(dev) for k, v in S.items()}
     exact, sums = O.manual_grads_emulated(Pd, Sd, x.to(dev), ed, beta, wg)
-    if prec == "f32":
-        ref = O.manual_grads(P, S, x, eps, beta, wg, 0.0)  # torch-CPU fp32: the reference's arithmetic
-    else:
-        ref, sums = O.manual_grads_emulated(Pd, Sd, x.to(dev), ed, beta, wg, operand_round=O.bf16_round,
-                                            dtype=torch.float32)
+    # the reference arithmetic: the same math in fp32 (+ the bf16 path's operand rounding)
+    ref, sums_r = O.manual_grads_emulated(Pd, Sd, x.to(dev), ed, beta, wg,
+                                          operand_round=O.bf16_round if prec == "bf16" else None,
+                                          dtype=torch.float32)
+    if prec == "bf16":
+        sums = sums_r  # the loss of the bf16 arithmetic (rounded operands)
     lt = loss.cpu().numpy()
     rtol_loss = 1e-5 if prec == "f32" else 1e-4
     assert abs(lt[0] - sums[0]) <= rtol_loss * abs(sums[0]), (lt[0], sums[0])
