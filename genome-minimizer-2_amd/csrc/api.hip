@@ -228,11 +228,14 @@ struct WsState {
   hipEvent_t slot_done = nullptr;
   gm2_allreduce_fn coll = nullptr;  // SyncBN's all-reduce (gm2_workspace_set_collective)
   void* coll_user = nullptr;
+  hipEvent_t adam9_done = nullptr;  // a deferred output-layer Adam update (GM2_OPT_DEFER_OUTPUT_ADAM)
+  bool adam9_pending = false;
 
   void create() {
     HIP_OK(hipGetDevice(&dev));
     for (auto& e : bucket) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&slot_done, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&adam9_done, hipEventDisableTiming));
   }
   void destroy() {
     if (side) (void)hipStreamDestroy(side);
@@ -240,6 +243,7 @@ struct WsState {
     for (auto e : bucket)
       if (e) (void)hipEventDestroy(e);
     if (slot_done) (void)hipEventDestroy(slot_done);
+    if (adam9_done) (void)hipEventDestroy(adam9_done);
     side = nullptr;
     ev.clear();
   }
@@ -252,6 +256,11 @@ struct WsState {
       for (auto& e : ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     return side;
+  }
+  // make `s` wait for a deferred output-layer Adam update still running on the side stream
+  void join(hipStream_t s) {
+    if (adam9_pending) HIP_OK(hipStreamWaitEvent(s, adam9_done, 0));
+    adam9_pending = false;
   }
   // SyncBN: SUM-all-reduce `count` doubles at device pointer `buf` across the ranks, on `s`
   void allreduce(double* buf, int64_t count, hipStream_t s) {
@@ -453,6 +462,18 @@ void check_batch_data(const gm2_batch* b, const Dims& d, const char* what) {
                    what, (long long)b->ld_data);
 }
 
+// entries [lo, hi) of a kind-1 table, block indices re-based to 0 (a launch over that subset)
+TensorTable table_range(const TensorTable& tt, int lo, int hi) {
+  TensorTable r{};
+  const int64_t base = tt.t[lo].tile0;
+  for (int i = lo; i < hi; ++i) {
+    r.t[r.n] = tt.t[i];
+    r.t[r.n].tile0 -= base;
+    r.n++;
+  }
+  return r;
+}
+
 // ---------------------------------------------------------------------------------------------
 // forward (train or eval). Fills A_l (+A_l^T when train), Y_l, save_l, HD, Z, ZT and runs the
 // fused reconstruction-loss epilogue (dL, dL^T when with_grad).
@@ -503,6 +524,7 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
     ldin = H;
     Kin = H;
   }
+  if (c.st) c.st->join(c.s);  // (a deferred output-layer update must be complete before the output layer)
   if (probs || counts) {  // 3') VAE.forward: p = sigmoid(logits) (model.py:89-90) and / or the
                           // per-strain (TP, FP, FN) of (p > thr) vs the strain's genes; no loss
     GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, B, (int)d.G, H, Bp, (int)d.Gp, 0};
@@ -510,7 +532,9 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
                         (const uint32_t*)(c.ws + c.xbo), d.Gp / 32, thr);
     return;
   }
-  // 3) output layer + reconstruction loss (+ dlogits), computed as logit^T: genes x strains
+  // 3) output layer + reconstruction loss (+ dlogits), computed as logit^T: genes x strains. A
+  // deferred output-layer Adam update of the previous step (side stream) must be complete here.
+  if (c.st) c.st->join(c.s);
   GemmArgs<T> g{c.t(l.sD3), H, c.t(l.A[5]), H, (int)d.G, B, H, (int)d.Gp, Bp, 0};
   launch_gemm_recon_loss<T>(g, prm + d.off[D9B], (const uint32_t*)(c.ws + c.xbo), d.Gp / 32, with_grad, scal, c.t(l.dL),
                             d.Gp, c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
@@ -732,6 +756,7 @@ template <typename T>
 void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr, float* bn, const float* scal,
                double* loss, void* ws, void* strm, WsState& st) {
   if (b->n == 0 && st.opt.sync_bn) {
+    st.join((hipStream_t)strm);  // (it zeroes the whole gradient buffer)
     if (st.slot.staged) HIP_OK(hipStreamWaitEvent((hipStream_t)strm, st.slot_done, 0));
     st.slot.staged = false;
     sync_bn_no_rows(lo, gr, bn, loss, ws, (hipStream_t)strm, st);
@@ -780,6 +805,17 @@ int with_ws(void* ws, F&& f) {
   });
 }
 
+// the same for a call that reads or writes parameters, moments or GEMM shadows from its first
+// launch on: it first joins a deferred output-layer Adam update (the training call instead waits
+// right before the output layer, so the update overlaps its first half)
+template <typename F>
+int with_ws_joined(void* ws, void* stream, F&& f) {
+  return with_ws(ws, [&](WsState& st) {
+    st.join((hipStream_t)stream);
+    f(st);
+  });
+}
+
 }  // namespace
 
 // =================================================================================================
@@ -814,7 +850,7 @@ int gm2_workspace_init(const gm2_dims* d, int prec, void* ws, size_t ws_bytes, v
 }
 
 int gm2_sync_shadows(const gm2_dims* d, int prec, const float* params, void* ws, void* stream) {
-  return with_ws(ws, [&](WsState& st) {
+  return with_ws_joined(ws, stream, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
     if (prec == GM2_F32) {
       Ctx<float> c(lo, ws, stream, &st);
@@ -837,7 +873,7 @@ int gm2_train_fwd_bwd(const gm2_dims* d, int prec, const gm2_batch* batch, const
 
 int gm2_grad_norm(const gm2_dims* d, int prec, const float* params, const float* grads, const float* scalars,
                   double* loss, void* ws, void* stream) {
-  return with_ws(ws, [&](WsState& st) {
+  return with_ws_joined(ws, stream, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
     const int64_t n = lo.d.off[NP];
     const int nb = grad_stats_blocks(n);
@@ -854,24 +890,34 @@ int gm2_grad_norm(const gm2_dims* d, int prec, const float* params, const float*
 
 int gm2_adam_step(const gm2_dims* d, int prec, float* params, const float* grads, float* m, float* v,
                   const float* scalars, void* ws, void* stream) {
-  return with_ws(ws, [&](WsState& st) {
+  return with_ws_joined(ws, stream, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
-    const int64_t n = lo.d.off[NP];
     const float* clip = (const float*)((char*)ws + lo.clip);
-    (void)n;
-    if (prec == GM2_F32) {
-      Ctx<float> c(lo, ws, stream, &st);
-      launch_adam_fused<float>(make_table(c, 1), grads, params, m, v, scalars, clip, c.s);
-    } else {
-      Ctx<bf16_t> c(lo, ws, stream, &st);
-      launch_adam_fused<bf16_t>(make_table(c, 1), grads, params, m, v, scalars, clip, c.s);
-    }
+    auto run = [&](auto tag) {
+      using T = decltype(tag);
+      Ctx<T> c(lo, ws, stream, &st);
+      const TensorTable all = make_table(c, 1);
+      const hipStream_t side = st.opt.defer_adam ? st.side_stream() : nullptr;
+      if (!side) {
+        launch_adam_fused<T>(all, grads, params, m, v, scalars, clip, c.s);
+        return;
+      }
+      // every tensor but the output layer now; decoder.9.{weight,bias} (the table's last two
+      // entries, half the bytes at v0) on the side stream, joined by the next call's output layer
+      launch_adam_fused<T>(table_range(all, 0, all.n - 2), grads, params, m, v, scalars, clip, c.s);
+      st.order(c.s, side);
+      launch_adam_fused<T>(table_range(all, all.n - 2, all.n), grads, params, m, v, scalars, clip, side);
+      HIP_OK(hipEventRecord(st.adam9_done, side));
+      st.adam9_pending = true;
+    };
+    if (prec == GM2_F32) run(float{});
+    else run(bf16_t{});
   });
 }
 
 int gm2_eval_forward(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params,
                      const float* bn_running, const float* scalars, double* loss, void* ws, void* stream) {
-  return with_ws(ws, [&](WsState& st) {
+  return with_ws_joined(ws, stream, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
     drop_stage(st, (hipStream_t)stream);  // these write input slot 0
     float* bn = const_cast<float*>(bn_running);  // eval mode never writes running stats
@@ -887,7 +933,7 @@ int gm2_eval_forward(const gm2_dims* d, int prec, const gm2_batch* batch, const 
 
 int gm2_decode_mask(const gm2_dims* d, const float* params, const float* bn_running, const float* z, int64_t n,
                     uint8_t* mask, int64_t ld_mask, float* probs, int64_t ld_probs, void* ws, void* stream) {
-  return with_ws(ws, [&](WsState& st) {
+  return with_ws_joined(ws, stream, [&](WsState& st) {
     const Layout lo = make_layout(d, GM2_F32);
     if (n <= 0 || n > lo.d.Bm) throw Gm2Error("decode rows %lld outside (0, batch_max]", (long long)n);
     if (ld_mask < lo.d.G || (probs && ld_probs < lo.d.G)) throw Gm2Error("decode: ld < G");
@@ -931,7 +977,7 @@ int gm2_mask_compact(const uint8_t* bits, int64_t n, int64_t ld_bits, const uint
 
 int gm2_decode_bits(const gm2_dims* d, const float* params, const float* bn_running, const float* z, int64_t n,
                     uint8_t* bits, int64_t ld_bits, float* probs, int64_t ld_probs, void* ws, void* stream) {
-  return with_ws(ws, [&](WsState& st) {
+  return with_ws_joined(ws, stream, [&](WsState& st) {
     const Layout lo = make_layout(d, GM2_F32);
     if (n <= 0 || n > lo.d.Bm) throw Gm2Error("decode rows %lld outside (0, batch_max]", (long long)n);
     if (ld_bits < gm2_packed_row_bytes(lo.d.G) || (probs && ld_probs < lo.d.G)) throw Gm2Error("decode_bits: ld too small");
@@ -943,7 +989,7 @@ int gm2_decode_bits(const gm2_dims* d, const float* params, const float* bn_runn
 
 int gm2_recon_counts(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, const float* bn_running,
                      float threshold, int32_t* counts, void* ws, void* stream) {
-  return with_ws(ws, [&](WsState& st) {
+  return with_ws_joined(ws, stream, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
     drop_stage(st, (hipStream_t)stream);  // these write input slot 0
     if (!batch->eps) throw Gm2Error("recon_counts: eps required (model(x) samples z)");
@@ -962,7 +1008,7 @@ int gm2_recon_counts(const gm2_dims* d, int prec, const gm2_batch* batch, const 
 
 int gm2_encode(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, const float* bn_running,
                float* mu, float* logvar, void* ws, void* stream) {
-  return with_ws(ws, [&](WsState& st) {
+  return with_ws_joined(ws, stream, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
     drop_stage(st, (hipStream_t)stream);  // these write input slot 0
     gm2_batch b = *batch;
@@ -1028,7 +1074,7 @@ int gm2_gemm(int prec, int pk, int qk, const void* P, int64_t ldp, const void* Q
 
 int gm2_forward(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, float* bn_running,
                 int train, float* probs, int64_t ld_probs, float* mu, float* logvar, void* ws, void* stream) {
-  return with_ws(ws, [&](WsState& st) {
+  return with_ws_joined(ws, stream, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
     drop_stage(st, (hipStream_t)stream);  // these write input slot 0
     if (!probs || ld_probs < lo.d.G) throw Gm2Error("forward: probs required, ld_probs >= G");
@@ -1050,7 +1096,7 @@ int gm2_forward(const gm2_dims* d, int prec, const gm2_batch* batch, const float
 int gm2_backward_outputs(const gm2_dims* d, int prec, const gm2_batch* batch, const float* params, int train,
                          const float* probs, int64_t ld_probs, const float* dprobs, const float* dmu,
                          const float* dlogvar, float* grads, void* ws, void* stream) {
-  return with_ws(ws, [&](WsState& st) {
+  return with_ws_joined(ws, stream, [&](WsState& st) {
     const Layout lo = make_layout(d, prec);
     drop_stage(st, (hipStream_t)stream);  // these write input slot 0
     if (!probs || !dprobs || ld_probs < lo.d.G) throw Gm2Error("backward_outputs: probs / dprobs required");
@@ -1108,6 +1154,10 @@ int gm2_workspace_set_option(void* ws, int key, int value) {
 
 int gm2_workspace_get_option(void* ws, int key, int* value) {
   return guarded([&] { *value = option_get(ws_state(ws).opt, key); });
+}
+
+int gm2_workspace_join(void* ws, void* stream) {
+  return with_ws(ws, [&](WsState& st) { st.join((hipStream_t)stream); });
 }
 
 int gm2_workspace_set_collective(void* ws, gm2_allreduce_fn fn, void* user) {

@@ -81,6 +81,7 @@ struct Options {
   int grid_cap = 2;      // GM2_OPT_GRID_CAP     capped grids: 1 dW9, 2 dWe0, 4 recon
   int input_chunks = 1;  // GM2_OPT_INPUT_CHUNKS launches of the input-layer weight gradient (1 or 4)
   int sync_bn = 0;       // GM2_OPT_SYNC_BN      train-mode BatchNorm over every rank's rows (collective)
+  int defer_adam = 0;    // GM2_OPT_DEFER_OUTPUT_ADAM  output-layer Adam update overlapped with the next step
 };
 // validated edit of one option (throws on an unknown key or a bad value)
 void option_set(Options& o, int key, int value);

@@ -59,6 +59,7 @@ void option_set(Options& o, int key, int value) {
       o.input_chunks = value;
       break;
     case GM2_OPT_SYNC_BN: o.sync_bn = value ? 1 : 0; break;
+    case GM2_OPT_DEFER_OUTPUT_ADAM: o.defer_adam = value ? 1 : 0; break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -75,6 +76,7 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_GRID_CAP: return o.grid_cap;
     case GM2_OPT_INPUT_CHUNKS: return o.input_chunks;
     case GM2_OPT_SYNC_BN: return o.sync_bn;
+    case GM2_OPT_DEFER_OUTPUT_ADAM: return o.defer_adam;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

@@ -31,12 +31,12 @@ EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_of
            "gm2_mask_row_offsets", "gm2_mask_compact", "gm2_recon_counts",
            "gm2_gemm", "gm2_grad_bucket_bounds", "gm2_wait_grad_bucket", "gm2_set_option", "gm2_get_option",
            "gm2_workspace_set_option", "gm2_workspace_get_option", "gm2_workspace_release",
-           "gm2_workspace_set_collective",
+           "gm2_workspace_set_collective", "gm2_workspace_join",
            "gm2_timing_begin", "gm2_timing_end"]
 ABI_VERSION = 3
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
 OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE, OPT_SMALL_SPLIT, OPT_BN_EPILOGUE, OPT_SMALL_WAVES = 1, 2, 3, 4, 5, 6
-OPT_INPUT_CHUNKS, OPT_SMALL_STAGES, OPT_GRID_CAP, OPT_SYNC_BN = 7, 8, 9, 10
+OPT_INPUT_CHUNKS, OPT_SMALL_STAGES, OPT_GRID_CAP, OPT_SYNC_BN, OPT_DEFER_OUTPUT_ADAM = 7, 8, 9, 10, 11
 # gm2_allreduce_fn (gm2.h): int (double* buf, int64_t count, void* stream, void* user)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
 
@@ -98,6 +98,7 @@ def lib():
         "gm2_workspace_get_option": (C.c_int, [vp, i32, C.POINTER(C.c_int)]),
         "gm2_workspace_release": (C.c_int, [vp]),
         "gm2_workspace_set_collective": (C.c_int, [vp, ALLREDUCE_FN, vp]),
+        "gm2_workspace_join": (C.c_int, [vp, vp]),
         "gm2_timing_begin": (C.c_int, [i32]),
         "gm2_timing_end": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     }
@@ -170,6 +171,11 @@ class Workspace:
         v = C.c_int()
         check(lib().gm2_workspace_get_option(self.ptr, int(key), C.byref(v)), "gm2_workspace_get_option")
         return v.value
+
+    def join(self):
+        """Make torch's current stream wait for work this workspace left running on its side
+        stream (a deferred output-layer Adam update, GM2_OPT_DEFER_OUTPUT_ADAM)."""
+        check(lib().gm2_workspace_join(self.ptr, stream()), "gm2_workspace_join")
 
     def set_collective(self, fn):
         """The SUM all-reduce SyncBN calls (gm2_workspace_set_collective): fn(tensor) reduces a

@@ -267,7 +267,16 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       (forward layers encoder.1 .. decoder.7, then backward decoder.7 .. encoder.1).
  *                       A rank with no rows in a global batch calls gm2_train_fwd_bwd with n = 0: it
  *                       takes part in the 12 all-reduces with zeros, writes zero gradients and loss
- *                       slots, and applies the same running-statistics update. Default 0. */
+ *                       slots, and applies the same running-statistics update. Default 0.
+ *   GM2_OPT_DEFER_OUTPUT_ADAM (workspace option) 1 = gm2_adam_step updates every tensor but the
+ *                       output layer (decoder.9.weight / .bias, half the optimizer's bytes at v0)
+ *                       on the caller's stream and returns with the output layer's update still
+ *                       running on the workspace's side stream, so it overlaps the next training
+ *                       call's gather, input layer and hidden layers; that call waits for it right
+ *                       before the output layer's first use. Results are bit-identical. Until the
+ *                       next call on this workspace, the caller's stream does NOT see the
+ *                       output layer's new parameters / moments: read them only after
+ *                       gm2_workspace_join (every libgm2 call on the workspace joins first). */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -278,12 +287,16 @@ enum {
   GM2_OPT_INPUT_CHUNKS = 7,
   GM2_OPT_SMALL_STAGES = 8,
   GM2_OPT_GRID_CAP = 9,
-  GM2_OPT_SYNC_BN = 10
+  GM2_OPT_SYNC_BN = 10,
+  GM2_OPT_DEFER_OUTPUT_ADAM = 11
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);
 int gm2_workspace_set_option(void* ws, int key, int value);
 int gm2_workspace_get_option(void* ws, int key, int* value);
+/* Make `stream` wait for work the workspace left running on its side stream (a deferred output-
+ * layer Adam update, GM2_OPT_DEFER_OUTPUT_ADAM); no-op when nothing is pending. */
+int gm2_workspace_join(void* ws, void* stream);
 
 /* The all-reduce SyncBN needs (GM2_OPT_SYNC_BN), supplied by the caller: SUM `count` doubles at the
  * DEVICE pointer `buf` (inside the workspace) across every rank, in place, ordered on `stream` (the

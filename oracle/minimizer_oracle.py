@@ -6,10 +6,11 @@ Restatement of the reference genome minimizer's per-sample algorithm, literally 
   _get_positions_to_remove   (:72-86): the set of every position in range(start, end) of them;
   _create_minimized_sequence (:88-103): the bases whose index is not in that set, in order.
 It works on any record exposing .seq and .features with .type / .qualifiers / .location.start/.end
-(gm2.minimizer.read_genbank's records). Parity status: the algorithm is restated from the source;
-Biopython (the reference's GenBank reader) is absent here, so the GenBank parsing itself is pinned
-only by hand-written location cases in tests/test_minimizer_cpu.py ("parity unpinned" against
-Biopython's own parser).
+(gm2.minimizer.read_genbank's records). Parity status: PINNED -- both this restatement and
+gm2.minimizer are checked against tests/golden/minimizer.npz, the outputs of the reference's own
+three methods run on synthetic records (tests/golden/make_golden_minimizer.py). Biopython (the
+reference's GenBank reader) is absent here, so the GenBank PARSING is pinned only by hand-written
+location cases in tests/test_minimizer_cpu.py ("parity unpinned" against Biopython's own parser).
 """
 
 

@@ -527,3 +527,41 @@ def test_two_workspaces_keep_their_own_options_and_state():
             for u, w in zip(x, y):
                 assert torch.equal(u, w)
     assert {k: native.get_option(k) for k in defaults} == defaults
+
+
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+def test_deferred_output_adam_bit_identical(prec):
+    """GM2_OPT_DEFER_OUTPUT_ADAM: the output layer's Adam update of step i runs on the workspace's
+    side stream beside step i+1's first half and is joined right before step i+1's output layer.
+    Four steps (fwd+bwd, clip statistics, Adam) give parameters, moments, gradients, losses and BN
+    statistics bit-identical to the in-step update; a read of the parameters after
+    Workspace.join() sees the final update."""
+    G, H, L, B = 3000, 256, 32, 512
+    P, S = perturb_bn(*oracle_state(G, H, L, 71), seed=72)
+    X = synth_x(2 * B, G, 73)
+    gen = torch.Generator().manual_seed(74)
+    rows = [torch.randperm(2 * B, generator=gen)[:B].to(torch.int32).cuda() for _ in range(4)]
+    eps = [torch.randn(B, L, generator=gen).cuda() for _ in range(4)]
+    pr = native.GM2_F32 if prec == "f32" else native.GM2_BF16
+    outs = []
+    for defer in (0, 1):
+        m = to_model(P, S, G, H, L, pr)
+        mat = ResidentMatrix(X)
+        ws = m.workspace(pr, B)
+        ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, defer)
+        grads = torch.zeros_like(m.params)
+        mom, vel = torch.zeros_like(m.params), torch.zeros_like(m.params)
+        losses = []
+        for i in range(4):
+            sc = scalars(beta=0.37, wgamma=0.55, lam=0.01, step=i + 1)
+            loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+            native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, rows[i], B, eps[i]), m.params, grads, m.bn,
+                                 sc, loss)
+            native.grad_norm(ws, m.params, grads, sc, loss)
+            native.adam_step(ws, m.params, grads, mom, vel, sc)
+            losses.append(loss)
+        ws.join()
+        outs.append([m.params.clone(), mom.clone(), vel.clone(), grads.clone(), m.bn.clone()] + losses)
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
