@@ -96,8 +96,9 @@ def parse():
     ap.add_argument("--input-chunks", type=int, choices=[1, 4], default=None,
                     help="input-layer weight-gradient launches (default: 4 under DDP, else 1)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5-shaped (G=20,000) step line")
-    ap.add_argument("--no-defer-adam", action="store_true",
-                    help="run the output layer's Adam update inside its own step (GM2_OPT_DEFER_OUTPUT_ADAM off)")
+    ap.add_argument("--defer-adam", action="store_true",
+                    help="overlap the output layer's Adam update with the next step (GM2_OPT_DEFER_OUTPUT_ADAM; "
+                         "bit-identical, measured neutral on one GPU: profiles/r03_defer_adam_ab.txt)")
     ap.add_argument("--c5-strains", type=int, default=12500,
                     help="strains resident per rank for the C5 line (the 1/8 shard of 100,000)")
     return ap.parse_args()
@@ -246,9 +247,9 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         ws.set_option(native.OPT_SMALL_STAGES, a.small_stages)
     if a.grid_cap is not None:
         ws.set_option(native.OPT_GRID_CAP, a.grid_cap)
-    # the output layer's Adam update overlaps the next step's gather, input layer and hidden layers
-    # (bit-identical; the timed region ends with a device-wide synchronize)
-    ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, 0 if a.no_defer_adam else 1)
+    # optionally the output layer's Adam update overlaps the next step's gather, input layer and
+    # hidden layers (bit-identical; the timed region ends with a device-wide synchronize)
+    ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, 1 if a.defer_adam else 0)
     # next-batch staging (gm2_batch.next) only under DDP, where the gather fills the wait for the
     # input-layer exchange; on one GPU it measured ~30 us/step slower (profiles/r02_prefetch_ab_*)
     prefetch = dist is not None and not a.no_prefetch

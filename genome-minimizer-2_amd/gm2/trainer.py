@@ -318,10 +318,6 @@ class VAETrainer:
         scal = self._upload(srows)
         ws = model.workspace(model.precision, (loader.batch_size + world - 1) // world)
         rec = torch.zeros(max(nb, 1), native.LOSS_SLOTS, dtype=torch.float64, device=self.device)
-        # the output layer's Adam update of each step overlaps the next step's first half
-        # (GM2_OPT_DEFER_OUTPUT_ADAM, bit-identical); joined before anything reads the parameters
-        if ws.get_option(native.OPT_DEFER_OUTPUT_ADAM) != 1:
-            ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, 1)
         sync = self._grad_sync(dist) if dist else None
         sync_bn = dist is not None and self.sync_bn
         if sync:
@@ -351,7 +347,7 @@ class VAETrainer:
             self.optimizer.step_count += 1
             model.shadows_current(model.precision)
             self._bump_bn()
-        ws.join()  # the last deferred output-layer update: parameters final on this stream
+        ws.join()  # (a deferred output-layer update, GM2_OPT_DEFER_OUTPUT_ADAM, if one was asked for)
         if dist:
             reduce_loss_rows(dist, rec)
             if not sync_bn:  # (SyncBN: every rank applied the same global-batch updates)
