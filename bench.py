@@ -96,9 +96,13 @@ def parse():
     ap.add_argument("--input-chunks", type=int, choices=[1, 4], default=None,
                     help="input-layer weight-gradient launches (default: 4 under DDP, else 1)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5-shaped (G=20,000) step line")
-    ap.add_argument("--defer-adam", action="store_true",
-                    help="overlap the output layer's Adam update with the next step (GM2_OPT_DEFER_OUTPUT_ADAM; "
-                         "bit-identical, measured neutral on one GPU: profiles/r03_defer_adam_ab.txt)")
+    ap.add_argument("--defer-adam", type=int, default=None,
+                    help="output layer's Adam update launched beside the next step's hidden layers on this many "
+                         "workgroups per CU, 0 = not deferred (GM2_OPT_DEFER_OUTPUT_ADAM; bit-identical)")
+    ap.add_argument("--dw9-last", type=int, choices=[0, 1], default=None,
+                    help="output-layer weight gradient beside the input-layer one (GM2_OPT_DW9_LAST)")
+    ap.add_argument("--side-priority", type=int, choices=[-1, 0, 1], default=None,
+                    help="priority of the workspace's side stream (GM2_OPT_SIDE_PRIORITY)")
     ap.add_argument("--c5-strains", type=int, default=12500,
                     help="strains resident per rank for the C5 line (the 1/8 shard of 100,000)")
     return ap.parse_args()
@@ -247,9 +251,14 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         ws.set_option(native.OPT_SMALL_STAGES, a.small_stages)
     if a.grid_cap is not None:
         ws.set_option(native.OPT_GRID_CAP, a.grid_cap)
-    # optionally the output layer's Adam update overlaps the next step's gather, input layer and
-    # hidden layers (bit-identical; the timed region ends with a device-wide synchronize)
-    ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, 1 if a.defer_adam else 0)
+    # the output layer's Adam update queued and launched beside the next step's hidden layers
+    # (bit-identical; the timed region ends with ws.join(), which launches / waits for the last one)
+    if a.defer_adam is not None:
+        ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, a.defer_adam)
+    if a.side_priority is not None:
+        ws.set_option(native.OPT_SIDE_PRIORITY, a.side_priority)
+    if a.dw9_last is not None:
+        ws.set_option(native.OPT_DW9_LAST, a.dw9_last)
     # next-batch staging (gm2_batch.next) only under DDP, where the gather fills the wait for the
     # input-layer exchange; on one GPU it measured ~30 us/step slower (profiles/r02_prefetch_ab_*)
     prefetch = dist is not None and not a.no_prefetch
@@ -268,6 +277,7 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
 
     for i in range(a.warmup):
         step(i)
+    ws.join()  # (a queued output-layer update runs before the timed region, the timed steps' inside it)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -276,6 +286,7 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
     t0 = time.perf_counter()
     for i in range(a.warmup, nsteps):
         step(i)
+    ws.join()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -296,6 +307,8 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         raise RuntimeError(f"non-finite loss / gradient norm at step(s) {np.flatnonzero(bad).tolist()}")
     info = {"prefetch": prefetch, "input_chunks": ws.get_option(native.OPT_INPUT_CHUNKS),
             "defer_adam": ws.get_option(native.OPT_DEFER_OUTPUT_ADAM),
+            "side_priority": ws.get_option(native.OPT_SIDE_PRIORITY),
+            "dw9_last": ws.get_option(native.OPT_DW9_LAST),
             "x": x if (rank == 0 and world == 1) else None, "mat": mat}
     del model, opt, ws, grads, sync
     return elapsed, k_ms, k_n, info
@@ -358,7 +371,8 @@ def main():
                                      f"SUM all-reduce overlapped with the backward, input-layer gradient in "
                                      f"{info['input_chunks']} launch(es)")
                    if world > 1 else "none (one GPU)",
-                   "input_prefetch": info["prefetch"], "deferred_output_adam": bool(info["defer_adam"])},
+                   "input_prefetch": info["prefetch"], "deferred_output_adam": info["defer_adam"],
+                   "side_priority": info["side_priority"], "dw9_last": info["dw9_last"]},
         "train_tflops": round(value * train_flops_per_vector(G, H, L) / 1e12, 2),
         "nonfinite_steps": 0,
         # dominant kernel: decoder output layer GEMM [B,H]x[H,G] + fused BCE/abundance/dlogits epilogue

@@ -96,6 +96,7 @@ struct Layout {
   int64_t nahdr, nasq;         // norm-ahead header int[4] and per-tile sums of squares (NormAhead)
   int64_t X1, XB1;             // second input slot: the next batch's rows, staged under this step's tail
   int64_t syncb;               // SyncBN all-reduce vector: 2H + 2 doubles
+  int64_t adamscal;            // scalar block of a queued output-layer Adam update
 };
 
 Layout make_layout(const gm2_dims* gd, int prec) {
@@ -157,6 +158,7 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.X1 = take(Bm * d.Gp * es);
   o.XB1 = take(Bm * (d.Gp / 32) * 4);
   o.syncb = take((2 * H + 2) * 8);
+  o.adamscal = take(GM2_NUM_SCALARS * 4);
   o.total = cur;
   return o;
 }
@@ -216,6 +218,20 @@ struct SlotState {
   int prec = -1;
 };
 
+// Events that only order this device's own streams (fork / join ring, staged input slot, deferred
+// update) release at device scope: a system-scope release writes the L2 back at every fork of the
+// backward (measured ~7 us of idle main stream per fork). The gradient-bucket events keep the
+// system-scope release (a collective's peers may read the buffer). Env GM2_EVENT_FENCE=system
+// restores it everywhere (A/B).
+unsigned order_event_flags() {
+  static const unsigned f = [] {
+    const char* e = std::getenv("GM2_EVENT_FENCE");
+    return (e && std::string(e) == "system") ? (unsigned)hipEventDisableTiming
+                                             : (unsigned)(hipEventDisableTiming | hipEventReleaseToDevice);
+  }();
+  return f;
+}
+
 struct WsState {
   Options opt;
   int dev = -1;
@@ -229,13 +245,26 @@ struct WsState {
   gm2_allreduce_fn coll = nullptr;  // SyncBN's all-reduce (gm2_workspace_set_collective)
   void* coll_user = nullptr;
   hipEvent_t adam9_done = nullptr;  // a deferred output-layer Adam update (GM2_OPT_DEFER_OUTPUT_ADAM)
-  bool adam9_pending = false;
+  bool adam9_pending = false;       // launched on the side stream, not yet joined
+  int side_prio = 0;                // priority the side stream was created with
+  int cus = 0;                      // compute units of dev
+  // the queued (not yet launched) output-layer update: launched by kick() beside the next training
+  // call's hidden layers, or by join() on the joining stream
+  struct QueuedAdam {
+    bool queued = false;
+    int prec = 0;
+    TensorTable tt{};
+    const float* g = nullptr;
+    float *p = nullptr, *m = nullptr, *v = nullptr;
+    const float *scal = nullptr, *clip = nullptr;
+  } qadam;
 
   void create() {
     HIP_OK(hipGetDevice(&dev));
+    HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     for (auto& e : bucket) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&slot_done, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&adam9_done, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&slot_done, order_event_flags()));
+    HIP_OK(hipEventCreateWithFlags(&adam9_done, order_event_flags()));
   }
   void destroy() {
     if (side) (void)hipStreamDestroy(side);
@@ -247,18 +276,54 @@ struct WsState {
     side = nullptr;
     ev.clear();
   }
-  // the side stream when GM2_OPT_SIDE_STREAM is on (created on first use), else nullptr
+  // the side stream when GM2_OPT_SIDE_STREAM is on (created on first use, at GM2_OPT_SIDE_PRIORITY;
+  // re-created after draining when that option changed), else nullptr
   hipStream_t side_stream() {
     if (!opt.side_stream) return nullptr;
+    if (side && side_prio != opt.side_priority) {
+      HIP_OK(hipStreamSynchronize(side));
+      HIP_OK(hipStreamDestroy(side));
+      side = nullptr;
+    }
     if (!side) {
-      HIP_OK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-      ev.resize(64);
-      for (auto& e : ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      int least = 0, greatest = 0;
+      HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      const int prio = opt.side_priority > 0 ? least : opt.side_priority < 0 ? greatest : 0;
+      HIP_OK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, std::min(std::max(prio, greatest), least)));
+      side_prio = opt.side_priority;
+      if (ev.empty()) {
+        ev.resize(64);
+        for (auto& e : ev) HIP_OK(hipEventCreateWithFlags(&e, order_event_flags()));
+      }
     }
     return side;
   }
-  // make `s` wait for a deferred output-layer Adam update still running on the side stream
+  void launch_queued(hipStream_t s, int max_grid = 0) {
+    QueuedAdam& q = qadam;
+    if (q.prec == GM2_F32) launch_adam_fused<float>(q.tt, q.g, q.p, q.m, q.v, q.scal, q.clip, s, max_grid);
+    else launch_adam_fused<bf16_t>(q.tt, q.g, q.p, q.m, q.v, q.scal, q.clip, s, max_grid);
+    q.queued = false;
+  }
+  // a training call's forward, after its input-layer GEMM: start the queued output-layer update on
+  // the side stream (ordered after everything on `s` so far)
+  void kick(hipStream_t s) {
+    if (!qadam.queued) return;
+    const hipStream_t sd = side_stream();
+    if (!sd) {
+      launch_queued(s);
+      return;
+    }
+    order(s, sd);
+    // a few workgroups per CU, looping over the blocks: room stays for the hidden layers' GEMM
+    // workgroups (an uncapped grid fills every CU and serialises them behind it)
+    launch_queued(sd, std::max(1, opt.defer_adam) * std::max(1, cus));
+    HIP_OK(hipEventRecord(adam9_done, sd));
+    adam9_pending = true;
+  }
+  // make `s` see a deferred output-layer update: a queued one is launched on `s`, a running one
+  // waited for
   void join(hipStream_t s) {
+    if (qadam.queued) launch_queued(s);
     if (adam9_pending) HIP_OK(hipStreamWaitEvent(s, adam9_done, 0));
     adam9_pending = false;
   }
@@ -513,6 +578,10 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
     }
     linear_pre_bn<T>(c, in, ldin, Bp, c.t(shadow_in[i]), i == 3 ? d.Lr : Kin, B, H, Kin, prm + d.off[kBlk[i][1]],
                      c.f(l.Y[i]), c.f(l.bnpart), train != 0);
+    // a queued output-layer Adam update of the previous step starts here, beside the hidden layers
+    // (HBM-bound next to latency-bound small GEMMs; the gather and the input-layer GEMM before this
+    // point leave it nothing: one is HBM-bound too, the other holds every CU's registers)
+    if (i == 0 && c.st) c.st->kick(c.s);
     if (sync) {  // SyncBN: this rank's column sums -> all-reduce -> the global batch's statistics
       launch_bn_sync_pack(c.f(l.bnpart), B, H, 0, syncb, c.s);
       c.st->allreduce(syncb, 2 * H + 2, c.s);
@@ -586,8 +655,8 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   // GPU; first keeps gradient bucket 0 early for the data-parallel exchange.)
   const BigGrads<T> bg = big_grads<T>(c, Bp);
   double* nasq = (double*)(c.ws + l.nasq);
-  fork();
-  {
+  auto output_weight_grad = [&] {
+    fork();
     const GemmArgs<T>& g9 = bg.g9;
     if (plan_gemm<T>(g9).splits == 1) {
       // (A5^T here on the side stream; on the main stream before the fork measured ~35 us/step
@@ -597,8 +666,13 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     } else {
       gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
     }
-  }
-  HIP_OK(hipEventRecord(st.bucket[0], w.s));
+    HIP_OK(hipEventRecord(st.bucket[0], w.s));
+  };
+  // GM2_OPT_DW9_LAST: forked beside the input-layer dWe0 GEMM instead, so the hidden-layer chain
+  // runs without the 126-us tiles of dW9 holding every CU, and the two big weight-gradient GEMMs'
+  // tile rounds interleave (their last rounds fill each other's idle CUs)
+  const bool dw9_last = st.opt.dw9_last != 0 && sr;
+  if (!dw9_last) output_weight_grad();
   // dA_j = dY . W (K-major dY, MN-major W) into the slab area; when the plan allows, the GEMM's
   // epilogue also takes BatchNorm j's backward partials (sum do, sum (y-mean) do)
   bool have_part = false;
@@ -646,6 +720,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       // is; dWe0 starts without waiting for it (the join follows the dWe0 launch: the side stream's
       // last small GEMM / column sums run beside dWe0's first tiles instead of before them)
       HIP_OK(hipEventRecord(st.bucket[1], w.s));
+      if (dw9_last) output_weight_grad();
       if (input_chunked(bg, H)) {  // four row-quarter launches, bucket 2 + q final after launch q
         for (int q = 0; q < 4; ++q) {
           GemmArgs<T> gq = bg.g0;
@@ -897,18 +972,25 @@ int gm2_adam_step(const gm2_dims* d, int prec, float* params, const float* grads
       using T = decltype(tag);
       Ctx<T> c(lo, ws, stream, &st);
       const TensorTable all = make_table(c, 1);
-      const hipStream_t side = st.opt.defer_adam ? st.side_stream() : nullptr;
-      if (!side) {
+      if (!st.opt.defer_adam || !st.opt.side_stream) {
         launch_adam_fused<T>(all, grads, params, m, v, scalars, clip, c.s);
         return;
       }
       // every tensor but the output layer now; decoder.9.{weight,bias} (the table's last two
-      // entries, half the bytes at v0) on the side stream, joined by the next call's output layer
+      // entries, half the bytes at v0) queued with a copy of the scalar block (see WsState::kick)
       launch_adam_fused<T>(table_range(all, 0, all.n - 2), grads, params, m, v, scalars, clip, c.s);
-      st.order(c.s, side);
-      launch_adam_fused<T>(table_range(all, all.n - 2, all.n), grads, params, m, v, scalars, clip, side);
-      HIP_OK(hipEventRecord(st.adam9_done, side));
-      st.adam9_pending = true;
+      float* qs = (float*)((char*)ws + lo.adamscal);
+      HIP_OK(hipMemcpyAsync(qs, scalars, GM2_NUM_SCALARS * 4, hipMemcpyDeviceToDevice, c.s));
+      WsState::QueuedAdam& q = st.qadam;
+      q.queued = true;
+      q.prec = prec;
+      q.tt = table_range(all, all.n - 2, all.n);
+      q.g = grads;
+      q.p = params;
+      q.m = m;
+      q.v = v;
+      q.scal = qs;
+      q.clip = clip;
     };
     if (prec == GM2_F32) run(float{});
     else run(bf16_t{});

@@ -39,7 +39,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 // Diagnostic timestamps (s_memrealtime, 100 MHz) of the store kernel's phases per workgroup; only
 // compiled into the standalone probe tools/stamp_gemm.hip, never into libgm2.
 #ifdef GM2_STAMPS
-__device__ unsigned long long g_stamp[16384][4];
+__device__ unsigned long long g_stamp[16384][8];
 #define GM2_STAMP(i) \
   if (threadIdx.x == 0) g_stamp[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime()
 #else
@@ -852,6 +852,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const 
                                                          float* __restrict__ loss_part, float* __restrict__ colpart,
                                                          int64_t ldcol) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  GM2_STAMP(0);
   const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
   if (ntiles == 0) {
     recon_loss_tile<C, T, PP, GRAD>(tile_of<C>(tm, tn), g, bias, xbits, ldxb, scal, dL, ldd, loss_part, colpart,
@@ -891,6 +892,7 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
     mainloop_pp<true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   else
     mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+  GM2_STAMP(2);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   const int q = lane >> 4, c = lane & 15;
   const float wgam = scal[kScalWGamma];
@@ -905,6 +907,7 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
     recon_tile<C, T, FAST, false, GRAD>(acc, xbits + ((tl.m0 + wm * C::WTM) >> 5), ldxb, bias_s, g.N, tl.n0, wm, wn,
                                         q, c, wgam, img, bce, psum);
   if constexpr (FAST) bce *= -0.6931471805599453f;
+  GM2_STAMP(4);
   if constexpr (GRAD) {
     __syncthreads();
     // dL rows (strains) of BM genes: full 16-byte stores along each row. Thread i keeps one chunk
@@ -962,6 +965,11 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
       if (gg < g.M) colpart[(int64_t)(tl.n0 / C::BN) * ldcol + gg] = v;
     }
   }
+#ifdef GM2_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  GM2_STAMP(3);
+#endif
 }
 
 template <class C, typename T>
@@ -1120,7 +1128,10 @@ TimedLaunch::TimedLaunch(int cls, hipStream_t st) : idx(-1), s(st) {
   if (!(t.classes & cls)) return;
   if (t.used == t.ev.size()) {
     hipEvent_t a, b;
-    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) throw Gm2Error("hipEventCreate");
+    // (device-scope release: no L2 write-back around the timed kernel)
+    if (hipEventCreateWithFlags(&a, hipEventReleaseToDevice) != hipSuccess ||
+        hipEventCreateWithFlags(&b, hipEventReleaseToDevice) != hipSuccess)
+      throw Gm2Error("hipEventCreate");
     t.ev.push_back({a, b});
   }
   idx = (int)t.used++;

@@ -81,7 +81,10 @@ struct Options {
   int grid_cap = 2;      // GM2_OPT_GRID_CAP     capped grids: 1 dW9, 2 dWe0, 4 recon
   int input_chunks = 1;  // GM2_OPT_INPUT_CHUNKS launches of the input-layer weight gradient (1 or 4)
   int sync_bn = 0;       // GM2_OPT_SYNC_BN      train-mode BatchNorm over every rank's rows (collective)
-  int defer_adam = 0;    // GM2_OPT_DEFER_OUTPUT_ADAM  output-layer Adam update overlapped with the next step
+  int defer_adam = 0;    // GM2_OPT_DEFER_OUTPUT_ADAM  output-layer Adam update beside the next step's hidden
+                         //   layers on this many workgroups per CU (0 = not deferred)
+  int side_priority = 0; // GM2_OPT_SIDE_PRIORITY  side stream priority: -1 high, 0 normal, 1 low
+  int dw9_last = 0;      // GM2_OPT_DW9_LAST  output-layer weight gradient forked beside dWe0, not first
 };
 // validated edit of one option (throws on an unknown key or a bad value)
 void option_set(Options& o, int key, int value);
@@ -266,10 +269,11 @@ struct TensorTable {
 template <typename T>
 void launch_shadow_sync(const TensorTable& tt, const float* params, hipStream_t s);
 // fused L1 + clip + Adam over the full 30-tensor table (tile0 = first 4096-element block of each
-// tensor), writing natural-layout shadows of the tensors that have one
+// tensor), writing natural-layout shadows of the tensors that have one; max_grid > 0 caps the
+// workgroups (each then loops over blocks)
 template <typename T>
 void launch_adam_fused(const TensorTable& tt, const float* grads, float* params, float* m, float* v, const float* scal,
-                       const float* clip, hipStream_t s);
+                       const float* clip, hipStream_t s, int max_grid = 0);
 // sum((g + lambda*sign(p))^2) and sum(|p|) over all params -> partials; then finalize
 // Clip-norm statistics taken in the GEMM epilogues of the training call (StoreEpi::sq): hdr[0] = 1
 // when both big weight gradients (input layer [lo0, hi0), output layer [lo9, hi9) of the flat

@@ -612,15 +612,13 @@ __global__ __launch_bounds__(256) void k_grad_finalize(const double* __restrict_
 
 // fused L1 + clip + Adam over one tensor table entry per block group, writing the fp32 master and
 // the natural-layout GEMM shadow in the same pass (30 B/param of HBM traffic instead of 30 + 6)
+// (one 4096-element block `blk` of tensor d)
 template <typename T>
-__global__ __launch_bounds__(256) void k_adam_fused(TensorTable tt, const float* __restrict__ g, float* __restrict__ p,
-                                                  float* __restrict__ m, float* __restrict__ v,
-                                                  const float* __restrict__ scal, const float* __restrict__ clip) {
-  int ti = 0;
-  while (ti + 1 < tt.n && (int64_t)blockIdx.x >= tt.t[ti + 1].tile0) ++ti;
-  const TensorDesc& d = tt.t[ti];
+__device__ __forceinline__ void adam_block(const TensorDesc& d, int64_t blk, const float* __restrict__ g,
+                                           float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
+                                           const float* __restrict__ scal, const float* __restrict__ clip) {
   const int64_t numel = d.rows * d.cols;
-  const int64_t e0 = ((int64_t)blockIdx.x - d.tile0) * 4096;  // 4096 elements per block
+  const int64_t e0 = (blk - d.tile0) * 4096;  // 4096 elements per block
   const float lam = scal[kScalLambda], negstep = scal[kScalNegStep], bc2s = scal[kScalBc2Sqrt];
   const float w1 = scal[kScalOneMinusB1], b2 = scal[kScalBeta2], w2 = scal[kScalOneMinusB2];
   const float aeps = scal[kScalAdamEps];
@@ -727,6 +725,20 @@ __global__ __launch_bounds__(256) void k_adam_fused(TensorTable tt, const float*
         }
       }
     }
+  }
+}
+
+// blocks blockIdx.x, + gridDim.x, ... of the table (one per workgroup unless the grid is capped:
+// the deferred output-layer update runs on a few workgroups per CU beside the hidden layers)
+template <typename T>
+__global__ __launch_bounds__(256) void k_adam_fused(TensorTable tt, const float* __restrict__ g, float* __restrict__ p,
+                                                  float* __restrict__ m, float* __restrict__ v,
+                                                  const float* __restrict__ scal, const float* __restrict__ clip,
+                                                  int64_t nblocks) {
+  int ti = 0;
+  for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+    while (ti + 1 < tt.n && blk >= tt.t[ti + 1].tile0) ++ti;
+    adam_block<T>(tt.t[ti], blk, g, p, m, v, scal, clip);
   }
 }
 
@@ -1182,12 +1194,14 @@ void launch_shadow_sync(const TensorTable& tt, const float* params, hipStream_t 
 
 template <typename T>
 void launch_adam_fused(const TensorTable& tt, const float* grads, float* params, float* m, float* v, const float* scal,
-                       const float* clip, hipStream_t s) {
+                       const float* clip, hipStream_t s, int max_grid) {
   const TensorDesc& last = tt.t[tt.n - 1];
   const int64_t blocks = last.tile0 + (last.rows * last.cols + 4095) / 4096;
   for (int i = 0; i < tt.n; ++i)
     if (tt.t[i].off % 4) throw Gm2Error("adam: tensor offset not 16-B aligned");
-  hipLaunchKernelGGL(k_adam_fused<T>, dim3((unsigned)blocks), dim3(256), 0, s, tt, grads, params, m, v, scal, clip);
+  const int64_t grid = max_grid > 0 ? std::min<int64_t>(blocks, max_grid) : blocks;
+  hipLaunchKernelGGL(k_adam_fused<T>, dim3((unsigned)grid), dim3(256), 0, s, tt, grads, params, m, v, scal, clip,
+                     blocks);
   GM2_CHECK_LAUNCH();
 }
 
@@ -1234,7 +1248,7 @@ void launch_grad_finalize(const double* part, int nblocks, const float* scal, fl
                                        hipStream_t, const double*);                                             \
   template void launch_transpose<T>(const T*, int64_t, int, int, T*, int64_t, hipStream_t);                    \
   template void launch_adam_fused<T>(const TensorTable&, const float*, float*, float*, float*, const float*,    \
-                                     const float*, hipStream_t);
+                                     const float*, hipStream_t, int);
 GM2_INST(float)
 GM2_INST(bf16_t)
 #undef GM2_INST

@@ -59,7 +59,15 @@ void option_set(Options& o, int key, int value) {
       o.input_chunks = value;
       break;
     case GM2_OPT_SYNC_BN: o.sync_bn = value ? 1 : 0; break;
-    case GM2_OPT_DEFER_OUTPUT_ADAM: o.defer_adam = value ? 1 : 0; break;
+    case GM2_OPT_DEFER_OUTPUT_ADAM:
+      if (value < 0 || value > 16) throw Gm2Error("deferred output-layer update: %d workgroups per CU (0..16)", value);
+      o.defer_adam = value;
+      break;
+    case GM2_OPT_SIDE_PRIORITY:
+      if (value < -1 || value > 1) throw Gm2Error("side priority %d: -1, 0 or 1", value);
+      o.side_priority = value;
+      break;
+    case GM2_OPT_DW9_LAST: o.dw9_last = value ? 1 : 0; break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -77,6 +85,8 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_INPUT_CHUNKS: return o.input_chunks;
     case GM2_OPT_SYNC_BN: return o.sync_bn;
     case GM2_OPT_DEFER_OUTPUT_ADAM: return o.defer_adam;
+    case GM2_OPT_SIDE_PRIORITY: return o.side_priority;
+    case GM2_OPT_DW9_LAST: return o.dw9_last;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

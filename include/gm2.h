@@ -268,15 +268,25 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       A rank with no rows in a global batch calls gm2_train_fwd_bwd with n = 0: it
  *                       takes part in the 12 all-reduces with zeros, writes zero gradients and loss
  *                       slots, and applies the same running-statistics update. Default 0.
- *   GM2_OPT_DEFER_OUTPUT_ADAM (workspace option) 1 = gm2_adam_step updates every tensor but the
+ *   GM2_OPT_DEFER_OUTPUT_ADAM (workspace option) n >= 1 = gm2_adam_step updates every tensor but the
  *                       output layer (decoder.9.weight / .bias, half the optimizer's bytes at v0)
- *                       on the caller's stream and returns with the output layer's update still
- *                       running on the workspace's side stream, so it overlaps the next training
- *                       call's gather, input layer and hidden layers; that call waits for it right
- *                       before the output layer's first use. Results are bit-identical. Until the
- *                       next call on this workspace, the caller's stream does NOT see the
- *                       output layer's new parameters / moments: read them only after
- *                       gm2_workspace_join (every libgm2 call on the workspace joins first). */
+ *                       on the caller's stream and returns with the output layer's update QUEUED
+ *                       (its scalar block copied into the workspace): the next training call
+ *                       launches it on the workspace's side stream right after its input-layer
+ *                       GEMM, on n workgroups per CU (1..16) beside the hidden layers, and waits
+ *                       for it before the output layer. 0 = not deferred (default).
+ *                       Results are bit-identical. Until then the output layer's parameters /
+ *                       moments are not updated: read them only after gm2_workspace_join (every
+ *                       other libgm2 call on the workspace joins first, which launches a queued
+ *                       update on its stream), and keep the buffers passed to gm2_adam_step alive.
+ *   GM2_OPT_SIDE_PRIORITY priority of the workspace's side stream (weight-gradient GEMMs, a
+ *                       deferred output-layer update): 0 = normal (default), 1 = low (the caller's
+ *                       critical-path kernels take CUs first), -1 = high. Takes effect at the next
+ *                       side-stream use (the stream is re-created after draining).
+ *   GM2_OPT_DW9_LAST    1 = the output-layer weight-gradient GEMM (gradient bucket 0) is forked
+ *                       beside the input-layer one at the end of the backward instead of first
+ *                       (the hidden-layer chain then runs without it); bucket 0 becomes final late,
+ *                       so a data-parallel exchange overlaps less of it. Default 0. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -288,7 +298,9 @@ enum {
   GM2_OPT_SMALL_STAGES = 8,
   GM2_OPT_GRID_CAP = 9,
   GM2_OPT_SYNC_BN = 10,
-  GM2_OPT_DEFER_OUTPUT_ADAM = 11
+  GM2_OPT_DEFER_OUTPUT_ADAM = 11,
+  GM2_OPT_SIDE_PRIORITY = 12,
+  GM2_OPT_DW9_LAST = 13
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);

@@ -473,6 +473,40 @@ def test_capped_grid_bit_identical(G):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("G", [20480, 16500])
+def test_backward_schedule_options_bit_identical(G):
+    """GM2_OPT_DW9_LAST (output-layer weight gradient forked beside the input-layer one) and
+    GM2_OPT_SIDE_PRIORITY (low / high side stream) only reorder launches: gradients, loss record and
+    clip statistics are bit-identical to the default schedule, with the one-launch and the
+    four-quarter input-layer gradient."""
+    H, L, B = 1024, 32, 1024
+    P, S = perturb_bn(*oracle_state(G, H, L, G + 7), seed=41)
+    X = synth_x(B, G, 42)
+    eps = torch.randn(B, L, generator=torch.Generator().manual_seed(43)).cuda()
+    sc = scalars(beta=0.37, wgamma=0.55, lam=0.0)
+    sc[native.S_NORM_AHEAD] = 1.0
+    outs = []
+    for last, prio, chunks in ((0, 0, 1), (1, 0, 1), (1, 1, 1), (1, -1, 4), (0, 1, 4)):
+        m = to_model(P, S, G, H, L, native.GM2_BF16)
+        mat = ResidentMatrix(X)
+        ws = m.workspace(native.GM2_BF16, B)
+        ws.set_option(native.OPT_DW9_LAST, last)
+        ws.set_option(native.OPT_SIDE_PRIORITY, prio)
+        ws.set_option(native.OPT_INPUT_CHUNKS, chunks)
+        grads = torch.zeros_like(m.params)
+        loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+        native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, B, eps), m.params, grads, m.bn, sc, loss)
+        native.grad_norm(ws, m.params, grads, sc, loss)
+        torch.cuda.synchronize()
+        outs.append((grads.cpu(), loss.cpu()))
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0])
+        assert torch.equal(outs[0][1][:3], o[1][:3])
+    # the clip statistics: from the GEMM epilogues (one input-layer launch) or the re-reading pass
+    for o in outs[1:]:
+        assert float(o[1][4]) == pytest.approx(float(outs[0][1][4]), rel=1e-6)
+
+
 def test_two_workspaces_keep_their_own_options_and_state():
     """ABI 3: tuning options, side stream, gradient-bucket events and the staged input slot belong to
     the workspace. Two models trained interleaved in one process, one with the ping-pong main loop,
@@ -531,11 +565,13 @@ def test_two_workspaces_keep_their_own_options_and_state():
 
 @pytest.mark.parametrize("prec", ["f32", "bf16"])
 def test_deferred_output_adam_bit_identical(prec):
-    """GM2_OPT_DEFER_OUTPUT_ADAM: the output layer's Adam update of step i runs on the workspace's
-    side stream beside step i+1's first half and is joined right before step i+1's output layer.
-    Four steps (fwd+bwd, clip statistics, Adam) give parameters, moments, gradients, losses and BN
-    statistics bit-identical to the in-step update; a read of the parameters after
-    Workspace.join() sees the final update."""
+    """GM2_OPT_DEFER_OUTPUT_ADAM = n: the output layer's Adam update of step i is queued (with a copy
+    of step i's scalar block, whose tensor is gone by then) and launched on the workspace's side
+    stream after step i+1's input-layer GEMM on n workgroups per CU, joined right before step i+1's
+    output layer. Four steps (fwd+bwd, clip statistics, Adam) give parameters, moments, gradients,
+    losses and BN statistics bit-identical to the in-step update, with n = 1 and 3 and with an
+    explicit Workspace.join() after a step (the queued update then runs on the caller's stream); a
+    read of the parameters after Workspace.join() sees the final update."""
     G, H, L, B = 3000, 256, 32, 512
     P, S = perturb_bn(*oracle_state(G, H, L, 71), seed=72)
     X = synth_x(2 * B, G, 73)
@@ -544,7 +580,7 @@ def test_deferred_output_adam_bit_identical(prec):
     eps = [torch.randn(B, L, generator=gen).cuda() for _ in range(4)]
     pr = native.GM2_F32 if prec == "f32" else native.GM2_BF16
     outs = []
-    for defer in (0, 1):
+    for defer, join_after in ((0, None), (1, None), (3, None), (2, 1)):
         m = to_model(P, S, G, H, L, pr)
         mat = ResidentMatrix(X)
         ws = m.workspace(pr, B)
@@ -559,9 +595,13 @@ def test_deferred_output_adam_bit_identical(prec):
                                  sc, loss)
             native.grad_norm(ws, m.params, grads, sc, loss)
             native.adam_step(ws, m.params, grads, mom, vel, sc)
+            del sc
+            if i == join_after:
+                ws.join()
             losses.append(loss)
         ws.join()
         outs.append([m.params.clone(), mom.clone(), vel.clone(), grads.clone(), m.bn.clone()] + losses)
     torch.cuda.synchronize()
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)

@@ -5,6 +5,7 @@
 //        -I../../genome-minimizer-2_amd/csrc stamp_gemm.hip -o stamp_gemm
 // Run:   ./stamp_gemm M N K pk qk      (pk/qk: operand K-major 1 / MN-major 0; random bf16 data)
 #include "../../genome-minimizer-2_amd/csrc/gemm.hip"
+#include "../../genome-minimizer-2_amd/csrc/options.hip"
 
 #include <algorithm>
 #include <cstdio>
@@ -42,16 +43,16 @@ int main(int argc, char** argv) {
   for (int rep = 0; rep < 5; ++rep) launch_gemm_store<bf16_t>(g, pl.splits, C, nullptr, 0, N, 0, nullptr, nullptr);
   hipDeviceSynchronize();
   const int tiles = (Mp / pl.tile) * (Np / pl.tile) * pl.splits;
-  std::vector<unsigned long long> st((size_t)16384 * 4);
+  std::vector<unsigned long long> st((size_t)16384 * 8);
   hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_stamp), st.size() * 8);
   unsigned long long t0 = ~0ull, tend = 0;
   for (int b = 0; b < tiles; ++b) {
-    t0 = std::min(t0, st[b * 4]);
-    tend = std::max(tend, st[b * 4 + 3]);
+    t0 = std::min(t0, st[b * 8]);
+    tend = std::max(tend, st[b * 8 + 3]);
   }
   std::vector<double> skew, pro, loop, epi;
   for (int b = 0; b < tiles; ++b) {
-    const unsigned long long* s = &st[b * 4];
+    const unsigned long long* s = &st[b * 8];
     skew.push_back((s[0] - t0) * 0.01);
     pro.push_back((s[1] - s[0]) * 0.01);
     loop.push_back((s[2] - s[1]) * 0.01);
