@@ -96,9 +96,10 @@ def parse():
     ap.add_argument("--input-chunks", type=int, choices=[1, 4], default=None,
                     help="input-layer weight-gradient launches (default: 4 under DDP, else 1)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5-shaped (G=20,000) step line")
-    ap.add_argument("--defer-adam", type=int, default=None,
+    ap.add_argument("--defer-adam", type=int, default=1,
                     help="output layer's Adam update launched beside the next step's hidden layers on this many "
-                         "workgroups per CU, 0 = not deferred (GM2_OPT_DEFER_OUTPUT_ADAM; bit-identical)")
+                         "workgroups per CU, 0 = not deferred (GM2_OPT_DEFER_OUTPUT_ADAM; bit-identical; default 1: "
+                         "3.34 -> 3.25 ms/step, profiles/r03_schedule_ab.txt)")
     ap.add_argument("--dw9-last", type=int, choices=[0, 1], default=None,
                     help="output-layer weight gradient beside the input-layer one (GM2_OPT_DW9_LAST)")
     ap.add_argument("--side-priority", type=int, choices=[-1, 0, 1], default=None,

@@ -320,6 +320,10 @@ class VAETrainer:
         rec = torch.zeros(max(nb, 1), native.LOSS_SLOTS, dtype=torch.float64, device=self.device)
         sync = self._grad_sync(dist) if dist else None
         sync_bn = dist is not None and self.sync_bn
+        # one process: the output layer's Adam update runs beside the next batch's hidden layers
+        # (GM2_OPT_DEFER_OUTPUT_ADAM, bit-identical; the loop below joins it before touching the
+        # gradient buffer itself and at the end of the epoch)
+        ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, 0 if dist else 1)
         if sync:
             sync.prepare(ws)
         if sync_bn:
@@ -338,6 +342,7 @@ class VAETrainer:
                 # DDP only: a global batch of fewer than 2 rows per rank runs on its first n // 2
                 # ranks (every row is still trained, each active rank with >= 2 rows for train-mode
                 # BatchNorm); this rank contributes a zero gradient and zero loss sums
+                ws.join()  # (a deferred update still reads the gradient buffer)
                 self.grads.zero_()
             if sync:
                 sync.after_backward(ws, ran)
