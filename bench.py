@@ -53,7 +53,7 @@ def decode_flops_per_genome(G, H, L):
 DEFAULTS = dict(batch=4096, genes=55039, hidden=1024, latent=64, precision="bf16")
 
 
-def pmc_traffic(a, kernel_prefix):
+def pmc_traffic(a, kernel_prefix, grid=None):
     """HBM bytes per launch of `kernel_prefix` from the newest committed PMC summary
     (profiles/rNN_pmc_traffic.json, written by tools/pmc.py from separate FETCH_SIZE / WRITE_SIZE
     rocprofv3 passes of this same command). Only valid for the default workload; else None."""
@@ -63,7 +63,8 @@ def pmc_traffic(a, kernel_prefix):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
     if not files:
         return None, None
-    rows = [r for r in json.load(open(files[-1]))["kernels"] if r["kernel"].startswith(kernel_prefix)]
+    rows = [r for r in json.load(open(files[-1]))["kernels"] if r["kernel"].startswith(kernel_prefix)
+            and (grid is None or r["grid"] == grid)]
     if not rows:
         return None, None
     return rows[0]["traffic_bytes"], os.path.relpath(files[-1], ROOT)
@@ -315,7 +316,7 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
     return elapsed, k_ms, k_n, info
 
 
-def roofline_entry(a, prec, G, H, B, k_ms, k_n, traffic_key=None):
+def roofline_entry(a, prec, G, H, B, k_ms, k_n):
     """Output-layer loss GEMM [B,H]x[H,G] + fused BCE/dlogits epilogue against the MFMA roofline:
     achieved = 2*B*H*G FLOP per launch / its average live-timed launch duration."""
     from gm2 import native
@@ -323,7 +324,9 @@ def roofline_entry(a, prec, G, H, B, k_ms, k_n, traffic_key=None):
     k_flops = 2.0 * B * H * G
     achieved = k_flops / (k_avg_ms * 1e-3) / 1e12
     peak = PEAK_BF16_TFLOPS if prec == native.GM2_BF16 else PEAK_F32_TFLOPS
-    traffic, traffic_src = pmc_traffic(a, "k_gemm_recon_loss") if traffic_key is None else (None, None)
+    # (the launch's grid: one 512-thread workgroup per 256x256 genes x strains tile)
+    grid = ((G + 255) // 256) * ((B + 255) // 256) * 512 if prec == native.GM2_BF16 else None
+    traffic, traffic_src = pmc_traffic(a, "k_gemm_recon_loss", grid)
     return {"bound": "mfma", "kernel": "k_gemm_recon_loss<bf16>" if prec == native.GM2_BF16
             else "k_gemm_recon_loss<f32>", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
@@ -393,7 +396,7 @@ def main():
                                  f"20,000 over 8), batch {B}/GPU", "value": round(v5, 1), "unit": "strain-vectors/s",
                      "n_gpus": world, "ms_per_step": round(el5 / a.steps * 1e3, 3),
                      "train_tflops": round(v5 * train_flops_per_vector(Gc, H, L) / 1e12, 2),
-                     "roofline": roofline_entry(a, prec, Gc, H, B, k5, n5, traffic_key="c5")}
+                     "roofline": roofline_entry(a, prec, Gc, H, B, k5, n5)}
     if rank == 0 and world == 1 and not a.no_f32_line:
         from gm2.data import ResidentMatrix
         other = native.GM2_F32 if prec == native.GM2_BF16 else native.GM2_BF16

@@ -30,30 +30,34 @@ def trace(d):
     return rows
 
 
-def counters(d):
+def counters(d, with_grid=False):
     out = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
         out[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
-        names[int(r["Dispatch_Id"])] = short(r["Kernel_Name"])
+        k = short(r["Kernel_Name"])
+        names[int(r["Dispatch_Id"])] = (k, int(r["Grid_Size"])) if with_grid else k
     return out, names
 
 
 def step_breakdown(tag, steps):
     rows = trace(f"gpurun_out/prof_{tag}")
     recon = [i for i, r in enumerate(rows) if "k_gemm_recon_loss" in r["Kernel_Name"]]
-    # the timed steps are the last `steps` recon launches; the window runs from the first timed
-    # step's first kernel (just after the previous step's last Adam) to the last Adam
+    # the timed steps of a C2-only run (bench.py --no-c5): from the `steps`-th last gather (a step's
+    # first kernel) to the end of the last Adam launch (the final join's deferred output-layer update)
+    gath = [i for i, r in enumerate(rows) if "k_gather" in r["Kernel_Name"]]
     adam = [i for i, r in enumerate(rows) if "k_adam_fused" in r["Kernel_Name"]]
-    lo = adam[-steps - 1] + 1
+    lo = gath[-steps]
     hi = adam[-1] + 1
     agg = collections.defaultdict(lambda: [0, 0.0])
+    grids = {}
     for r in rows[lo:hi]:
         k = short(r["Kernel_Name"])
         agg[k][0] += 1
         agg[k][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
+        grids.setdefault(k, int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1) * int(r.get("Grid_Size_Z", 1) or 1))
     wall = (int(rows[hi - 1]["End_Timestamp"]) - int(rows[lo]["Start_Timestamp"])) * 1e-3 / steps
-    return wall, {k: (v[0] / steps, v[1] / steps) for k, v in agg.items()}, len(recon)
+    return wall, {k: (v[0] / steps, v[1] / steps) for k, v in agg.items()}, grids
 
 
 def mfma(tag):
@@ -74,7 +78,7 @@ def traffic(tag):
     out = {}
     for kind, scale in (("fetch", 2.0), ("write", 1.0)):
         try:
-            c, names = counters(f"gpurun_out/pmc_{kind}_{tag}")
+            c, names = counters(f"gpurun_out/pmc_{kind}_{tag}", with_grid=True)
         except FileNotFoundError:
             continue
         per = collections.defaultdict(list)
@@ -86,14 +90,14 @@ def traffic(tag):
 
 
 def main(tag, dst=None, steps=6):
-    wall, brk, _ = step_breakdown(tag, steps)
+    wall, brk, grids = step_breakdown(tag, steps)
     util = mfma(tag)
     tr = traffic(tag)
     rows = []
-    print(f"step wall (first kernel start -> last Adam end): {wall:.1f} us")
+    print(f"step wall (a step's gather -> the last Adam end, per step): {wall:.1f} us")
     for k, (n, us) in sorted(brk.items(), key=lambda kv: -kv[1][1]):
         u = util.get(k, (None, 0))[0]
-        t = tr.get(k, {})
+        t = tr.get((k, grids.get(k)), {})
         rows.append({"kernel": k, "launches_per_step": n, "us_per_step": round(us, 1),
                      "mfma_busy": None if u is None else round(u, 4),
                      "fetch_bytes": t.get("fetch"), "write_bytes": t.get("write")})
