@@ -101,6 +101,8 @@ def parse():
                     help="output layer's Adam update launched beside the next step's hidden layers on this many "
                          "workgroups per CU, 0 = not deferred (GM2_OPT_DEFER_OUTPUT_ADAM; bit-identical; default 1: "
                          "3.34 -> 3.25 ms/step, profiles/r03_schedule_ab.txt)")
+    ap.add_argument("--no-zero-copy", action="store_true",
+                    help="gather each step's rows instead of reading the resident operands in place")
     ap.add_argument("--dw9-last", type=int, choices=[0, 1], default=None,
                     help="output-layer weight gradient beside the input-layer one (GM2_OPT_DW9_LAST)")
     ap.add_argument("--side-priority", type=int, choices=[-1, 0, 1], default=None,
@@ -261,16 +263,20 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         ws.set_option(native.OPT_SIDE_PRIORITY, a.side_priority)
     if a.dw9_last is not None:
         ws.set_option(native.OPT_DW9_LAST, a.dw9_last)
-    # next-batch staging (gm2_batch.next) only under DDP, where the gather fills the wait for the
-    # input-layer exchange; on one GPU it measured ~30 us/step slower (profiles/r02_prefetch_ab_*)
-    prefetch = dist is not None and not a.no_prefetch
+    # zero-copy rows (gm2_batch.resident): the resident matrix's bf16 rows + target bits, built once
+    # before timing, read in place by each step's input-layer GEMMs and loss epilogue (no gather)
+    res = mat.operands(prec) if not a.no_zero_copy else None
+    # next-batch staging (gm2_batch.next) only under DDP without zero-copy rows, where the gather
+    # fills the wait for the input-layer exchange; on one GPU it measured ~30 us/step slower
+    # (profiles/r02_prefetch_ab_*)
+    prefetch = dist is not None and not a.no_prefetch and res is None
 
     def step(i):
         eps = torch.randn(B, L, device=dev)
         # the next step's rows are staged during this step's tail (gm2_batch.next; the last timed step
         # stages one batch nobody uses, so the timed region holds K gathers)
         nxt = native.make_batch(mat.data, mat.ld, rows[(i + 1) * B:(i + 2) * B], B, None) if prefetch else None
-        batch = native.make_batch(mat.data, mat.ld, rows[i * B:(i + 1) * B], B, eps, next=nxt)
+        batch = native.make_batch(mat.data, mat.ld, rows[i * B:(i + 1) * B], B, eps, next=nxt, resident=res)
         native.train_fwd_bwd(ws, batch, model.params, grads, model.bn, scal[i], loss[i])
         if sync is not None:
             sync.after_backward(ws)  # bucketed SUM all-reduce overlapped with the backward
@@ -310,7 +316,7 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
     info = {"prefetch": prefetch, "input_chunks": ws.get_option(native.OPT_INPUT_CHUNKS),
             "defer_adam": ws.get_option(native.OPT_DEFER_OUTPUT_ADAM),
             "side_priority": ws.get_option(native.OPT_SIDE_PRIORITY),
-            "dw9_last": ws.get_option(native.OPT_DW9_LAST),
+            "dw9_last": ws.get_option(native.OPT_DW9_LAST), "zero_copy": res is not None,
             "x": x if (rank == 0 and world == 1) else None, "mat": mat}
     del model, opt, ws, grads, sync
     return elapsed, k_ms, k_n, info
@@ -368,7 +374,8 @@ def main():
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": a.precision, "data": "synthetic",
         "config": {"workload": "C2: v0 train step (fwd+bwd+clip+Adam), synthetic pan-genome "
-                               f"{a.strains}x{G} u8 resident per GPU, batch {B}/GPU",
+                               f"{a.strains}x{G} u8 resident per GPU (+ its bf16 rows / target bits, read in place), "
+                               f"batch {B}/GPU",
                    "preset": "v0", "genes": G, "hidden": H, "latent": L, "global_batch": B * world,
                    "parallelism": f"dp{world}",
                    "grad_exchange": (f"{a.grad_exchange} (decoder.9 / encoder.0 weight buckets; rest f32), RCCL "
@@ -376,7 +383,8 @@ def main():
                                      f"{info['input_chunks']} launch(es)")
                    if world > 1 else "none (one GPU)",
                    "input_prefetch": info["prefetch"], "deferred_output_adam": info["defer_adam"],
-                   "side_priority": info["side_priority"], "dw9_last": info["dw9_last"]},
+                   "side_priority": info["side_priority"], "dw9_last": info["dw9_last"],
+                   "zero_copy_rows": info["zero_copy"]},
         "train_tflops": round(value * train_flops_per_vector(G, H, L) / 1e12, 2),
         "nonfinite_steps": 0,
         # dominant kernel: decoder output layer GEMM [B,H]x[H,G] + fused BCE/abundance/dlogits epilogue

@@ -97,6 +97,7 @@ struct Layout {
   int64_t X1, XB1;             // second input slot: the next batch's rows, staged under this step's tail
   int64_t syncb;               // SyncBN all-reduce vector: 2H + 2 doubles
   int64_t adamscal;            // scalar block of a queued output-layer Adam update
+  int64_t ridx;                // zero-copy rows: int32 [roundup(Bm, 256)] resident-matrix row per batch row
 };
 
 Layout make_layout(const gm2_dims* gd, int prec) {
@@ -159,6 +160,7 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.XB1 = take(Bm * (d.Gp / 32) * 4);
   o.syncb = take((2 * H + 2) * 8);
   o.adamscal = take(GM2_NUM_SCALARS * 4);
+  o.ridx = take(round_up(Bm, 2 * kTile) * 4);
   o.total = cur;
   return o;
 }
@@ -174,6 +176,13 @@ struct Ctx {
   int64_t slab_off, slab_cap;  // split-K scratch of this stream
   int64_t xo, xbo;             // input slot of this call: gathered rows X [Bm][Gp] (T), target bits
   WsState* st;                 // host-side state of the workspace
+  // zero-copy rows (gm2_batch.resident, training calls): the input layer's GEMMs and the loss
+  // epilogue read the resident matrix's rows through ridx [roundup(Bm, 256)] instead of X / XB
+  const int32_t* ridx = nullptr;
+  const T* xres = nullptr;
+  int64_t ld_xres = 0;
+  const uint32_t* xbres = nullptr;
+  int64_t ld_xbres = 0;
   Ctx(const Layout& l, void* w, void* strm, WsState* state = nullptr)
       : lo(l), ws((char*)w), s((hipStream_t)strm), d(l.d), slab_off(l.slabs), slab_cap(l.slab_cap), xo(l.X),
         xbo(l.XB), st(state) {}
@@ -183,6 +192,11 @@ struct Ctx {
     c.slab_cap = lo.side_cap;
     c.xo = xo;
     c.xbo = xbo;
+    c.ridx = ridx;
+    c.xres = xres;
+    c.ld_xres = ld_xres;
+    c.xbres = xbres;
+    c.ld_xbres = ld_xbres;
     return c;
   }
   T* t(int64_t off) const { return (T*)(ws + off); }
@@ -393,8 +407,9 @@ void bucket_bounds(const Dims& d, int64_t* lh) {
 // GEMM into the fp32 slab scratch (split-K slices summed by the consumer). Returns #slabs.
 template <typename T>
 int gemm_to_slabs(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64_t ldq, int Np, int M, int N,
-                  int K, int64_t ldc, int pk = 1, int qk = 1) {
+                  int K, int64_t ldc, int pk = 1, int qk = 1, const int32_t* prow = nullptr) {
   GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0, pk, qk};
+  g.prow = prow;
   const int S = plan_gemm<T>(g).splits;
   const int64_t slab = (int64_t)Mp * ldc;
   if ((int64_t)S * slab > c.slab_cap) throw Gm2Error("slab capacity exceeded");
@@ -405,8 +420,9 @@ int gemm_to_slabs(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, 
 // split over K into slabs and summed by k_slab_sum (deterministic order).
 template <typename T>
 void gemm_to(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64_t ldq, int Np, int M, int N, int K,
-             float* C0, float* C1, int msplit, int64_t ldc, int pk = 1, int qk = 1) {
+             float* C0, float* C1, int msplit, int64_t ldc, int pk = 1, int qk = 1, const int32_t* qrow = nullptr) {
   GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0, pk, qk};
+  g.qrow = qrow;
   int S = plan_gemm<T>(g).splits;
   const int64_t slab = round_up((int64_t)M * N, 4);
   if ((int64_t)S * slab > c.slab_cap) S = 1;
@@ -442,6 +458,11 @@ BigGrads<T> big_grads(const Ctx<T>& c, int Bp) {
   const int H = (int)c.d.H, G = (int)c.d.G, Gp = (int)c.d.Gp;
   BigGrads<T> r{{c.t(l.AT5), Bp, c.t(l.dL), Gp, H, G, Bp, H, Gp, 0, 1, 0},
                 {c.t(l.dYT0), Bp, c.t(c.xo), Gp, H, G, Bp, H, Gp, 0, 1, 0}, false, 0, 0};
+  if (c.ridx) {  // zero-copy rows: X's rows are the resident matrix's, through ridx
+    r.g0.Q = c.xres;
+    r.g0.ldq = c.ld_xres;
+    r.g0.qrow = c.ridx;
+  }
   r.direct = plan_gemm<T>(r.g9).splits == 1 && plan_gemm<T>(r.g0).splits == 1;
   r.n9 = gemm_tiles<T>(r.g9);
   r.n0 = gemm_tiles<T>(r.g0);
@@ -455,14 +476,14 @@ BigGrads<T> big_grads(const Ctx<T>& c, int Bp) {
 // tiles (statistics in the store epilogue); otherwise split-K slabs + k_bn_fwd_partial.
 template <typename T>
 void linear_pre_bn(const Ctx<T>& c, const T* in, int64_t ldin, int Bp, const T* W, int64_t ldw, int B, int H, int K,
-                   const float* bias, float* Y, float* part, bool stats) {
+                   const float* bias, float* Y, float* part, bool stats, const int32_t* prow = nullptr) {
   GemmArgs<T> g{in, ldin, W, ldw, B, H, K, Bp, H, 0};
   StoreEpi bn;
   bn.mode = stats ? 1 : 0;
   bn.part = (float2*)part;
   bn.ldp = H;
-  if (launch_gemm_bn<T>(g, Y, H, bias, bn, c.s)) return;
-  const int S = gemm_to_slabs<T>(c, in, ldin, Bp, W, ldw, H, B, H, K, H);
+  if (!prow && launch_gemm_bn<T>(g, Y, H, bias, bn, c.s)) return;
+  const int S = gemm_to_slabs<T>(c, in, ldin, Bp, W, ldw, H, B, H, K, H, 1, 1, prow);
   launch_bn_fwd_partial(c.f(c.slab_off), S, (int64_t)Bp * H, H, bias, B, H, Y, part, c.s);
 }
 
@@ -558,13 +579,17 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   double* syncb = (double*)(c.ws + l.syncb);
   const int Bp = (int)round_up(B, kTile);
   const int H = (int)d.H, L = (int)d.L;
-  // 1) strain rows -> X [Bp][Gp] (T) + bit-packed target (unless a previous training call staged them)
-  if (!staged)
+  // 1) strain rows -> X [Bp][Gp] (T) + bit-packed target (unless a previous training call staged
+  // them, or the call reads the resident matrix's rows in place: c.ridx)
+  if (c.ridx)
+    launch_resident_rows(b->rows, B, (int)round_up(d.Bm, 2 * kTile), b->resident_rows, const_cast<int32_t*>(c.ridx),
+                         c.s);
+  else if (!staged)
     launch_gather_rows<T>(b->data, b->ld_data, b->rows, B, (int)d.G, c.t(c.xo), d.Gp, (int)d.Gp, Bp,
                           (uint32_t*)(c.ws + c.xbo), d.Gp / 32, c.s);
   // 2) encoder blocks, heads + reparameterisation, decoder blocks (all NT GEMMs)
-  const T* in = c.t(c.xo);
-  int64_t ldin = d.Gp;
+  const T* in = c.ridx ? c.xres : c.t(c.xo);
+  int64_t ldin = c.ridx ? c.ld_xres : d.Gp;
   int Kin = (int)d.Gp;
   const int64_t shadow_in[6] = {l.sE0, l.sE1, l.sE2, l.sD0, l.sD1, l.sD2};
   for (int i = 0; i < 6; ++i) {
@@ -577,7 +602,7 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
       Kin = (int)d.Lp;
     }
     linear_pre_bn<T>(c, in, ldin, Bp, c.t(shadow_in[i]), i == 3 ? d.Lr : Kin, B, H, Kin, prm + d.off[kBlk[i][1]],
-                     c.f(l.Y[i]), c.f(l.bnpart), train != 0);
+                     c.f(l.Y[i]), c.f(l.bnpart), train != 0, i == 0 ? c.ridx : nullptr);
     // a queued output-layer Adam update of the previous step starts here, beside the hidden layers
     // (HBM-bound next to latency-bound small GEMMs; the gather and the input-layer GEMM before this
     // point leave it nothing: one is HBM-bound too, the other holds every CU's registers)
@@ -605,8 +630,12 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   // deferred output-layer Adam update of the previous step (side stream) must be complete here.
   if (c.st) c.st->join(c.s);
   GemmArgs<T> g{c.t(l.sD3), H, c.t(l.A[5]), H, (int)d.G, B, H, (int)d.Gp, Bp, 0};
-  launch_gemm_recon_loss<T>(g, prm + d.off[D9B], (const uint32_t*)(c.ws + c.xbo), d.Gp / 32, with_grad, scal, c.t(l.dL),
-                            d.Gp, c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
+  if (c.ridx)
+    launch_gemm_recon_loss<T>(g, prm + d.off[D9B], c.xbres, c.ld_xbres, with_grad, scal, c.t(l.dL), d.Gp,
+                              c.f(l.losspart), c.f(l.colpart), d.Gp, c.s, c.ridx);
+  else
+    launch_gemm_recon_loss<T>(g, prm + d.off[D9B], (const uint32_t*)(c.ws + c.xbo), d.Gp / 32, with_grad, scal,
+                              c.t(l.dL), d.Gp, c.f(l.losspart), c.f(l.colpart), d.Gp, c.s);
   int na_ok = 0, na_n = 0;
   if (norm_hdr) {  // the training call: record whether its backward takes the clip statistics
     const BigGrads<T> bg = big_grads<T>(c, Bp);
@@ -733,7 +762,8 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
         }
       } else {
         if (!bg.direct || !launch_gemm_sq<T>(bg.g0, gr + d.off[E0W], G, nasq + bg.n9, c.s))
-          gemm_to<T>(c, c.t(l.dYT0), Bp, H, c.t(c.xo), Gp, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0);
+          gemm_to<T>(c, c.t(l.dYT0), Bp, H, bg.g0.Q, bg.g0.ldq, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0,
+                     bg.g0.qrow);
         for (int q = 0; q < 4; ++q) HIP_OK(hipEventRecord(st.bucket[2 + q], c.s));
       }
       if (sr) st.order(w.s, c.s);  // join: the caller's stream sees every weight gradient
@@ -827,6 +857,24 @@ void sync_bn_no_rows(const Layout& lo, float* gr, float* bn, double* loss, void*
   st.recorded = true;
 }
 
+// gm2_batch.resident usable in place for this training call: its precision, padding and alignment,
+// and GEMM plans that take zero-copy rows (bf16 256x256 ping-pong); otherwise the rows are gathered
+template <typename T>
+bool zero_copy_ok(const Ctx<T>& c, const gm2_batch* b) {
+  const Dims& d = c.d;
+  if (!b->resident || b->resident_prec != c.lo.prec || sizeof(T) != 2) return false;
+  if (!b->resident_bits || b->resident_rows < 0 || b->resident_rows > INT32_MAX - 1) return false;
+  if (b->ld_resident < d.Gp || b->ld_resident % 64 || ((uintptr_t)b->resident & 15)) return false;
+  if (b->ld_resident_bits < d.Gp / 32 || b->ld_resident_bits % 4 || ((uintptr_t)b->resident_bits & 15)) return false;
+  const int B = (int)b->n, Bp = (int)round_up(B, kTile), H = (int)d.H;
+  if (B < 1 || Bp % (2 * kTile)) return false;
+  GemmArgs<T> enc{(const T*)b->resident, b->ld_resident, c.t(c.lo.sE0), d.Gp, B, H, (int)d.Gp, Bp, H, 0};
+  enc.prow = (const int32_t*)1;
+  GemmArgs<T> dwe0{c.t(c.lo.dYT0), Bp, (const T*)b->resident, b->ld_resident, H, (int)d.G, Bp, H, (int)d.Gp, 0, 1, 0};
+  dwe0.qrow = (const int32_t*)1;
+  return gemm_idx_ok<T>(enc) && gemm_idx_ok<T>(dwe0);
+}
+
 template <typename T>
 void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr, float* bn, const float* scal,
                double* loss, void* ws, void* strm, WsState& st) {
@@ -838,6 +886,17 @@ void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr
     return;
   }
   Ctx<T> c(lo, ws, strm, &st);
+  if (zero_copy_ok<T>(c, b)) {  // the resident matrix's rows in place: no gather, no staging
+    c.ridx = (const int32_t*)((char*)ws + lo.ridx);
+    c.xres = (const T*)b->resident;
+    c.ld_xres = b->ld_resident;
+    c.xbres = b->resident_bits;
+    c.ld_xbres = b->ld_resident_bits;
+    drop_stage(st, c.s);
+    forward<T>(c, b, prm, bn, 1, 1, scal, loss, gr, nullptr, 0, nullptr, 0.5f, true, false);
+    backward<T>(c, b, prm, gr, scal, nullptr, nullptr, 1, nullptr);
+    return;
+  }
   SlotState& ss = st.slot;
   const bool hit = ss.staged && ss.prec == lo.prec && ss.total == lo.total && ss.data == b->data &&
                    ss.ld == b->ld_data && ss.rows == b->rows && ss.n == b->n;
@@ -934,6 +993,43 @@ int gm2_sync_shadows(const gm2_dims* d, int prec, const float* params, void* ws,
       Ctx<bf16_t> c(lo, ws, stream, &st);
       launch_shadow_sync<bf16_t>(make_table(c), params, c.s);
     }
+  });
+}
+
+int gm2_resident_layout(int64_t S, int64_t G, int prec, int64_t* ld, int64_t* ld_bits, int64_t* rows_alloc,
+                        size_t* bytes, size_t* bits_bytes) {
+  return guarded([&] {
+    if (S < 0 || S > INT32_MAX - 64 || G <= 0 || (prec != GM2_F32 && prec != GM2_BF16))
+      throw Gm2Error("resident layout: S=%lld G=%lld prec=%d", (long long)S, (long long)G, prec);
+    const int64_t l = round_up(G, 2 * kTile), r = round_up(S + 1, 64);
+    *ld = l;
+    *ld_bits = l / 32;
+    *rows_alloc = r;
+    *bytes = (size_t)(r * l * (prec == GM2_F32 ? 4 : 2));
+    *bits_bytes = (size_t)(r * (l / 32) * 4);
+  });
+}
+
+int gm2_resident_build(const uint8_t* data, int64_t ld_data, int64_t S, int64_t G, int prec, void* out,
+                       uint32_t* bits, void* stream) {
+  return guarded([&] {
+    int64_t l = 0, lb = 0, r = 0;
+    size_t by = 0, bb = 0;
+    if (gm2_resident_layout(S, G, prec, &l, &lb, &r, &by, &bb) != 0) throw Gm2Error("%s", g_err.c_str());
+    if (!out || !bits || ((uintptr_t)out & 15) || ((uintptr_t)bits & 15)) throw Gm2Error("resident: null or misaligned output");
+    if (S > 0 && (!data || ld_data % 16 || ld_data < G || ((uintptr_t)data & 15)))
+      throw Gm2Error("resident: data rows must be 16-B aligned with ld_data (%lld) a multiple of 16 and >= G",
+                     (long long)ld_data);
+    // the gather with identity rows: rows < S copied (0/1 -> T, target bits), rows S.. r-1 and
+    // columns G.. ld-1 zero
+    const uint8_t* src = S > 0 ? data : (const uint8_t*)out;
+    const int64_t lds = S > 0 ? ld_data : 16;
+    if (prec == GM2_F32)
+      launch_gather_rows<float>(src, lds, nullptr, (int)S, (int)G, (float*)out, l, (int)l, (int)r, bits, lb,
+                                (hipStream_t)stream);
+    else
+      launch_gather_rows<bf16_t>(src, lds, nullptr, (int)S, (int)G, (bf16_t*)out, l, (int)l, (int)r, bits, lb,
+                                 (hipStream_t)stream);
   });
 }
 

@@ -309,10 +309,12 @@ constexpr int BUF = 4 * REGION;    // one K-tile: A0, A1, B0, B1
 __device__ __forceinline__ int a_row(int r, int a) { return (r >> 6) * 128 + a * 64 + (r & 63); }
 __device__ __forceinline__ int b_row(int r, int b) { return (r >> 5) * 64 + b * 32 + (r & 31); }
 
-// one half-tile: 1024 16-B chunks, 2 per thread (lane-linear LDS destination, swizzled source)
-template <bool KMAJ, bool ISA>
+// one half-tile: 1024 16-B chunks, 2 per thread (lane-linear LDS destination, swizzled source).
+// IDX (zero-copy rows): the thread's two rows (K-major) / k-rows (MN-major), j = 0, 1, are rr[j],
+// read from the tile's LDS index table ahead of the issuing phase (idx_rows below)
+template <bool KMAJ, bool ISA, bool IDX = false>
 __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ P, int64_t ld, int base, int half, int k0,
-                                           char* region, int tid) {
+                                           char* region, int tid, const int* rr = nullptr) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int i = j * 512 + tid;
@@ -321,14 +323,28 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ P, int64_t
       const int row = i >> 3;
       const int c = (i & 7) ^ ((row >> 1) & 7);
       const int g = ISA ? a_row(row, half) : b_row(row, half);
-      src = P + (int64_t)(base + g) * ld + k0 + c * 8;
+      const int64_t r = IDX ? (int64_t)rr[j] : (int64_t)(base + g);
+      src = P + r * ld + k0 + c * 8;
     } else {
       const int k = i >> 4;
       const int e = ((i & 15) ^ swz_mn(k)) * 8;
       const int g = ISA ? a_row(e, half) : b_row(e, half);
-      src = P + (int64_t)(k0 + k) * ld + base + g;
+      const int64_t r = IDX ? (int64_t)rr[j] : (int64_t)(k0 + k);
+      src = P + r * ld + base + g;
     }
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(region + (j * 512 + (tid & ~63)) * 16), 16, 0, 0);
+  }
+}
+
+// the table entries of the thread's two rows of a K-major half-tile (tile-local rows a_row(.)) or
+// of its two k-rows of an MN-major half-tile of K-tile t (table = the split's k-rows)
+template <bool KMAJ>
+__device__ __forceinline__ void idx_rows(const int* sidx, int half, int t, int tid, int (&rr)[2]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = j * 512 + tid;
+    if constexpr (KMAJ) rr[j] = sidx[a_row(i >> 3, half)];
+    else rr[j] = sidx[t * 64 + (i >> 4)];
   }
 }
 
@@ -339,10 +355,10 @@ __device__ __forceinline__ void barrier() {
 }
 }  // namespace pp
 
-template <bool AK, bool BK>
+template <bool AK, bool BK, int IDX = 0>
 __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_t ldp, const bf16_t* __restrict__ Q,
                                             int64_t ldq, int m0, int n0, int kbeg, int nk, char* smem,
-                                            f32x4 (&acc)[8][4]) {
+                                            f32x4 (&acc)[8][4], const int* sidx = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // wave-uniform in an SGPR: the stagger barriers below must be branched around, not exec-masked
   const int wm = __builtin_amdgcn_readfirstlane(wid >> 2), wn = wid & 3;
@@ -356,11 +372,19 @@ __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_
     const int off = h == 0 ? 0 : h == 3 ? 1 : h + 1;  // A0 0, A1 1, B0 2, B1 3
     return smem + (t & 1) * pp::BUF + off * pp::REGION;
   };
+  // zero-copy rows: IDX 1 = P's rows (the tile's A rows: fixed, held for the tile), IDX 2 = Q's
+  // k-rows (read one phase ahead of the two B-half issues of each K-tile, so the table read never
+  // waits behind the phase's fragment reads)
+  int ra0[2] = {0, 0}, ra1[2] = {0, 0}, rq[2] = {0, 0};
+  if constexpr (IDX == 1) {
+    pp::idx_rows<true>(sidx, 0, 0, tid, ra0);
+    pp::idx_rows<true>(sidx, 1, 0, tid, ra1);
+  }
   auto issue = [&](int t, int h) {
     const int k0 = kbeg + t * 64;
     char* r = region(t, h);
-    if (h == 0 || h == 3) pp::stage_half<AK, true>(P, ldp, m0, h == 0 ? 0 : 1, k0, r, tid);
-    else pp::stage_half<BK, false>(Q, ldq, n0, h == 1 ? 0 : 1, k0, r, tid);
+    if (h == 0 || h == 3) pp::stage_half<AK, true, IDX == 1>(P, ldp, m0, h == 0 ? 0 : 1, k0, r, tid, h == 0 ? ra0 : ra1);
+    else pp::stage_half<BK, false, IDX == 2>(Q, ldq, n0, h == 1 ? 0 : 1, k0, r, tid, rq);
   };
   bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
   auto read_a = [&](int t, int a) {
@@ -390,6 +414,7 @@ __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_
     __builtin_amdgcn_s_setprio(0);
   };
   // prologue: all four half-tiles of tile 0; A0, B0 retired before the first reads
+  if constexpr (IDX == 2) pp::idx_rows<false>(sidx, 0, 0, tid, rq);
 #pragma unroll
   for (int h = 0; h < 4; ++h) issue(0, h);
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -398,6 +423,9 @@ __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_
   if (wm == 1) pp::barrier();  // stagger: group 1 one barrier behind
   for (int t = 0; t < nk; ++t) {
     const bool more = t + 1 < nk;
+    if constexpr (IDX == 2) {
+      if (more) pp::idx_rows<false>(sidx, 0, t + 1, tid, rq);
+    }
     // phase 0: (a0, b0)
     read_a(t, 0);
     read_b(t, 0, fb0);
@@ -466,12 +494,14 @@ __device__ __forceinline__ double sq4(float a, float b, float c, float d) {
   return ((double)a * a + (double)b * b) + ((double)c * c + (double)d * d);
 }
 
-template <class C, typename T, bool AK, bool BK, bool PP>
+template <class C, typename T, bool AK, bool BK, bool PP, int IDX>
 __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g, float* __restrict__ C0,
                                            float* __restrict__ C1, int msplit, int64_t ldc, int64_t slab,
                                            const float* __restrict__ bias, const StoreEpi& bn, char* smem);
 
-template <class C, typename T, bool AK, bool BK, bool PP>
+// IDX (zero-copy rows, PP only): 1 = P's rows through g.prow, 2 = Q's k-rows through g.qrow; the
+// tile's slice of the index array sits in an LDS table after the staging ring
+template <class C, typename T, bool AK, bool BK, bool PP, int IDX = 0>
 __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __restrict__ C0, float* __restrict__ C1,
                                                     int msplit, int64_t ldc, int64_t slab,
                                                     const float* __restrict__ bias, StoreEpi bn) {
@@ -479,7 +509,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
   GM2_STAMP(0);
   const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
   if (bn.ntiles == 0) {  // one tile per workgroup
-    store_tile<C, T, AK, BK, PP>(tile_of<C>(tm, tn), g, C0, C1, msplit, ldc, slab, bias, bn, smem);
+    store_tile<C, T, AK, BK, PP, IDX>(tile_of<C>(tm, tn), g, C0, C1, msplit, ldc, slab, bias, bn, smem);
     return;
   }
   // capped grid (one K pass): workgroup wg takes logical tiles wg, wg + grid, ... (every wave of
@@ -487,12 +517,12 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
   const int ntile = tm * tn;
   for (int t = xcd_wg(); t < bn.ntiles; t += gridDim.x) {
     __syncthreads();
-    store_tile<C, T, AK, BK, PP>(tile_at<C>(t % ntile, tm, tn, t / ntile), g, C0, C1, msplit, ldc, slab, bias, bn,
-                                 smem);
+    store_tile<C, T, AK, BK, PP, IDX>(tile_at<C>(t % ntile, tm, tn, t / ntile), g, C0, C1, msplit, ldc, slab, bias,
+                                      bn, smem);
   }
 }
 
-template <class C, typename T, bool AK, bool BK, bool PP>
+template <class C, typename T, bool AK, bool BK, bool PP, int IDX>
 __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g, float* __restrict__ C0,
                                            float* __restrict__ C1, int msplit, int64_t ldc, int64_t slab,
                                            const float* __restrict__ bias, const StoreEpi& bn, char* smem) {
@@ -500,10 +530,20 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
   const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = (kend - kbeg) / E<T>::KT;
   f32x4 acc[C::FM][C::FN];
-  if constexpr (PP)
-    mainloop_pp<AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
-  else
+  if constexpr (PP) {
+    int* sidx = (int*)(smem + C::LDS);
+    if constexpr (IDX == 1) {
+      for (int i = threadIdx.x; i < C::BM; i += C::NT) sidx[i] = g.prow[tl.m0 + i];
+      __syncthreads();
+    } else if constexpr (IDX == 2) {
+      for (int i = threadIdx.x; i < kend - kbeg; i += C::NT) sidx[i] = g.qrow[kbeg + i];
+      __syncthreads();
+    }
+    mainloop_pp<AK, BK, IDX>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc, sidx);
+  } else {
+    static_assert(IDX == 0, "zero-copy rows: ping-pong main loop only");
     mainloop<C, T, AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
+  }
   GM2_STAMP(2);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   float* Cz = C0 + (int64_t)tl.split * slab;
@@ -738,7 +778,8 @@ __device__ __forceinline__ float bfi(int m, float a, float b) {
 template <class C, typename T, bool FAST, bool WG, bool GRAD>
 __device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], const uint32_t* __restrict__ xrow,
                                            int64_t ldxb, const float* bias_s, int N, int n0, int wm, int wn, int q,
-                                           int c, float wgam, T* img, float& bce, float& psum) {
+                                           int c, float wgam, T* img, float& bce, float& psum,
+                                           const int* xidx) {
   constexpr int PR = C::BM + 8;
   constexpr int XW = C::WTM / 32;  // target words of this wave's gene span per strain row
   static_assert(XW == 4 || XW == 2, "wave gene span");
@@ -750,7 +791,8 @@ __device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], con
     const int sl = wn * C::WTN + ni * 16 + c;  // strain (tile-local)
     const bool sok = n0 + sl < N;
     uint32_t xw[XW];
-    const uint32_t* xp = xrow + (int64_t)(n0 + sl) * ldxb;
+    // (zero-copy rows: the strain's row of the resident target bits, from the tile's LDS table)
+    const uint32_t* xp = xrow + (int64_t)(xidx ? xidx[sl] : n0 + sl) * ldxb;
     if (sok) {
       if constexpr (XW == 4) {
         const uint4 v = *(const uint4*)xp;
@@ -841,7 +883,7 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
                                                 const uint32_t* __restrict__ xbits, int64_t ldxb,
                                                 const float* __restrict__ scal, T* __restrict__ dL, int64_t ldd,
                                                 float* __restrict__ loss_part, float* __restrict__ colpart,
-                                                int64_t ldcol, char* smem);
+                                                int64_t ldcol, char* smem, const int32_t* __restrict__ xrows);
 
 // ntiles > 0: capped grid, workgroup wg takes tiles wg, wg + grid, ... (GM2_OPT_GRID_CAP bit 4)
 template <class C, typename T, bool PP, bool GRAD>
@@ -850,19 +892,19 @@ __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const 
                                                          int ntiles, const float* __restrict__ scal,
                                                          T* __restrict__ dL, int64_t ldd,
                                                          float* __restrict__ loss_part, float* __restrict__ colpart,
-                                                         int64_t ldcol) {
+                                                         int64_t ldcol, const int32_t* __restrict__ xrows) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   GM2_STAMP(0);
   const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
   if (ntiles == 0) {
     recon_loss_tile<C, T, PP, GRAD>(tile_of<C>(tm, tn), g, bias, xbits, ldxb, scal, dL, ldd, loss_part, colpart,
-                                    ldcol, smem);
+                                    ldcol, smem, xrows);
     return;
   }
   for (int t = xcd_wg(); t < ntiles; t += gridDim.x) {
     __syncthreads();
     recon_loss_tile<C, T, PP, GRAD>(tile_at<C>(t, tm, tn, 0), g, bias, xbits, ldxb, scal, dL, ldd, loss_part,
-                                    colpart, ldcol, smem);
+                                    colpart, ldcol, smem, xrows);
   }
 }
 
@@ -871,7 +913,7 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
                                                 const uint32_t* __restrict__ xbits, int64_t ldxb,
                                                 const float* __restrict__ scal, T* __restrict__ dL, int64_t ldd,
                                                 float* __restrict__ loss_part, float* __restrict__ colpart,
-                                                int64_t ldcol, char* smem) {
+                                                int64_t ldcol, char* smem, const int32_t* __restrict__ xrows) {
   constexpr bool FAST = sizeof(T) == 2;
   // (m = genes, n = strains)
   // LDS: [0, image / staging) | per-row-group dl sums | BCE, sum(p) slots | bias slice
@@ -883,10 +925,13 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
   float* colred = (float*)(smem + IMG);  // [RG][BM]
   float* red = colred + RG * C::BM;     // [2][32]
   float* bias_s = red + 64;             // [BM]
+  int* xidx = (int*)(bias_s + C::BM);   // [BN] zero-copy strain rows of the target bits
   for (int i = threadIdx.x; i < C::BM; i += C::NT) {
     const float b = tl.m0 + i < g.M ? bias[tl.m0 + i] : 0.f;
     bias_s[i] = FAST ? b * -1.4426950408889634f : b;
   }
+  if (xrows)
+    for (int i = threadIdx.x; i < C::BN; i += C::NT) xidx[i] = xrows[tl.n0 + i];
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP)
     mainloop_pp<true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
@@ -902,10 +947,10 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
   // branch between the two element loops
   if (wgam != 0.f)
     recon_tile<C, T, FAST, true, GRAD>(acc, xbits + ((tl.m0 + wm * C::WTM) >> 5), ldxb, bias_s, g.N, tl.n0, wm, wn, q,
-                                       c, wgam, img, bce, psum);
+                                       c, wgam, img, bce, psum, xrows ? xidx : nullptr);
   else
     recon_tile<C, T, FAST, false, GRAD>(acc, xbits + ((tl.m0 + wm * C::WTM) >> 5), ldxb, bias_s, g.N, tl.n0, wm, wn,
-                                        q, c, wgam, img, bce, psum);
+                                        q, c, wgam, img, bce, psum, xrows ? xidx : nullptr);
   if constexpr (FAST) bce *= -0.6931471805599453f;
   GM2_STAMP(4);
   if constexpr (GRAD) {
@@ -976,7 +1021,7 @@ template <class C, typename T>
 constexpr int recon_lds_bytes() {
   constexpr int img = std::max<int>(C::LDS, C::BN * (C::BM + 8) * (int)sizeof(T));
   constexpr int rg = C::NT / (C::BM / (16 / (int)sizeof(T)));
-  return img + (rg * C::BM + 64 + C::BM) * 4;
+  return img + (rg * C::BM + 64 + C::BM + C::BN) * 4;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1234,10 +1279,15 @@ static int device_cus() {
   return cus[dev] = std::max(n, 1);
 }
 
-template <class C, typename T, bool AK, bool BK, bool PP>
+template <class C, typename T, bool AK, bool BK, bool PP, int IDX = 0>
 static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
                            const float* bias, const StoreEpi& bn, hipStream_t s) {
-  ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP>, C::LDS);
+  // (zero-copy rows: the index table after the staging ring -- a tile's rows, or a split's k-rows)
+  constexpr int table_max = IDX == 1 ? C::BM * 4 : IDX == 2 ? kMaxIdxRows * 4 : 0;
+  static_assert(C::LDS + table_max <= 160 * 1024, "LDS budget");
+  const int lds = C::LDS + (IDX == 1 ? C::BM * 4 : IDX == 2 ? a.k_per_split * 4 : 0);
+  if (IDX == 2 && a.k_per_split > kMaxIdxRows) throw Gm2Error("zero-copy rows: %d k-rows per split", a.k_per_split);
+  ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP, IDX>, C::LDS + table_max);
   int grid = tiles;
   StoreEpi ep = bn;
   if (bn.ntiles) {  // capped grid: the same number of rounds on fewer CUs
@@ -1245,7 +1295,7 @@ static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1
     grid = (tiles + rounds - 1) / rounds;
     ep.ntiles = grid < tiles ? tiles : 0;
   }
-  hipLaunchKernelGGL((k_gemm_store<C, T, AK, BK, PP>), dim3(grid), dim3(C::NT), C::LDS, s, a, C0, C1 ? C1 : C0,
+  hipLaunchKernelGGL((k_gemm_store<C, T, AK, BK, PP, IDX>), dim3(grid), dim3(C::NT), lds, s, a, C0, C1 ? C1 : C0,
                      C1 ? msplit : (1 << 30), ldc, slab, bias, ep);
 }
 
@@ -1253,8 +1303,19 @@ template <class C, typename T, bool AK, bool BK>
 static void store_launch(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
                          const float* bias, const StoreEpi& bn, hipStream_t s) {
   if constexpr (std::is_same_v<C, Big> && sizeof(T) == 2) {
+    if (a.prow || a.qrow) {  // zero-copy rows: the input layer's two GEMMs (gemm_idx_ok checked)
+      if (!pp_enabled()) throw Gm2Error("zero-copy rows need the ping-pong main loop");
+      if constexpr (AK && BK) {
+        if (a.prow && !a.qrow) return store_launch_k<C, T, AK, BK, true, 1>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+      }
+      if constexpr (AK && !BK) {
+        if (a.qrow && !a.prow) return store_launch_k<C, T, AK, BK, true, 2>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+      }
+      throw Gm2Error("zero-copy rows: layout not instantiated");
+    }
     if (pp_enabled()) return store_launch_k<C, T, AK, BK, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
   }
+  if (a.prow || a.qrow) throw Gm2Error("zero-copy rows: bf16 256x256 tiles only");
   store_launch_k<C, T, AK, BK, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
 }
 
@@ -1370,7 +1431,7 @@ int gemm_recon_row_tiles(const GemmArgs<T>& g) {  // strain tiles (rows of colpa
 template <class C, typename T, bool PP>
 static void recon_impl_k(const GemmArgs<T>& g, const float* bias, const uint32_t* X, int64_t ldx, int with_grad,
                          const float* scal, T* dL, int64_t ldd, float* loss_part, float* colpart, int64_t ldcol,
-                         hipStream_t s) {
+                         hipStream_t s, const int32_t* xrows) {
   check_gemm(g, C::BM);
   if (ldx * 32 < g.Mp || (ldx & 3)) throw Gm2Error("recon: target bit rows too short");
   constexpr int lds = recon_lds_bytes<C, T>();
@@ -1385,7 +1446,7 @@ static void recon_impl_k(const GemmArgs<T>& g, const float* bias, const uint32_t
   auto go = [&](auto kern) {
     ensure_lds_attr((const void*)kern, lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(C::NT), lds, s, g, bias, X, ldx, ntiles, scal, dL, ldd, loss_part,
-                       colpart, ldcol);
+                       colpart, ldcol, xrows);
   };
   if (with_grad) go(k_gemm_recon_loss<C, T, PP, true>);
   else go(k_gemm_recon_loss<C, T, PP, false>);
@@ -1394,12 +1455,12 @@ static void recon_impl_k(const GemmArgs<T>& g, const float* bias, const uint32_t
 template <class C, typename T>
 static void recon_impl(const GemmArgs<T>& g, const float* bias, const uint32_t* X, int64_t ldx, int with_grad,
                        const float* scal, T* dL, int64_t ldd, float* loss_part, float* colpart, int64_t ldcol,
-                       hipStream_t s) {
+                       hipStream_t s, const int32_t* xrows) {
   if constexpr (std::is_same_v<C, Big> && sizeof(T) == 2) {
     if (pp_enabled())
-      return recon_impl_k<C, T, true>(g, bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol, s);
+      return recon_impl_k<C, T, true>(g, bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol, s, xrows);
   }
-  recon_impl_k<C, T, false>(g, bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol, s);
+  recon_impl_k<C, T, false>(g, bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol, s, xrows);
 }
 
 // the fp32 parity path stays on the 128-tile (a 256-row fp32 dL image would not fit the LDS).
@@ -1418,17 +1479,28 @@ static bool recon_big(const GemmArgs<T>& g) {
 template <typename T>
 void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const uint32_t* X, int64_t ldx, int with_grad,
                             const float* scal, T* dL, int64_t ldd, float* loss_part, float* colpart, int64_t ldcol,
-                            hipStream_t s) {
+                            hipStream_t s, const int32_t* xrows) {
   TimedLaunch tl(kKcReconLoss, s);
   bool done = false;
   if constexpr (sizeof(T) == 2) {
     if (recon_big(g)) {
-      recon_impl<Big, T>(g, bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol, s);
+      recon_impl<Big, T>(g, bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol, s, xrows);
       done = true;
     }
   }
-  if (!done) recon_impl<Small, T>(g, bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol, s);
+  if (!done) recon_impl<Small, T>(g, bias, X, ldx, with_grad, scal, dL, ldd, loss_part, colpart, ldcol, s, xrows);
   GM2_CHECK_LAUNCH();
+}
+
+template <typename T>
+bool gemm_idx_ok(const GemmArgs<T>& g) {
+  if (sizeof(T) != 2 || !pp_enabled()) return false;
+  const GemmPlan p = plan_gemm<T>(g);
+  if (p.tile != 256) return false;
+  if (!g.qrow) return true;  // (P rows: one 256-row table per tile)
+  const int nkt = g.K / E<T>::KT, splits = std::max(1, std::min(p.splits, nkt));
+  const int kps = (int)(round_up(nkt, splits) / splits) * E<T>::KT;
+  return kps <= kMaxIdxRows;  // (Q k-rows: a split's k-rows in the table)
 }
 
 template <typename T>
@@ -1457,7 +1529,9 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
   template int gemm_recon_row_tiles<T>(const GemmArgs<T>&);                                                     \
   template GemmPlan plan_gemm<T>(const GemmArgs<T>&);                                                          \
   template void launch_gemm_recon_loss<T>(const GemmArgs<T>&, const float*, const uint32_t*, int64_t, int,        \
-                                          const float*, T*, int64_t, float*, float*, int64_t, hipStream_t);
+                                          const float*, T*, int64_t, float*, float*, int64_t, hipStream_t,      \
+                                          const int32_t*);                                                      \
+  template bool gemm_idx_ok<T>(const GemmArgs<T>&);
 GM2_INST(float)
 GM2_INST(bf16_t)
 #undef GM2_INST

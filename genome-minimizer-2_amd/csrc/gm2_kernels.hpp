@@ -64,6 +64,11 @@ struct GemmArgs {
   int Mp, Np;    // padded M / N extents covered by the operand buffers (multiples of 128)
   int k_per_split;
   int pk = 1, qk = 1;
+  // zero-copy batch rows (bf16 256x256 ping-pong plans only; GemmPlan must be tile 256): P's rows
+  // (K-major P) or Q's k-rows (MN-major Q) are rows prow[m] / qrow[k] of the operand buffer instead
+  // of m / k -- the input layer's GEMMs read the resident matrix's rows in place (gm2_batch.resident)
+  const int32_t* prow = nullptr;
+  const int32_t* qrow = nullptr;
 };
 
 // ---- tuning options (gm2.h GM2_OPT_*): results are bit-identical under every value ----
@@ -171,7 +176,12 @@ GemmPlan plan_gemm(const GemmArgs<T>& g);
 template <typename T>
 void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const uint32_t* xbits, int64_t ldxb, int with_grad,
                             const float* scal, T* dL, int64_t ldd, float* loss_part, float* colpart, int64_t ldcol,
-                            hipStream_t s);
+                            hipStream_t s, const int32_t* xrows = nullptr);
+// whether a GEMM with zero-copy rows (GemmArgs.prow / qrow) runs as planned: bf16, ping-pong main
+// loop on, the 256x256 plan (and for qrow at most kMaxIdxRows k-rows per split)
+constexpr int kMaxIdxRows = 8192;
+template <typename T>
+bool gemm_idx_ok(const GemmArgs<T>& g);
 // output layer + threshold (sampling / metrics): u8 mask, packed bits, probs, per-row (TP, FP, FN)
 template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs,
@@ -183,6 +193,9 @@ constexpr int kBnRowChunk = 128;  // rows per BatchNorm partial-statistics chunk
 
 // gather strain rows of the resident u8 matrix into X [Bp][ldx] (T), plus the row-major bit-packed
 // target [Bp][ldxb words] (bit g%32 of word g/32 of row b = X[b][g]) that the reconstruction-loss
+// zero-copy rows: ridx[i] = rows[i] (or i when rows is null) for i < n, the resident matrix's zero
+// row S for n <= i < nfill
+void launch_resident_rows(const int32_t* rows, int n, int nfill, int64_t S, int32_t* ridx, hipStream_t s);
 // epilogue reads; zero-fills columns >= G and rows >= B up to the padded extents
 template <typename T>
 void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* rows, int B, int G, T* X, int64_t ldx,

@@ -1074,6 +1074,18 @@ void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* row
   GM2_CHECK_LAUNCH();
 }
 
+__global__ __launch_bounds__(256) void k_resident_rows(const int32_t* __restrict__ rows, int n, int nfill, int zero_row,
+                                                     int32_t* __restrict__ ridx) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < nfill) ridx[i] = i < n ? (rows ? rows[i] : i) : zero_row;
+}
+
+void launch_resident_rows(const int32_t* rows, int n, int nfill, int64_t S, int32_t* ridx, hipStream_t s) {
+  if (n > nfill || S < 0 || S > INT32_MAX) throw Gm2Error("resident rows: n=%d fill=%d S=%lld", n, nfill, (long long)S);
+  hipLaunchKernelGGL(k_resident_rows, dim3((nfill + 255) / 256), dim3(256), 0, s, rows, n, nfill, (int)S, ridx);
+  GM2_CHECK_LAUNCH();
+}
+
 void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, const float* bias, int B, int H,
                            float* Y, float* part, hipStream_t s) {
   if (H % 64) throw Gm2Error("bn: H %% 64");

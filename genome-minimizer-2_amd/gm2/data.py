@@ -43,6 +43,15 @@ class ResidentMatrix:
         buf[: self.n, : self.G] = t.cpu()
         self.data = buf.to(device)
 
+    def operands(self, prec):
+        """The matrix as GEMM operands for `prec` (native.ResidentOperands), built on first use and
+        kept: training steps then read their rows in place instead of gathering them."""
+        from . import native
+        cache = self.__dict__.setdefault("_operands", {})
+        if prec not in cache:
+            cache[prec] = native.ResidentOperands(self.data, self.ld, self.n, self.G, prec)
+        return cache[prec]
+
     def __len__(self):
         return self.n
 

@@ -32,8 +32,9 @@ EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_of
            "gm2_gemm", "gm2_grad_bucket_bounds", "gm2_wait_grad_bucket", "gm2_set_option", "gm2_get_option",
            "gm2_workspace_set_option", "gm2_workspace_get_option", "gm2_workspace_release",
            "gm2_workspace_set_collective", "gm2_workspace_join",
+           "gm2_resident_layout", "gm2_resident_build",
            "gm2_timing_begin", "gm2_timing_end"]
-ABI_VERSION = 3
+ABI_VERSION = 4
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
 OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE, OPT_SMALL_SPLIT, OPT_BN_EPILOGUE, OPT_SMALL_WAVES = 1, 2, 3, 4, 5, 6
 OPT_INPUT_CHUNKS, OPT_SMALL_STAGES, OPT_GRID_CAP, OPT_SYNC_BN, OPT_DEFER_OUTPUT_ADAM = 7, 8, 9, 10, 11
@@ -51,7 +52,9 @@ class Batch(C.Structure):
 
 
 Batch._fields_ = [("data", C.c_void_p), ("ld_data", C.c_int64), ("rows", C.c_void_p), ("n", C.c_int64),
-                  ("eps", C.c_void_p), ("next", C.POINTER(Batch))]
+                  ("eps", C.c_void_p), ("next", C.POINTER(Batch)),
+                  ("resident", C.c_void_p), ("ld_resident", C.c_int64), ("resident_bits", C.c_void_p),
+                  ("ld_resident_bits", C.c_int64), ("resident_rows", C.c_int64), ("resident_prec", C.c_int)]
 
 
 _lib = None
@@ -100,6 +103,9 @@ def lib():
         "gm2_workspace_release": (C.c_int, [vp]),
         "gm2_workspace_set_collective": (C.c_int, [vp, ALLREDUCE_FN, vp]),
         "gm2_workspace_join": (C.c_int, [vp, vp]),
+        "gm2_resident_layout": (C.c_int, [i64, i64, i32, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                           C.POINTER(C.c_int64), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+        "gm2_resident_build": (C.c_int, [vp, i64, i64, i64, i32, vp, vp, vp]),
         "gm2_timing_begin": (C.c_int, [i32]),
         "gm2_timing_end": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     }
@@ -216,9 +222,29 @@ class Workspace:
                 pass
 
 
-def make_batch(data, ld, rows, n, eps, next: "Batch | None" = None) -> Batch:
+class ResidentOperands:
+    """The resident matrix as GEMM operands (gm2_resident_build): T rows [S + 1 ...][ld] with a zero
+    row S and zero pad columns, and their packed target bits [..][ld_bits]; training calls read the
+    batch's rows in place through gm2_batch.resident (no per-step gather)."""
+
+    def __init__(self, data, ld_data, S, G, prec):
+        ld, ldb, rows = C.c_int64(), C.c_int64(), C.c_int64()
+        nb, nbb = C.c_size_t(), C.c_size_t()
+        check(lib().gm2_resident_layout(int(S), int(G), prec, C.byref(ld), C.byref(ldb), C.byref(rows), C.byref(nb),
+                                        C.byref(nbb)), "gm2_resident_layout")
+        dt = torch.float32 if prec == GM2_F32 else torch.bfloat16
+        self.rows_t = torch.empty(rows.value, ld.value, dtype=dt, device=data.device)
+        self.bits = torch.empty(rows.value, ldb.value, dtype=torch.int32, device=data.device)
+        self.ld, self.ld_bits, self.S, self.prec = ld.value, ldb.value, int(S), prec
+        check(lib().gm2_resident_build(data.data_ptr(), int(ld_data), int(S), int(G), prec, self.rows_t.data_ptr(),
+                                       self.bits.data_ptr(), stream()), "gm2_resident_build")
+
+
+def make_batch(data, ld, rows, n, eps, next: "Batch | None" = None,
+               resident: "ResidentOperands | None" = None) -> Batch:
     """`next` (training only): the batch the following train_fwd_bwd on the same workspace gets; its
-    rows are gathered during this step's tail (gm2_batch.next). Keep its tensors unchanged until then."""
+    rows are gathered during this step's tail (gm2_batch.next). Keep its tensors unchanged until then.
+    `resident` (training only): the same matrix as ResidentOperands, read in place (no gather)."""
     b = Batch(data.data_ptr(), int(ld), None if rows is None else rows.data_ptr(), int(n),
               None if eps is None else eps.data_ptr())
     # the tensors the descriptor points at stay alive as long as it does (a staged `next` batch is
@@ -227,6 +253,14 @@ def make_batch(data, ld, rows, n, eps, next: "Batch | None" = None) -> Batch:
     if next is not None:
         b.next = C.pointer(next)
         b._keep_next = next
+    if resident is not None:
+        b.resident = resident.rows_t.data_ptr()
+        b.ld_resident = resident.ld
+        b.resident_bits = resident.bits.data_ptr()
+        b.ld_resident_bits = resident.ld_bits
+        b.resident_rows = resident.S
+        b.resident_prec = resident.prec
+        b._keep_res = resident
     return b
 
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GM2_ABI_VERSION 3
+#define GM2_ABI_VERSION 4
 #define GM2_NUM_PARAMS 30 /* tensors in model.parameters() */
 #define GM2_NUM_SCALARS 16
 
@@ -62,6 +62,19 @@ typedef struct gm2_batch {
    * (data, rows) must stay unchanged until that call; eps is not read. Any other call that gathers
    * rows (eval, encode, forward, recon counts) first waits for and discards a pending stage. */
   const struct gm2_batch* next;
+  /* optional (ABI 4): the resident matrix as GEMM operands, built once by gm2_resident_build from
+   * the same data. When set (resident_prec = the workspace precision) gm2_train_fwd_bwd reads the
+   * batch's rows IN PLACE: the input-layer GEMMs take rows resident[rows[i]] of the [S + 1][ld]
+   * matrix and the loss epilogue the matching target-bit rows, so no rows are gathered (next is
+   * then not staged). Used when the plans allow it (bf16 workspace, 256x256 tiles, rows padded to a
+   * multiple of 256, ld_resident >= the workspace's padded G); otherwise the call gathers from
+   * data as before. Other calls always gather. Zero-initialised (NULL) = not used. */
+  const void* resident;          /* T [resident_rows + 1 (zero row) ...][ld_resident], pad columns zero */
+  int64_t ld_resident;           /* elements, multiple of 64 */
+  const uint32_t* resident_bits; /* [...][ld_resident_bits] packed target bits (bit g % 32 of word g / 32) */
+  int64_t ld_resident_bits;      /* 32-bit words, multiple of 4 */
+  int64_t resident_rows;         /* S: the data rows; row S of both arrays is all zero */
+  int resident_prec;             /* GM2_F32 / GM2_BF16: the element type of `resident` */
 } gm2_batch;
 
 /* device scalar block (fp32[GM2_NUM_SCALARS]) read by the kernels, written by the host per step
@@ -113,6 +126,15 @@ int gm2_workspace_release(void* ws);
 /* Re-derive the padded GEMM copies of the Linear weights from `params` (after init,
  * load_state_dict, or any host-side edit). gm2_adam_step keeps them current itself. */
 int gm2_sync_shadows(const gm2_dims* d, int precision, const float* params, void* ws, void* stream);
+
+/* Resident-matrix operands (gm2_batch.resident), built once from the 0/1 u8 rows data [S][ld_data]:
+ * gm2_resident_layout gives the element pitch ld (roundup(G, 256)), the bit-row pitch ld_bits
+ * (ld / 32 words), the row count to allocate (roundup(S + 1, 64): row S and beyond are zero) and the
+ * byte sizes of the two arrays; gm2_resident_build fills them (T = float or bf16 by prec). */
+int gm2_resident_layout(int64_t S, int64_t G, int prec, int64_t* ld, int64_t* ld_bits, int64_t* rows_alloc,
+                        size_t* bytes, size_t* bits_bytes);
+int gm2_resident_build(const uint8_t* data, int64_t ld_data, int64_t S, int64_t G, int prec, void* out,
+                       uint32_t* bits, void* stream);
 
 /* Training forward + backward of one batch (replaces trainer.py:110-118: model(data),
  * compute_total_loss, total_loss.backward()). Overwrites `grads` with the data-term gradient

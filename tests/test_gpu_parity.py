@@ -507,6 +507,67 @@ def test_backward_schedule_options_bit_identical(G):
         assert float(o[1][4]) == pytest.approx(float(outs[0][1][4]), rel=1e-6)
 
 
+@pytest.mark.parametrize("G,B,rows_none", [(16384, 1024, False), (20000, 1000, False), (16384, 1024, True)])
+def test_zero_copy_rows_bit_identical(G, B, rows_none):
+    """gm2_batch.resident (ABI 4): a bf16 training call reads its rows in place from the resident
+    operands (gm2_resident_build) -- the input-layer GEMM's rows, the input-layer weight gradient's
+    k-rows and the loss epilogue's target bits through the batch's row indices -- instead of
+    gathering them. To prove the in-place path ran, the batch's u8 `data` is a DIFFERENT matrix (all
+    zeros) than the one the resident operands were built from: three steps (fwd+bwd, clip
+    statistics, Adam) must still equal, bit for bit, the gathering run on the resident's own matrix,
+    including a ragged batch (1000 rows: pad rows read the zero row) and rows = NULL (first n rows)."""
+    H, L = 1024, 32
+    S = 2 * B + 5
+    P, Sb = perturb_bn(*oracle_state(G, H, L, G + B + 3), seed=61)
+    X = synth_x(S, G, 62)
+    gen = torch.Generator().manual_seed(63)
+    rows = [None if rows_none else torch.randperm(S, generator=gen)[:B].to(torch.int32).cuda() for _ in range(3)]
+    eps = [torch.randn(B, L, generator=gen).cuda() for _ in range(3)]
+    outs = []
+    for zero_copy in (False, True):
+        m = to_model(P, Sb, G, H, L, native.GM2_BF16)
+        mat = ResidentMatrix(X)
+        res = mat.operands(native.GM2_BF16) if zero_copy else None
+        data = torch.zeros_like(mat.data) if zero_copy else mat.data
+        ws = m.workspace(native.GM2_BF16, B)
+        grads = torch.zeros_like(m.params)
+        mom, vel = torch.zeros_like(m.params), torch.zeros_like(m.params)
+        out = []
+        for i in range(3):
+            sc = scalars(beta=0.37, wgamma=0.55, lam=0.01, step=i + 1)
+            sc[native.S_NORM_AHEAD] = 1.0
+            loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+            batch = native.make_batch(data, mat.ld, rows[i], B, eps[i], resident=res)
+            native.train_fwd_bwd(ws, batch, m.params, grads, m.bn, sc, loss)
+            native.grad_norm(ws, m.params, grads, sc, loss)
+            out += [grads.clone(), loss.clone()]
+            native.adam_step(ws, m.params, grads, mom, vel, sc)
+        ws.join()
+        torch.cuda.synchronize()
+        outs.append(out + [m.params.clone(), m.bn.clone(), mom.clone(), vel.clone()])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_resident_operands_match_the_matrix():
+    """gm2_resident_build: rows < S are the 0/1 matrix in bf16 / f32 with zero pad columns up to
+    ld = roundup(G, 256), row S (and the allocation's tail) zero, and the packed bits match numpy
+    packbits(bitorder='little') of each row."""
+    G, S = 1000, 77
+    X = synth_x(S, G, 64)
+    mat = ResidentMatrix(X)
+    for prec, dt in ((native.GM2_BF16, torch.bfloat16), (native.GM2_F32, torch.float32)):
+        r = mat.operands(prec)
+        assert r.ld == 1024 and r.rows_t.dtype == dt and r.rows_t.shape[0] >= S + 1
+        full = r.rows_t.float().cpu().numpy()
+        np.testing.assert_array_equal(full[:S, :G], X.astype(np.float32))
+        assert not full[:S, G:].any() and not full[S:].any()
+        bits = r.bits.cpu().numpy().view(np.uint8)
+        want = np.packbits(X.astype(np.uint8), axis=1, bitorder="little")
+        np.testing.assert_array_equal(bits[:S, :want.shape[1]], want)
+        assert not bits[:S, want.shape[1]:].any() and not bits[S:].any()
+
+
 def test_two_workspaces_keep_their_own_options_and_state():
     """ABI 3: tuning options, side stream, gradient-bucket events and the staged input slot belong to
     the workspace. Two models trained interleaved in one process, one with the ping-pong main loop,

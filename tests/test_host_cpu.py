@@ -32,12 +32,13 @@ def test_header_constants_match_binding():
     """The ctypes mirror (gm2/native.py) uses the values include/gm2.h defines: ABI version, gradient
     bucket count, option keys, the gm2_batch field order (ABI 2 adds `next`); option setters accept
     and reject values without a GPU, and the bucket bounds tile the gradient buffer in order. ABI 3:
-    options and bucket events are per workspace; a workspace libgm2 never initialised is refused."""
+    options and bucket events are per workspace; a workspace libgm2 never initialised is refused.
+    ABI 4: gm2_batch gains the resident-operand fields; gm2_resident_layout sizes them."""
     import ctypes
     from gm2 import native
     txt = open(os.path.join(ROOT, "include", "gm2.h")).read()
     assert int(re.search(r"#define GM2_ABI_VERSION (\d+)", txt).group(1)) == native.lib().gm2_abi_version() \
-        == native.ABI_VERSION == 3
+        == native.ABI_VERSION == 4
     bogus = ctypes.c_void_p(0x1000)
     v = ctypes.c_int()
     assert native.lib().gm2_workspace_set_option(bogus, native.OPT_GRID_CAP, 1) != 0
@@ -49,7 +50,22 @@ def test_header_constants_match_binding():
     opts = dict((k, int(v)) for k, v in re.findall(r"GM2_OPT_([A-Z_]+) = (\d+)", txt))
     for k, v in opts.items():
         assert getattr(native, "OPT_" + k) == v, k
-    assert [f[0] for f in native.Batch._fields_] == ["data", "ld_data", "rows", "n", "eps", "next"]
+    assert [f[0] for f in native.Batch._fields_] == ["data", "ld_data", "rows", "n", "eps", "next", "resident",
+                                                     "ld_resident", "resident_bits", "ld_resident_bits",
+                                                     "resident_rows", "resident_prec"]
+    # (the header's struct fields, in order)
+    body = re.search(r"typedef struct gm2_batch \{(.*?)\} gm2_batch;", txt, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = re.findall(r"(\w+);", body)
+    assert fields == [f[0] for f in native.Batch._fields_]
+    ld, ldb, rows = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    nb, nbb = ctypes.c_size_t(), ctypes.c_size_t()
+    assert native.lib().gm2_resident_layout(10000, 55039, native.GM2_BF16, ctypes.byref(ld), ctypes.byref(ldb),
+                                            ctypes.byref(rows), ctypes.byref(nb), ctypes.byref(nbb)) == 0
+    assert (ld.value, ldb.value, rows.value) == (55040, 1720, 10048)
+    assert nb.value == 10048 * 55040 * 2 and nbb.value == 10048 * 1720 * 4
+    assert native.lib().gm2_resident_layout(-1, 5, native.GM2_BF16, ctypes.byref(ld), ctypes.byref(ldb),
+                                            ctypes.byref(rows), ctypes.byref(nb), ctypes.byref(nbb)) != 0
     native.set_option(native.OPT_INPUT_CHUNKS, 4)
     assert native.get_option(native.OPT_INPUT_CHUNKS) == 4
     native.set_option(native.OPT_INPUT_CHUNKS, 1)

@@ -45,7 +45,7 @@ def step_breakdown(tag, steps):
     recon = [i for i, r in enumerate(rows) if "k_gemm_recon_loss" in r["Kernel_Name"]]
     # the timed steps of a C2-only run (bench.py --no-c5): from the `steps`-th last gather (a step's
     # first kernel) to the end of the last Adam launch (the final join's deferred output-layer update)
-    gath = [i for i, r in enumerate(rows) if "k_gather" in r["Kernel_Name"]]
+    gath = [i for i, r in enumerate(rows) if "k_gather" in r["Kernel_Name"] or "k_resident_rows" in r["Kernel_Name"]]
     adam = [i for i, r in enumerate(rows) if "k_adam_fused" in r["Kernel_Name"]]
     lo = gath[-steps]
     hi = adam[-1] + 1

@@ -7,7 +7,7 @@ import sys
 
 rows = list(csv.DictReader(open(f"gpurun_out/prof_{sys.argv[1]}/run_kernel_trace.csv")))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-gath = [i for i, r in enumerate(rows) if "k_gather" in r["Kernel_Name"]]
+gath = [i for i, r in enumerate(rows) if "k_gather" in r["Kernel_Name"] or "k_resident_rows" in r["Kernel_Name"]]
 lo, hi = gath[-2], gath[-1]
 t0 = int(rows[lo]["Start_Timestamp"])
 
