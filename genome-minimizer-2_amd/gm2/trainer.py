@@ -328,6 +328,9 @@ class VAETrainer:
             sync.prepare(ws)
         if sync_bn:
             enable_sync_bn(dist, ws)
+        # bf16: the matrix's bf16 rows and target bits, built once and read in place by each step
+        # (gm2_batch.resident: no per-batch gather)
+        res = mat.operands(model.precision) if model.precision == native.GM2_BF16 else None
         for bi, rows in enumerate(batches):
             n = rows.shape[0]
             # SyncBN: plain contiguous slices (a rank may get 0 or 1 rows: the statistics are the
@@ -336,7 +339,7 @@ class VAETrainer:
             eps = self._eps(n)[lo:hi].contiguous()
             ran = hi > lo or sync_bn
             if ran:
-                batch = native.make_batch(mat.data, mat.ld, rows[lo:hi], hi - lo, eps)
+                batch = native.make_batch(mat.data, mat.ld, rows[lo:hi], hi - lo, eps, resident=res)
                 native.train_fwd_bwd(ws, batch, model.params, self.grads, model.bn, scal[bi], rec[bi])
             else:
                 # DDP only: a global batch of fewer than 2 rows per rank runs on its first n // 2
