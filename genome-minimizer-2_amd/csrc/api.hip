@@ -1074,9 +1074,8 @@ int gm2_adam_step(const gm2_dims* d, int prec, float* params, const float* grads
       }
       // every tensor but the output layer now; decoder.9.{weight,bias} (the table's last two
       // entries, half the bytes at v0) queued with a copy of the scalar block (see WsState::kick)
-      launch_adam_fused<T>(table_range(all, 0, all.n - 2), grads, params, m, v, scalars, clip, c.s);
       float* qs = (float*)((char*)ws + lo.adamscal);
-      HIP_OK(hipMemcpyAsync(qs, scalars, GM2_NUM_SCALARS * 4, hipMemcpyDeviceToDevice, c.s));
+      launch_adam_fused<T>(table_range(all, 0, all.n - 2), grads, params, m, v, scalars, clip, c.s, 0, qs);
       WsState::QueuedAdam& q = st.qadam;
       q.queued = true;
       q.prec = prec;

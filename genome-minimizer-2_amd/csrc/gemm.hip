@@ -810,6 +810,7 @@ __device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], con
     for (int k = 0; k < XW; ++k) xw[k] >>= 4 * q;
     T* irow = img + sl * PR + wm * C::WTM + 4 * q;
     float bce_c = 0.f, ps_c = 0.f;
+    f32x2_t bce2 = {0.f, 0.f}, ps2 = {0.f, 0.f};  // (FAST: pairs of elements)
     // the tile's bias slice sits in LDS (zero beyond G; pre-scaled by -log2 e on the FAST path);
     // slice mi + 1 is read while slice mi is computed
     const float* bsl = bias_s + wm * C::WTM + 4 * q;
@@ -820,6 +821,33 @@ __device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], con
       if (mi + 1 < C::FM) b4n = *(const float4*)(bsl + (mi + 1) * 16);
       const float bn[4] = {b4.x, b4.y, b4.z, b4.w};
       float dl4[4];
+      if constexpr (FAST) {
+        // two elements per step in packed fp32 (v_pk_fma / v_pk_add / v_pk_mul: the register pairs
+        // of the accumulator and the bias), the transcendentals, bit-field selects and clamps per
+        // element; the same operations in the same order as one element at a time
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x2_t a2 = {acc[mi][ni][2 * h], acc[mi][ni][2 * h + 1]};
+          const f32x2_t b2 = {bn[2 * h], bn[2 * h + 1]};
+          const f32x2_t y2 = a2 * f32x2_t{-1.4426950408889634f, -1.4426950408889634f} + b2;  // -l log2 e
+          const f32x2_t d2 = f32x2_t{__builtin_amdgcn_exp2f(y2.x), __builtin_amdgcn_exp2f(y2.y)} + 1.0f;
+          const f32x2_t p2 = {__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y)};
+          const f32x2_t nomp2 = p2 - 1.0f;  // -(1 - p)
+          const int msk0 = __builtin_amdgcn_sbfe((int)xw[mi >> 1], (mi & 1) * 16 + 2 * h, 1);  // x ? -1 : 0
+          const int msk1 = __builtin_amdgcn_sbfe((int)xw[mi >> 1], (mi & 1) * 16 + 2 * h + 1, 1);
+          const float l0 = fmaxf(__builtin_amdgcn_logf(fabsf(bfi(msk0, p2.x, nomp2.x))), -144.26950408889634f);
+          const float l1 = fmaxf(__builtin_amdgcn_logf(fabsf(bfi(msk1, p2.y, nomp2.y))), -144.26950408889634f);
+          bce2 += f32x2_t{l0, l1};  // max(log2, -100/ln 2)
+          ps2 += p2;
+          const f32x2_t r2 = {bfi(msk0, nomp2.x, p2.x), bfi(msk1, nomp2.y, p2.y)};  // p - x
+          const f32x2_t q2 = nomp2 * f32x2_t{-1e12f, -1e12f} * p2;
+          const f32x2_t s2 = {__builtin_amdgcn_fmed3f(q2.x, 0.0f, 1.0f), __builtin_amdgcn_fmed3f(q2.y, 0.0f, 1.0f)};
+          f32x2_t dl2 = r2 * s2;
+          if constexpr (WG) dl2 = f32x2_t{-wgam, -wgam} * (nomp2 * p2) + dl2;
+          dl4[2 * h] = dl2.x;
+          dl4[2 * h + 1] = dl2.y;
+        }
+      } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if constexpr (FAST) {
@@ -847,6 +875,7 @@ __device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], con
           dl4[j] = dp * omp * p;
         }
       }
+      }
       if constexpr (GRAD) {
         if constexpr (sizeof(T) == 2) {
           uint2 pk;
@@ -857,6 +886,10 @@ __device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], con
           *(f32x4*)(irow + mi * 16) = f32x4{dl4[0], dl4[1], dl4[2], dl4[3]};
         }
       }
+    }
+    if constexpr (FAST) {
+      bce_c = bce2.x + bce2.y;
+      ps_c = ps2.x + ps2.y;
     }
     if (sok) {
       bce += bce_c;

@@ -286,7 +286,7 @@ void launch_shadow_sync(const TensorTable& tt, const float* params, hipStream_t 
 // workgroups (each then loops over blocks)
 template <typename T>
 void launch_adam_fused(const TensorTable& tt, const float* grads, float* params, float* m, float* v, const float* scal,
-                       const float* clip, hipStream_t s, int max_grid = 0);
+                       const float* clip, hipStream_t s, int max_grid = 0, float* scal_copy = nullptr);
 // sum((g + lambda*sign(p))^2) and sum(|p|) over all params -> partials; then finalize
 // Clip-norm statistics taken in the GEMM epilogues of the training call (StoreEpi::sq): hdr[0] = 1
 // when both big weight gradients (input layer [lo0, hi0), output layer [lo9, hi9) of the flat

@@ -734,7 +734,9 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_adam_fused(TensorTable tt, const float* __restrict__ g, float* __restrict__ p,
                                                   float* __restrict__ m, float* __restrict__ v,
                                                   const float* __restrict__ scal, const float* __restrict__ clip,
-                                                  int64_t nblocks) {
+                                                  int64_t nblocks, float* __restrict__ scal_copy) {
+  // (a copy of the scalar block for a queued update that runs after the caller's block is gone)
+  if (scal_copy && blockIdx.x == 0 && threadIdx.x < kNumScal) scal_copy[threadIdx.x] = scal[threadIdx.x];
   int ti = 0;
   for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
     while (ti + 1 < tt.n && blk >= tt.t[ti + 1].tile0) ++ti;
@@ -1206,14 +1208,14 @@ void launch_shadow_sync(const TensorTable& tt, const float* params, hipStream_t 
 
 template <typename T>
 void launch_adam_fused(const TensorTable& tt, const float* grads, float* params, float* m, float* v, const float* scal,
-                       const float* clip, hipStream_t s, int max_grid) {
+                       const float* clip, hipStream_t s, int max_grid, float* scal_copy) {
   const TensorDesc& last = tt.t[tt.n - 1];
   const int64_t blocks = last.tile0 + (last.rows * last.cols + 4095) / 4096;
   for (int i = 0; i < tt.n; ++i)
     if (tt.t[i].off % 4) throw Gm2Error("adam: tensor offset not 16-B aligned");
   const int64_t grid = max_grid > 0 ? std::min<int64_t>(blocks, max_grid) : blocks;
   hipLaunchKernelGGL(k_adam_fused<T>, dim3((unsigned)grid), dim3(256), 0, s, tt, grads, params, m, v, scal, clip,
-                     blocks);
+                     blocks, scal_copy);
   GM2_CHECK_LAUNCH();
 }
 
@@ -1260,7 +1262,7 @@ void launch_grad_finalize(const double* part, int nblocks, const float* scal, fl
                                        hipStream_t, const double*);                                             \
   template void launch_transpose<T>(const T*, int64_t, int, int, T*, int64_t, hipStream_t);                    \
   template void launch_adam_fused<T>(const TensorTable&, const float*, float*, float*, float*, const float*,    \
-                                     const float*, hipStream_t, int);
+                                     const float*, hipStream_t, int, float*);
 GM2_INST(float)
 GM2_INST(bf16_t)
 #undef GM2_INST
