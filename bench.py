@@ -105,6 +105,9 @@ def parse():
                     help="gather each step's rows instead of reading the resident operands in place")
     ap.add_argument("--dw9-last", type=int, choices=[0, 1], default=None,
                     help="output-layer weight gradient beside the input-layer one (GM2_OPT_DW9_LAST)")
+    ap.add_argument("--tail-split", type=int, choices=[0, 1, 2, 3], default=None,
+                    help="split the short last tile round of the weight-gradient GEMMs: bit 1 dW9, bit 2 dWe0 "
+                         "(GM2_OPT_TAIL_SPLIT)")
     ap.add_argument("--side-priority", type=int, choices=[-1, 0, 1], default=None,
                     help="priority of the workspace's side stream (GM2_OPT_SIDE_PRIORITY)")
     ap.add_argument("--c5-strains", type=int, default=12500,
@@ -262,6 +265,8 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         ws.set_option(native.OPT_SIDE_PRIORITY, a.side_priority)
     if a.dw9_last is not None:
         ws.set_option(native.OPT_DW9_LAST, a.dw9_last)
+    if a.tail_split is not None:
+        ws.set_option(native.OPT_TAIL_SPLIT, a.tail_split)
     # zero-copy rows (gm2_batch.resident): the resident matrix's bf16 rows + target bits, built once
     # before timing, read in place by each step's input-layer GEMMs and loss epilogue (no gather)
     res = mat.operands(prec) if not a.no_zero_copy else None
@@ -315,7 +320,8 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
     info = {"prefetch": prefetch, "input_chunks": ws.get_option(native.OPT_INPUT_CHUNKS),
             "defer_adam": ws.get_option(native.OPT_DEFER_OUTPUT_ADAM),
             "side_priority": ws.get_option(native.OPT_SIDE_PRIORITY),
-            "dw9_last": ws.get_option(native.OPT_DW9_LAST), "zero_copy": res is not None,
+            "dw9_last": ws.get_option(native.OPT_DW9_LAST), "tail_split": ws.get_option(native.OPT_TAIL_SPLIT),
+            "zero_copy": res is not None,
             "x": x if (rank == 0 and world == 1) else None, "mat": mat}
     del model, opt, ws, grads, sync
     return elapsed, k_ms, k_n, info
@@ -383,6 +389,7 @@ def main():
                    if world > 1 else "none (one GPU)",
                    "input_prefetch": info["prefetch"], "deferred_output_adam": info["defer_adam"],
                    "side_priority": info["side_priority"], "dw9_last": info["dw9_last"],
+                   "tail_split": info["tail_split"],
                    "zero_copy_rows": info["zero_copy"]},
         "train_tflops": round(value * train_flops_per_vector(G, H, L) / 1e12, 2),
         "nonfinite_steps": 0,

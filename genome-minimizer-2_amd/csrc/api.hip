@@ -98,6 +98,10 @@ struct Layout {
   int64_t syncb;               // SyncBN all-reduce vector: 2H + 2 doubles
   int64_t adamscal;            // scalar block of a queued output-layer Adam update
   int64_t ridx;                // zero-copy rows: int32 [roundup(Bm, 256)] resident-matrix row per batch row
+  // split-tail scratch of the two one-pass weight-gradient GEMMs (GM2_OPT_TAIL_SPLIT): tile parts
+  // (fp32) and arrival counters (zero from gm2_workspace_init; each launch leaves them zero)
+  int64_t tailp9, tailc9, tailp0, tailc0;
+  int tails;
 };
 
 Layout make_layout(const gm2_dims* gd, int prec) {
@@ -161,6 +165,13 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.syncb = take((2 * H + 2) * 8);
   o.adamscal = take(GM2_NUM_SCALARS * 4);
   o.ridx = take(round_up(Bm, 2 * kTile) * 4);
+  // (only where those GEMMs can have more 256x256 tiles than a chip has CUs)
+  const bool tails = prec == GM2_BF16 && (H / 256) * (d.Gp / 256) > 256;
+  o.tails = tails ? 1 : 0;
+  o.tailp9 = take(tails ? kTailPartBytes : 0);
+  o.tailc9 = take(tails ? kTailCntBytes : 0);
+  o.tailp0 = take(tails ? kTailPartBytes : 0);
+  o.tailc0 = take(tails ? kTailCntBytes : 0);
   o.total = cur;
   return o;
 }
@@ -201,6 +212,8 @@ struct Ctx {
   }
   T* t(int64_t off) const { return (T*)(ws + off); }
   float* f(int64_t off) const { return (float*)(ws + off); }
+  float* tail_part(int64_t off) const { return lo.tails ? (float*)(ws + off) : nullptr; }
+  int* tail_cnt(int64_t off) const { return lo.tails ? (int*)(ws + off) : nullptr; }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -691,7 +704,8 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       // (A5^T here on the side stream; on the main stream before the fork measured ~35 us/step
       // slower, profiles/r02_a5t_placement_ab.txt)
       launch_transpose<T>(c.t(l.A[5]), H, Bp, H, c.t(l.AT5), Bp, w.s);
-      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, w.s, bg.direct ? nasq : nullptr);
+      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, w.s, bg.direct ? nasq : nullptr, c.tail_part(l.tailp9),
+                           c.tail_cnt(l.tailc9));
     } else {
       gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
     }
@@ -761,7 +775,8 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
           HIP_OK(hipEventRecord(st.bucket[2 + q], c.s));
         }
       } else {
-        if (!bg.direct || !launch_gemm_sq<T>(bg.g0, gr + d.off[E0W], G, nasq + bg.n9, c.s))
+        if (!bg.direct || !launch_gemm_sq<T>(bg.g0, gr + d.off[E0W], G, nasq + bg.n9, c.s, false,
+                                             c.tail_part(l.tailp0), c.tail_cnt(l.tailc0)))
           gemm_to<T>(c, c.t(l.dYT0), Bp, H, bg.g0.Q, bg.g0.ldq, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0,
                      bg.g0.qrow);
         for (int q = 0; q < 4; ++q) HIP_OK(hipEventRecord(st.bucket[2 + q], c.s));

@@ -497,7 +497,65 @@ __device__ __forceinline__ double sq4(float a, float b, float c, float d) {
 template <class C, typename T, bool AK, bool BK, bool PP, int IDX>
 __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g, float* __restrict__ C0,
                                            float* __restrict__ C1, int msplit, int64_t ldc, int64_t slab,
-                                           const float* __restrict__ bias, const StoreEpi& bn, char* smem);
+                                           const float* __restrict__ bias, const StoreEpi& bn, char* smem,
+                                           int tj = -1, int part = 0);
+
+// Split tail (StoreEpi::tail_S > 1): part `part` of tail tile tj has its K-part's accumulators in
+// acc. Every part stores them (lane-linear, 16-B per lane, coalesced) into its slot and counts
+// itself in; the last to arrive sums the slots in part order -- its own from registers -- into
+// acc, resets the tile's counter for the next launch and returns true (it runs the epilogue); the
+// others return false. No workgroup waits on another. The parts may run on different XCDs (L2s
+// not coherent with each other): the slots move through system-coherent (sc1) buffer stores /
+// loads, the stores drained before the count -- no cache-wide writeback or invalidate, which would
+// cost every other workgroup on the XCD its cached operands.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+constexpr int kSc1 = 16;  // buffer instruction cache policy: sc1
+
+template <class C>
+__device__ __forceinline__ bool tail_join(f32x4 (&acc)[C::FM][C::FN], const StoreEpi& bn, int tj, int part,
+                                          char* smem) {
+  constexpr int NF = C::FM * C::FN;
+  const int S = bn.tail_S;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(bn.tail_part, 0, 0x7fffffff, 0x00020000);
+  // byte offset of fragment f of part q's slot for this thread
+  auto off = [&](int q, int f) { return ((tj * S + q) * NF + f) * C::NT * 16 + (int)threadIdx.x * 16; };
+#pragma unroll
+  for (int mi = 0; mi < C::FM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < C::FN; ++ni)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[mi][ni]), rs, off(part, mi * C::FN + ni),
+                                             0, kSc1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = (int*)smem;  // (the staging LDS is free after the main loop)
+  if (threadIdx.x == 0)
+    *flag = __hip_atomic_fetch_add(bn.tail_cnt + tj, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int arrived = *flag;
+  if (arrived != S - 1) return false;
+  auto ld = [&](int q, int f) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off(q, f), 0, kSc1));
+  };
+  if (S == 2) {  // one other part: a + b == b + a, so either order is part order
+    const int other = part ^ 1;
+#pragma unroll
+    for (int mi = 0; mi < C::FM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < C::FN; ++ni) acc[mi][ni] = acc[mi][ni] + ld(other, mi * C::FN + ni);
+  } else {
+#pragma unroll
+    for (int mi = 0; mi < C::FM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < C::FN; ++ni) {
+        f32x4 sum = part == 0 ? acc[mi][ni] : ld(0, mi * C::FN + ni);
+        for (int q = 1; q < S; ++q) sum = sum + (q == part ? acc[mi][ni] : ld(q, mi * C::FN + ni));
+        acc[mi][ni] = sum;
+      }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(bn.tail_cnt + tj, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return true;
+}
 
 // IDX (zero-copy rows, PP only): 1 = P's rows through g.prow, 2 = Q's k-rows through g.qrow; the
 // tile's slice of the index array sits in an LDS table after the staging ring
@@ -508,6 +566,22 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
   extern __shared__ __attribute__((aligned(16))) char smem[];
   GM2_STAMP(0);
   const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
+  if constexpr (std::is_same_v<C, Big>) {
+    if (bn.tail_S > 1) {  // split tail: one item per workgroup, whole tiles first (see StoreEpi)
+      // XCD-aware order within each dispatch round of tail_cus workgroups, rounds in launch order,
+      // so the tail parts are the last round
+      const int base = (blockIdx.x / bn.tail_cus) * bn.tail_cus;
+      const int w = base + xcd_wg(blockIdx.x - base, min(bn.tail_cus, (int)gridDim.x - base));
+      if (w < bn.tail_R) {
+        store_tile<C, T, AK, BK, PP, IDX>(tile_at<C>(w, tm, tn, 0), g, C0, C1, msplit, ldc, slab, bias, bn, smem);
+      } else {
+        const int tj = (w - bn.tail_R) / bn.tail_S;
+        store_tile<C, T, AK, BK, PP, IDX>(tile_at<C>(bn.tail_R + tj, tm, tn, 0), g, C0, C1, msplit, ldc, slab, bias,
+                                          bn, smem, tj, w - bn.tail_R - tj * bn.tail_S);
+      }
+      return;
+    }
+  }
   if (bn.ntiles == 0) {  // one tile per workgroup
     store_tile<C, T, AK, BK, PP, IDX>(tile_of<C>(tm, tn), g, C0, C1, msplit, ldc, slab, bias, bn, smem);
     return;
@@ -525,9 +599,15 @@ __global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __re
 template <class C, typename T, bool AK, bool BK, bool PP, int IDX>
 __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g, float* __restrict__ C0,
                                            float* __restrict__ C1, int msplit, int64_t ldc, int64_t slab,
-                                           const float* __restrict__ bias, const StoreEpi& bn, char* smem) {
-  const int kbeg = tl.split * g.k_per_split;
-  const int kend = min(g.K, kbeg + g.k_per_split);
+                                           const float* __restrict__ bias, const StoreEpi& bn, char* smem,
+                                           int tj, int part) {
+  int kbeg = tl.split * g.k_per_split;
+  int kend = min(g.K, kbeg + g.k_per_split);
+  if (tj >= 0) {  // split-tail part: K-tiles [part * per, (part + 1) * per) of the one pass
+    const int per = (g.K / E<T>::KT + bn.tail_S - 1) / bn.tail_S;
+    kbeg = part * per * E<T>::KT;
+    kend = min(g.K, kbeg + per * E<T>::KT);
+  }
   const int nk = (kend - kbeg) / E<T>::KT;
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP) {
@@ -544,6 +624,8 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
     static_assert(IDX == 0, "zero-copy rows: ping-pong main loop only");
     mainloop<C, T, AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
   }
+  GM2_STAMP(5);
+  if (tj >= 0 && !tail_join<C>(acc, bn, tj, part, smem)) return;
   GM2_STAMP(2);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   float* Cz = C0 + (int64_t)tl.split * slab;
@@ -1323,7 +1405,10 @@ static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1
   ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP, IDX>, C::LDS + table_max);
   int grid = tiles;
   StoreEpi ep = bn;
-  if (bn.ntiles) {  // capped grid: the same number of rounds on fewer CUs
+  if (bn.tail_S > 1) {  // split tail: one workgroup per item (plan_tail)
+    grid = bn.tail_R + bn.tail_rem * bn.tail_S;
+    ep.ntiles = 0;
+  } else if (bn.ntiles) {  // capped grid: the same number of rounds on fewer CUs
     const int cus = device_cus(), rounds = (tiles + cus - 1) / cus;
     grid = (tiles + rounds - 1) / rounds;
     ep.ntiles = grid < tiles ? tiles : 0;
@@ -1391,8 +1476,28 @@ int gemm_tiles(const GemmArgs<T>& g) {
   return use_big(g) ? (g.Mp / Big::BM) * (g.Np / Big::BN) : (g.Mp / SmallDeep::BM) * (g.Np / SmallDeep::BN);
 }
 
+// Split-tail plan of a one-pass 256-tile launch over `tiles` tiles (StoreEpi::tail_*): R whole
+// rounds of c = min(CUs, kTailItems) tiles, then the rem left-over tiles in S parts each (S <= CUs / rem, <= 4, >= 8 K-tiles per part); false when the last round is full or the
+// parts would be too small
+static bool plan_tail(int tiles, int K, float* part, int* cnt, StoreEpi& ep) {
+  if (!part || !cnt) return false;
+  const int cus = std::min(device_cus(), kTailItems), nk = K / 64;
+  const int R = tiles / cus, rem = tiles - R * cus;
+  if (R == 0 || rem == 0) return false;
+  const int S = std::min({cus / rem, 4, nk / 8});
+  if (S < 2) return false;
+  ep.tail_R = R * cus;
+  ep.tail_cus = cus;
+  ep.tail_rem = rem;
+  ep.tail_S = S;
+  ep.tail_part = part;
+  ep.tail_cnt = cnt;
+  return true;
+}
+
 template <typename T>
-bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s, bool force_big) {
+bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s, bool force_big,
+                    float* tail_part, int* tail_cnt) {
   // force_big: a one-pass 256x256-tile launch even where the plan would pick 128 tiles (a row
   // slice of a big-tile GEMM, same per-element results as the whole)
   const bool big = force_big ? (sizeof(T) == 2 && g.Mp % 256 == 0 && g.Np % 256 == 0) : use_big(g);
@@ -1404,6 +1509,8 @@ bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hip
   if constexpr (sizeof(T) == 2) {
     if (big) {
       check_gemm(g, 256);
+      if (!force_big && (opts().tail_split & 2) && pp_enabled())
+        plan_tail((g.Mp / 256) * (g.Np / 256), g.K, tail_part, tail_cnt, ep);
       store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
       return true;
     }
@@ -1414,7 +1521,8 @@ bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hip
 }
 
 template <typename T>
-bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, double* sq) {
+bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, double* sq, float* tail_part,
+                       int* tail_cnt) {
   if (plan_gemm(g).splits != 1) return false;
   StoreEpi ep;
   ep.trans = 1;
@@ -1423,6 +1531,8 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
   if constexpr (sizeof(T) == 2) {
     if (use_big(g)) {
       check_gemm(g, 256);
+      if ((opts().tail_split & 1) && pp_enabled())
+        plan_tail((g.Mp / 256) * (g.Np / 256), g.K, tail_part, tail_cnt, ep);
       store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
       return true;
     }
@@ -1552,8 +1662,8 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
 }
 
 #define GM2_INST(T)                                                                                              \
-  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t, double*);                \
-  template bool launch_gemm_sq<T>(const GemmArgs<T>&, float*, int64_t, double*, hipStream_t, bool);              \
+  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t, double*, float*, int*); \
+  template bool launch_gemm_sq<T>(const GemmArgs<T>&, float*, int64_t, double*, hipStream_t, bool, float*, int*);              \
   template int gemm_tiles<T>(const GemmArgs<T>&);                        \
   template bool launch_gemm_bn<T>(const GemmArgs<T>&, float*, int64_t, const float*, const StoreEpi&, hipStream_t);   \
   template int launch_gemm_store<T>(const GemmArgs<T>&, int, float*, float*, int, int64_t, int64_t, const float*, \

@@ -71,7 +71,7 @@ struct GemmArgs {
   const int32_t* qrow = nullptr;
 };
 
-// ---- tuning options (gm2.h GM2_OPT_*): results are bit-identical under every value ----
+// ---- tuning options (gm2.h GM2_OPT_*): results are bit-identical under every value but tail_split ----
 // Each workspace carries its own copy (gm2_workspace_set_option); gm2_set_option edits the process
 // defaults that new workspaces and workspace-less calls (gm2_gemm) start from. The launchers read
 // the options of the call in progress through opts(), which an OptionScope sets per C-ABI call.
@@ -90,6 +90,7 @@ struct Options {
                          //   layers on this many workgroups per CU (0 = not deferred)
   int side_priority = 0; // GM2_OPT_SIDE_PRIORITY  side stream priority: -1 high, 0 normal, 1 low
   int dw9_last = 0;      // GM2_OPT_DW9_LAST  output-layer weight gradient forked beside dWe0, not first
+  int tail_split = 0;    // GM2_OPT_TAIL_SPLIT  split tails of the one-pass weight-gradient GEMMs: 1 dW9, 2 dWe0
 };
 // validated edit of one option (throws on an unknown key or a bad value)
 void option_set(Options& o, int key, int value);
@@ -141,18 +142,35 @@ struct StoreEpi {
   // (grid = ceil(tiles / rounds) for the same number of rounds: the idle CUs of the last round
   // become free CUs for the other stream's work for the whole launch)
   int ntiles = 0;
+  // split tail (tail_S > 1; one K pass, 256x256 tiles): one workgroup per item -- the first tail_R
+  // tiles whole (whole dispatch rounds of tail_cus workgroups), then the last tail_rem tiles in
+  // tail_S K-parts each. The parts meet through tail_part (each part's fp32 accumulators,
+  // [tile][part][BM * BN]) and tail_cnt[tile] (arrival counters, zero between launches: the last
+  // part to arrive resets its tile's); the last to arrive sums the parts in part order and runs
+  // the epilogue.
+  int tail_R = 0, tail_cus = 0, tail_rem = 0, tail_S = 1;
+  float* tail_part = nullptr;
+  int* tail_cnt = nullptr;
 };
+// split-tail scratch of one GEMM: at most kTailItems tile parts of 256 x 256 fp32 + counters
+constexpr int kTailItems = 256;
+constexpr int64_t kTailPartBytes = (int64_t)kTailItems * 256 * 256 * 4;
+constexpr int64_t kTailCntBytes = kTailItems * 4;
 // GEMM + BatchNorm statistics of its output in one launch when the plan allows (one K pass of
 // 128-row tiles); returns false (nothing launched) otherwise
 template <typename T>
 bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const StoreEpi& bn, hipStream_t s);
 // C^T = (P . Q^T)^T into C [N][ldc] in one launch when the plan is one K pass; false otherwise
+// (tail_part / tail_cnt: split-tail scratch, kTailPartBytes / kTailCntBytes, used when the option
+// GM2_OPT_TAIL_SPLIT selects this GEMM and the tile count leaves a short last round)
 template <typename T>
-bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, double* sq = nullptr);
+bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, double* sq = nullptr,
+                       float* tail_part = nullptr, int* tail_cnt = nullptr);
 // C = P . Q^T in one K pass with the per-tile sum of squares of C into sq (see StoreEpi::sq);
 // false (nothing launched) when the plan splits K
 template <typename T>
-bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s, bool force_big = false);
+bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s, bool force_big = false,
+                    float* tail_part = nullptr, int* tail_cnt = nullptr);
 // tiles of a one-pass launch of g (the sq entries it writes)
 template <typename T>
 int gemm_tiles(const GemmArgs<T>& g);

@@ -68,6 +68,10 @@ void option_set(Options& o, int key, int value) {
       o.side_priority = value;
       break;
     case GM2_OPT_DW9_LAST: o.dw9_last = value ? 1 : 0; break;
+    case GM2_OPT_TAIL_SPLIT:
+      if (value < 0 || value > 3) throw Gm2Error("tail split bits %d: 0..3", value);
+      o.tail_split = value;
+      break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -87,6 +91,7 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_DEFER_OUTPUT_ADAM: return o.defer_adam;
     case GM2_OPT_SIDE_PRIORITY: return o.side_priority;
     case GM2_OPT_DW9_LAST: return o.dw9_last;
+    case GM2_OPT_TAIL_SPLIT: return o.tail_split;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

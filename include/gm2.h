@@ -254,7 +254,8 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  * own stream; gm2_timing_end synchronises those events and returns their summed duration and the
  * launch count. Classes: GM2_KC_RECON_LOSS (decoder output layer GEMM + fused BCE / dlogits
  * epilogue), GM2_KC_GEMM_STORE (every other GEMM), GM2_KC_MASK (sampling output layer GEMM). */
-/* Tuning switches (no effect on results' semantics; every value is parity-tested). Each workspace
+/* Tuning switches (no effect on results' semantics; every value is parity-tested; bit-identical
+ * results under every value but GM2_OPT_TAIL_SPLIT's). Each workspace
  * has its own set: gm2_workspace_set_option / gm2_workspace_get_option edit / read it and act on
  * the calls that use that workspace. gm2_set_option / gm2_get_option edit / read the PROCESS
  * DEFAULTS: the set a workspace receives at gm2_workspace_init, and the one gm2_gemm (no
@@ -308,7 +309,14 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *   GM2_OPT_DW9_LAST    1 = the output-layer weight-gradient GEMM (gradient bucket 0) is forked
  *                       beside the input-layer one at the end of the backward instead of first
  *                       (the hidden-layer chain then runs without it); bucket 0 becomes final late,
- *                       so a data-parallel exchange overlaps less of it. Default 0. */
+ *                       so a data-parallel exchange overlaps less of it. Default 0.
+ *   GM2_OPT_TAIL_SPLIT  bit 1 = the output-layer, bit 2 = the input-layer weight-gradient GEMM
+ *                       splits the tiles of its short last round (one K pass, 256x256 tiles, more
+ *                       tiles than CUs, e.g. 860 on 256 CUs = 3 rounds + 92) into 2..4 K-parts on
+ *                       otherwise idle CUs; the last part to finish sums the parts (in part order:
+ *                       deterministic) and stores the tile. The ONE option that changes bits: a
+ *                       split tile's fp32 sums are formed in two parts (same values up to fp32
+ *                       rounding). Default 0. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -322,7 +330,8 @@ enum {
   GM2_OPT_SYNC_BN = 10,
   GM2_OPT_DEFER_OUTPUT_ADAM = 11,
   GM2_OPT_SIDE_PRIORITY = 12,
-  GM2_OPT_DW9_LAST = 13
+  GM2_OPT_DW9_LAST = 13,
+  GM2_OPT_TAIL_SPLIT = 14
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);

@@ -549,6 +549,44 @@ def test_zero_copy_rows_bit_identical(G, B, rows_none):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("G,zero_copy", [(20480, True), (20000, False)])
+def test_split_tail_close_and_deterministic(G, zero_copy):
+    """GM2_OPT_TAIL_SPLIT: the weight-gradient GEMMs' short last round (G = 20480: 320 tiles on 256
+    CUs = 1 round + 64 tiles; G = 20000 -> 79 x 4 = 316) runs as K-parts on otherwise idle CUs. The
+    split tiles' sums are formed in parts, so gradients equal the unsplit run up to fp32 rounding
+    (the loss record, which the forward alone sets, bit for bit); two calls on one workspace give
+    identical bits (the parts sum in part order and every launch leaves its counters at zero)."""
+    H, L, B = 1024, 32, 1024
+    P, S = perturb_bn(*oracle_state(G, H, L, G + B), seed=71)
+    X = synth_x(B, G, 72)
+    eps = torch.randn(B, L, generator=torch.Generator().manual_seed(73)).cuda()
+    sc = scalars(beta=0.37, wgamma=0.55, lam=0.0)
+    sc[native.S_NORM_AHEAD] = 1.0
+    outs = []
+    for split in (0, 3):
+        m = to_model(P, S, G, H, L, native.GM2_BF16)
+        mat = ResidentMatrix(X)
+        res = mat.operands(native.GM2_BF16) if zero_copy else None
+        ws = m.workspace(native.GM2_BF16, B)
+        ws.set_option(native.OPT_TAIL_SPLIT, split)
+        for _ in range(2):
+            grads = torch.zeros_like(m.params)
+            loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+            native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, B, eps, resident=res), m.params, grads,
+                                 m.bn, sc, loss)
+            native.grad_norm(ws, m.params, grads, sc, loss)
+            torch.cuda.synchronize()
+            outs.append((grads.cpu(), loss.cpu()))
+    (g0, l0), (g0b, l0b), (g1, l1), (g1b, l1b) = outs
+    assert torch.equal(g0, g0b) and torch.equal(g1, g1b)
+    assert torch.equal(l1, l1b)
+    assert torch.equal(l0[:3], l1[:3])
+    scale = float(g0.abs().max())
+    assert float((g0 - g1).abs().max()) <= 1e-5 * scale
+    assert not torch.equal(g0, g1)  # the split path ran (its tiles' rounding differs somewhere)
+    assert float(l1[4]) == pytest.approx(float(l0[4]), rel=1e-6)
+
+
 def test_resident_operands_match_the_matrix():
     """gm2_resident_build: rows < S are the 0/1 matrix in bf16 / f32 with zero pad columns up to
     ld = roundup(G, 256), row S (and the allocation's tail) zero, and the packed bits match numpy

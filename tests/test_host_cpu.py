@@ -73,6 +73,12 @@ def test_header_constants_match_binding():
         native.set_option(native.OPT_INPUT_CHUNKS, 2)
     with pytest.raises(RuntimeError, match="4 or 5"):
         native.set_option(native.OPT_SMALL_STAGES, 3)
+    old = native.get_option(native.OPT_TAIL_SPLIT)
+    native.set_option(native.OPT_TAIL_SPLIT, 3)
+    assert native.get_option(native.OPT_TAIL_SPLIT) == 3
+    native.set_option(native.OPT_TAIL_SPLIT, old)
+    with pytest.raises(RuntimeError, match="tail split"):
+        native.set_option(native.OPT_TAIL_SPLIT, 4)
     G, H, L = 55039, 1024, 64
     b = native.grad_bucket_bounds(native.dims(G, H, L, 4096))
     cover = sorted(b)
