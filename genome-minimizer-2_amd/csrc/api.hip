@@ -152,9 +152,9 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.colpart = take(o.colpart_cap * 4);
   o.losspart_cap = std::max<int64_t>((d.Gp / kTile) * (Bm / kTile) * 2, Bm / 64);
   o.losspart = take(o.losspart_cap * 4);
-  o.klpart = take((Bm / 64) * 4);
+  o.klpart = take((Bm / kReparamRows) * 4);
   o.gradpart = take(2048 * 2 * 8);
-  o.colbwd_cap = (Bm / 64) * std::max<int64_t>(H, 2 * d.L);
+  o.colbwd_cap = std::max<int64_t>((Bm / 64) * std::max<int64_t>(H, 2 * d.L), (Bm / kReparamRows) * 2 * d.L);
   o.colbwd = take(7 * o.colbwd_cap * 4);
   o.nahdr = take(16);
   o.nasq = take(2 * (d.Gp / kTile + 1) * (H / kTile + 1) * 8);
@@ -655,7 +655,7 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
     na_ok = bg.direct ? 1 : 0;
     na_n = bg.n9 + bg.n0;
   }
-  launch_fwd_tail(c.f(l.losspart), gemm_recon_grid_blocks<T>(g), c.f(l.klpart), Bp / 64, loss, c.f(l.colpart),
+  launch_fwd_tail(c.f(l.losspart), gemm_recon_grid_blocks<T>(g), c.f(l.klpart), Bp / kReparamRows, loss, c.f(l.colpart),
                   gemm_recon_row_tiles<T>(g), d.Gp, (int)d.G, with_grad ? grads + d.off[D9B] : nullptr,
                   norm_hdr ? (int*)(c.ws + l.nahdr) : nullptr, na_ok, na_n, c.s);
 }
@@ -807,7 +807,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       launch_reparam_bwd<T>(c.f(c.slab_off), S, (int64_t)Bp * L, L, c.f(l.HD), b->eps, scal, B, Bp, L, c.t(l.dH),
                             L2r, dmu_ext, dlv_ext, colh, c.s);
       fork();
-      launch_colsum(colh, Bp / 64, 2 * L, 2 * L, gr + d.off[MUB], gr + d.off[LVB], L, w.s);
+      launch_colsum(colh, Bp / kReparamRows, 2 * L, 2 * L, gr + d.off[MUB], gr + d.off[LVB], L, w.s);
       gemm_to<T>(w, c.t(l.dH), L2r, L2r, c.t(l.A[2]), H, H, 2 * L, H, Bp, gr + d.off[MUW], gr + d.off[LVW], L, H, 0,
                  0);
       S = dx_pre_bn(c.t(l.dH), L2r, c.t(l.sHD), H, (int)d.K2L, 2);

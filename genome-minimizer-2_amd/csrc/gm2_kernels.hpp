@@ -208,6 +208,7 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
 
 // ---- kernels.hip ----
 constexpr int kBnRowChunk = 128;  // rows per BatchNorm partial-statistics chunk
+constexpr int kReparamRows = 16;  // batch rows per block of the reparameterisation kernels (their partials)
 
 // gather strain rows of the resident u8 matrix into X [Bp][ldx] (T), plus the row-major bit-packed
 // target [Bp][ldxb words] (bit g%32 of word g/32 of row b = X[b][g]) that the reconstruction-loss

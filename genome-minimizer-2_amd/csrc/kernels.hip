@@ -292,7 +292,8 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict_
 
 // ---------------------------------------------------------------------------------------------
 // reparameterization: mu|lv = heads (+bias); z = mu + exp(0.5*lv)*eps; KL partial sums.
-// Block: 64 rows; thread loops over (row, l) pairs.
+// Block: kReparamRows rows (Bp / kReparamRows blocks: the work is latency-bound, so many short
+// blocks); each thread's (row, l) elements are loaded before any is used.
 // ---------------------------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void k_reparam(const float* __restrict__ slabs, int S, int64_t slab, int L,
@@ -301,23 +302,38 @@ __global__ __launch_bounds__(256) void k_reparam(const float* __restrict__ slabs
                                                T* __restrict__ Z, int64_t ldz, T* __restrict__ ZT, int64_t ldzt,
                                                float* __restrict__ kl_part) {
   __shared__ float red[4];
-  const int r0 = blockIdx.x * 64;
-  const int ldh = 2 * L;
+  constexpr int PT = kReparamRows * 256 / 256;  // elements per thread at L = 256 (host: L <= 256)
+  const int r0 = blockIdx.x * kReparamRows;
+  const int ldh = 2 * L, n = kReparamRows * L;
+  float mu[PT], lv[PT], e[PT];
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    const int i = threadIdx.x + j * 256, rl = i / L, l = i - rl * L, r = r0 + rl;
+    mu[j] = lv[j] = e[j] = 0.f;
+    if (i < n && r < B) {
+      const int64_t o = (int64_t)r * ldh;
+      mu[j] = slabs[o + l];
+      lv[j] = slabs[o + L + l];
+      for (int z = 1; z < S; ++z) {
+        mu[j] += slabs[z * slab + o + l];
+        lv[j] += slabs[z * slab + o + L + l];
+      }
+      e[j] = eps ? eps[(int64_t)r * L + l] : 0.f;
+    }
+  }
   float kl = 0.f;
-  for (int i = threadIdx.x; i < 64 * L; i += 256) {
-    const int rl = i / L, l = i % L, r = r0 + rl;
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    const int i = threadIdx.x + j * 256, rl = i / L, l = i - rl * L, r = r0 + rl;
+    if (i >= n) break;
     float z = 0.f;
     if (r < B) {
       const int64_t o = (int64_t)r * ldh;
-      float mu = slabs[o + l], lv = slabs[o + L + l];
-      for (int s = 1; s < S; ++s) { mu += slabs[s * slab + o + l]; lv += slabs[s * slab + o + L + l]; }
-      mu += bmu[l];
-      lv += blv[l];
-      HD[o + l] = mu;
-      HD[o + L + l] = lv;
-      const float sd = expf(0.5f * lv);
-      z = mu + sd * (eps ? eps[(int64_t)r * L + l] : 0.f);
-      kl += ((1.0f + lv) - mu * mu) - expf(lv);
+      const float m = mu[j] + bmu[l], v = lv[j] + blv[l];
+      HD[o + l] = m;
+      HD[o + L + l] = v;
+      z = m + expf(0.5f * v) * e[j];
+      kl += ((1.0f + v) - m * m) - expf(v);
     }
     Z[(int64_t)r * ldz + l] = E<T>::cvt(z);
     if (ZT) ZT[(int64_t)l * ldzt + r] = E<T>::cvt(z);
@@ -340,22 +356,36 @@ __global__ __launch_bounds__(256) void k_reparam_bwd(const float* __restrict__ d
                                                    const float* __restrict__ dmu_ext,
                                                    const float* __restrict__ dlv_ext, float* __restrict__ colpart) {
   __shared__ float acc[2][256];
+  constexpr int PT = kReparamRows;  // elements per thread at L = 256 (host: L <= 256)
   const float beta = scal[kScalBeta];
-  const int r0 = blockIdx.x * 64;
-  const int L2 = 2 * L;
+  const int r0 = blockIdx.x * kReparamRows;
+  const int L2 = 2 * L, n = kReparamRows * L;
   // 256 % L == 0 (host-checked): thread t always sees column t % L, so its column sums live in
-  // registers and are combined in a fixed order (deterministic bias gradients)
+  // registers and are combined in a fixed order (deterministic bias gradients). Every load of the
+  // thread is issued before any is used (the work is latency-bound).
+  float dv[PT], muv[PT], lvv[PT], ev[PT];
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    const int i = threadIdx.x + j * 256, rl = i / L, l = i - rl * L, r = r0 + rl;
+    dv[j] = muv[j] = lvv[j] = ev[j] = 0.f;
+    if (i < n && r < B) {
+      const int64_t o = (int64_t)r * ldslab + l;
+      dv[j] = dz[o];
+      for (int s = 1; s < S; ++s) dv[j] += dz[s * slab + o];
+      muv[j] = HD[(int64_t)r * L2 + l];
+      lvv[j] = HD[(int64_t)r * L2 + L + l];
+      ev[j] = eps[(int64_t)r * L + l];
+    }
+  }
   float smu = 0.f, slv = 0.f;
-  for (int i = threadIdx.x; i < 64 * L; i += 256) {
-    const int rl = i / L, l = i % L, r = r0 + rl;
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    const int i = threadIdx.x + j * 256, rl = i / L, l = i - rl * L, r = r0 + rl;
+    if (i >= n) break;
     float gmu = 0.f, glv = 0.f;
     if (r < B) {
-      const int64_t o = (int64_t)r * ldslab + l;
-      float d = dz[o];
-      for (int s = 1; s < S; ++s) d += dz[s * slab + o];
-      const float mu = HD[(int64_t)r * L2 + l], lv = HD[(int64_t)r * L2 + L + l];
+      const float d = dv[j], mu = muv[j], lv = lvv[j], e = ev[j];
       const float sd = expf(0.5f * lv);
-      const float e = eps[(int64_t)r * L + l];
       gmu = d + (0.5f * beta) * (2.0f * mu);
       glv = 0.5f * ((d * e) * sd) + (-0.5f * beta + (0.5f * beta) * expf(lv));
       if (dmu_ext) gmu += dmu_ext[(int64_t)r * L + l];
@@ -1112,7 +1142,8 @@ void launch_reparam(const float* slabs, int S, int64_t slab, int L, const float*
                     const float* eps, int B, int Bp, float* HD, T* Z, int64_t ldz, T* ZT, int64_t ldzt, int Lrows,
                     float* kl_part, hipStream_t s) {
   (void)Lrows;
-  hipLaunchKernelGGL(k_reparam<T>, dim3(Bp / 64), dim3(256), 0, s, slabs, S, slab, L, bmu, blv, eps, B, HD, Z, ldz,
+  if (L > 256 || Bp % kReparamRows) throw Gm2Error("reparam: latent_dim <= 256");
+  hipLaunchKernelGGL(k_reparam<T>, dim3(Bp / kReparamRows), dim3(256), 0, s, slabs, S, slab, L, bmu, blv, eps, B, HD, Z, ldz,
                      ZT, ldzt, kl_part);
   GM2_CHECK_LAUNCH();
 }
@@ -1122,7 +1153,7 @@ void launch_reparam_bwd(const float* dzslabs, int S, int64_t slab, int64_t ldsla
                         const float* scal, int B, int Bp, int L, T* dH, int64_t ldh, const float* dmu_ext,
                         const float* dlv_ext, float* colpart, hipStream_t s) {
   if (L > 256 || 256 % L) throw Gm2Error("reparam_bwd: latent_dim must divide 256");
-  hipLaunchKernelGGL(k_reparam_bwd<T>, dim3(Bp / 64), dim3(256), 0, s, dzslabs, S, slab, ldslab, HD, eps, scal, B, L,
+  hipLaunchKernelGGL(k_reparam_bwd<T>, dim3(Bp / kReparamRows), dim3(256), 0, s, dzslabs, S, slab, ldslab, HD, eps, scal, B, L,
                      dH, ldh, dmu_ext, dlv_ext, colpart);
   GM2_CHECK_LAUNCH();
 }

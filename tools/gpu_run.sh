@@ -11,7 +11,7 @@ if [ -n "$DIAG" ]; then
   [ $rc -ne 0 ] && exit $rc
 fi
 if [ "$PT" != "skip" ]; then
-  timeout -k 10 1000 python3 -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -rf $PT > gpurun_out/gpu_tests_$T.log 2>&1
+  eval timeout -k 10 1000 python3 -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -rf "$PT" > gpurun_out/gpu_tests_$T.log 2>&1
   rc=$?; echo "pytest rc=$rc" >> gpurun_out/gpu_tests_$T.log
   # assertion failures (rc 1) still let the bench run; crashes / timeouts stop here
   [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
