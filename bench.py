@@ -105,6 +105,8 @@ def parse():
                     help="gather each step's rows instead of reading the resident operands in place")
     ap.add_argument("--dw9-last", type=int, choices=[0, 1], default=None,
                     help="output-layer weight gradient beside the input-layer one (GM2_OPT_DW9_LAST)")
+    ap.add_argument("--grad-buckets", type=int, choices=[0, 1], default=0,
+                    help="record gradient-bucket events on one GPU too (GM2_OPT_GRAD_BUCKETS; always 1 under DDP)")
     ap.add_argument("--tail-split", type=int, choices=[0, 1, 2, 3], default=None,
                     help="split the short last tile round of the weight-gradient GEMMs: bit 1 dW9, bit 2 dWe0 "
                          "(GM2_OPT_TAIL_SPLIT)")
@@ -261,6 +263,8 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
     # the output layer's Adam update queued and launched beside the next step's hidden layers
     # (bit-identical; the timed region ends with ws.join(), which launches / waits for the last one)
     ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, a.defer_adam if a.defer_adam is not None else (1 if world == 1 else 0))
+    # gradient-bucket events only where an exchange waits on them (GM2_OPT_GRAD_BUCKETS)
+    ws.set_option(native.OPT_GRAD_BUCKETS, 1 if world > 1 else a.grad_buckets)
     if a.side_priority is not None:
         ws.set_option(native.OPT_SIDE_PRIORITY, a.side_priority)
     if a.dw9_last is not None:
@@ -321,6 +325,7 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
             "defer_adam": ws.get_option(native.OPT_DEFER_OUTPUT_ADAM),
             "side_priority": ws.get_option(native.OPT_SIDE_PRIORITY),
             "dw9_last": ws.get_option(native.OPT_DW9_LAST), "tail_split": ws.get_option(native.OPT_TAIL_SPLIT),
+            "grad_buckets": ws.get_option(native.OPT_GRAD_BUCKETS),
             "zero_copy": res is not None,
             "x": x if (rank == 0 and world == 1) else None, "mat": mat}
     del model, opt, ws, grads, sync
@@ -389,7 +394,7 @@ def main():
                    if world > 1 else "none (one GPU)",
                    "input_prefetch": info["prefetch"], "deferred_output_adam": info["defer_adam"],
                    "side_priority": info["side_priority"], "dw9_last": info["dw9_last"],
-                   "tail_split": info["tail_split"],
+                   "tail_split": info["tail_split"], "grad_bucket_events": info["grad_buckets"],
                    "zero_copy_rows": info["zero_copy"]},
         "train_tflops": round(value * train_flops_per_vector(G, H, L) / 1e12, 2),
         "nonfinite_steps": 0,

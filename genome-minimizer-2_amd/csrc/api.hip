@@ -266,6 +266,7 @@ struct WsState {
   std::vector<hipEvent_t> ev;  // fork/join ring
   size_t next = 0;
   hipEvent_t bucket[GM2_GRAD_BUCKETS] = {};
+  int bucket_ev[GM2_GRAD_BUCKETS] = {0, 1, 2, 3, 4, 5};  // the event that marks bucket b final
   bool recorded = false;  // a training backward has recorded the bucket events
   SlotState slot;
   hipEvent_t slot_done = nullptr;
@@ -709,7 +710,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     } else {
       gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
     }
-    HIP_OK(hipEventRecord(st.bucket[0], w.s));
+    if (st.opt.grad_buckets) HIP_OK(hipEventRecord(st.bucket[0], w.s));
   };
   // GM2_OPT_DW9_LAST: forked beside the input-layer dWe0 GEMM instead, so the hidden-layer chain
   // runs without the 126-us tiles of dW9 holding every CU, and the two big weight-gradient GEMMs'
@@ -762,7 +763,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       // bucket 1 (every hidden-layer weight gradient) is final when the side stream's queue so far
       // is; dWe0 starts without waiting for it (the join follows the dWe0 launch: the side stream's
       // last small GEMM / column sums run beside dWe0's first tiles instead of before them)
-      HIP_OK(hipEventRecord(st.bucket[1], w.s));
+      if (st.opt.grad_buckets) HIP_OK(hipEventRecord(st.bucket[1], w.s));
       if (dw9_last) output_weight_grad();
       if (input_chunked(bg, H)) {  // four row-quarter launches, bucket 2 + q final after launch q
         for (int q = 0; q < 4; ++q) {
@@ -772,14 +773,17 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
           gq.M = gq.Mp = H / 4;
           if (!launch_gemm_sq<T>(gq, gr + d.off[E0W] + (int64_t)r0 * G, G, nullptr, c.s, true))
             throw Gm2Error("input-layer quarter GEMM: not a one-pass plan");
-          HIP_OK(hipEventRecord(st.bucket[2 + q], c.s));
+          if (st.opt.grad_buckets) HIP_OK(hipEventRecord(st.bucket[2 + q], c.s));
+          st.bucket_ev[2 + q] = 2 + q;
         }
       } else {
         if (!bg.direct || !launch_gemm_sq<T>(bg.g0, gr + d.off[E0W], G, nasq + bg.n9, c.s, false,
                                              c.tail_part(l.tailp0), c.tail_cnt(l.tailc0)))
           gemm_to<T>(c, c.t(l.dYT0), Bp, H, bg.g0.Q, bg.g0.ldq, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0,
                      bg.g0.qrow);
-        for (int q = 0; q < 4; ++q) HIP_OK(hipEventRecord(st.bucket[2 + q], c.s));
+        // one launch: buckets 2..5 become final together, one event marks all four
+        if (st.opt.grad_buckets) HIP_OK(hipEventRecord(st.bucket[2], c.s));
+        for (int q = 0; q < 4; ++q) st.bucket_ev[2 + q] = 2;
       }
       if (sr) st.order(w.s, c.s);  // join: the caller's stream sees every weight gradient
       if (nx) {  // the next batch's rows -> the other input slot, on the side stream after dWe0 (beside
@@ -797,7 +801,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
         // beside the data-parallel exchange, which waits on bucket events instead
         if (sr) st.order(w.s, c.s);
       }
-      st.recorded = true;
+      st.recorded = st.opt.grad_buckets != 0;
       break;
     }
     if (i == 3) {  // decoder input layer, then back through the reparameterisation and the heads
@@ -868,8 +872,12 @@ void sync_bn_no_rows(const Layout& lo, float* gr, float* bn, double* loss, void*
     HIP_OK(hipMemsetAsync(syncb, 0, (size_t)n * 8, s));
     st.allreduce(syncb, n, s);
   }
-  for (auto e : st.bucket) HIP_OK(hipEventRecord(e, s));
-  st.recorded = true;
+  if (st.opt.grad_buckets)
+    for (int b = 0; b < GM2_GRAD_BUCKETS; ++b) {
+      HIP_OK(hipEventRecord(st.bucket[b], s));
+      st.bucket_ev[b] = b;
+    }
+  st.recorded = st.opt.grad_buckets != 0;
 }
 
 // gm2_batch.resident usable in place for this training call: its precision, padding and alignment,
@@ -1327,8 +1335,10 @@ int gm2_grad_bucket_bounds(const gm2_dims* d, int64_t* lo_hi) {
 int gm2_wait_grad_bucket(void* ws, int bucket, void* stream) {
   return with_ws(ws, [&](WsState& st) {
     if (bucket < 0 || bucket >= GM2_GRAD_BUCKETS) throw Gm2Error("bucket %d out of range", bucket);
-    if (!st.recorded) throw Gm2Error("no gm2_train_fwd_bwd has run on this workspace yet");
-    HIP_OK(hipStreamWaitEvent((hipStream_t)stream, st.bucket[bucket], 0));
+    if (!st.recorded)
+      throw Gm2Error("no gm2_train_fwd_bwd has recorded gradient buckets on this workspace (none has run, or "
+                     "GM2_OPT_GRAD_BUCKETS is 0)");
+    HIP_OK(hipStreamWaitEvent((hipStream_t)stream, st.bucket[st.bucket_ev[bucket]], 0));
   });
 }
 

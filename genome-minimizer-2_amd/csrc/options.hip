@@ -72,6 +72,7 @@ void option_set(Options& o, int key, int value) {
       if (value < 0 || value > 3) throw Gm2Error("tail split bits %d: 0..3", value);
       o.tail_split = value;
       break;
+    case GM2_OPT_GRAD_BUCKETS: o.grad_buckets = value ? 1 : 0; break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -92,6 +93,7 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_SIDE_PRIORITY: return o.side_priority;
     case GM2_OPT_DW9_LAST: return o.dw9_last;
     case GM2_OPT_TAIL_SPLIT: return o.tail_split;
+    case GM2_OPT_GRAD_BUCKETS: return o.grad_buckets;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

@@ -324,6 +324,8 @@ class VAETrainer:
         # (GM2_OPT_DEFER_OUTPUT_ADAM, bit-identical; the loop below joins it before touching the
         # gradient buffer itself and at the end of the epoch)
         ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, 0 if dist else 1)
+        # (one process exchanges no gradients: no bucket events, GM2_OPT_GRAD_BUCKETS)
+        ws.set_option(native.OPT_GRAD_BUCKETS, 1 if dist else 0)
         if sync:
             sync.prepare(ws)
         if sync_bn:

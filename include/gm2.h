@@ -316,7 +316,11 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       otherwise idle CUs; the last part to finish sums the parts (in part order:
  *                       deterministic) and stores the tile. The ONE option that changes bits: a
  *                       split tile's fp32 sums are formed in two parts (same values up to fp32
- *                       rounding). Default 0. */
+ *                       rounding). Default 0.
+ *   GM2_OPT_GRAD_BUCKETS (workspace option) 1 = gm2_train_fwd_bwd records the gradient-bucket
+ *                       events gm2_wait_grad_bucket waits on (default); 0 = it records none (each
+ *                       is a system-scope release on the stream: ~7 us of idle GPU apiece), and
+ *                       gm2_wait_grad_bucket fails. For a single process that exchanges nothing. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -331,7 +335,8 @@ enum {
   GM2_OPT_DEFER_OUTPUT_ADAM = 11,
   GM2_OPT_SIDE_PRIORITY = 12,
   GM2_OPT_DW9_LAST = 13,
-  GM2_OPT_TAIL_SPLIT = 14
+  GM2_OPT_TAIL_SPLIT = 14,
+  GM2_OPT_GRAD_BUCKETS = 15
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);

@@ -549,6 +549,40 @@ def test_zero_copy_rows_bit_identical(G, B, rows_none):
         assert torch.equal(a, b)
 
 
+def test_grad_bucket_events_off_bit_identical():
+    """GM2_OPT_GRAD_BUCKETS = 0 (one process, no exchange): the backward records no bucket events --
+    same gradients and loss record bit for bit -- and gm2_wait_grad_bucket then fails loudly; with
+    the default every bucket can be waited on (buckets 2..5 of the one-launch input layer share one
+    event)."""
+    G, H, L, B = 16500, 1024, 32, 1024
+    P, S = perturb_bn(*oracle_state(G, H, L, G + 9), seed=81)
+    X = synth_x(B, G, 82)
+    eps = torch.randn(B, L, generator=torch.Generator().manual_seed(83)).cuda()
+    sc = scalars(beta=0.37, wgamma=0.55, lam=0.0)
+    sc[native.S_NORM_AHEAD] = 1.0
+    outs = []
+    for rec in (1, 0):
+        m = to_model(P, S, G, H, L, native.GM2_BF16)
+        mat = ResidentMatrix(X)
+        ws = m.workspace(native.GM2_BF16, B)
+        ws.set_option(native.OPT_GRAD_BUCKETS, rec)
+        grads = torch.zeros_like(m.params)
+        loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+        native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, B, eps), m.params, grads, m.bn, sc, loss)
+        s = torch.cuda.Stream()
+        if rec:
+            for b in range(native.GRAD_BUCKETS):
+                native.wait_grad_bucket(ws, b, s)
+        else:
+            with pytest.raises(RuntimeError, match="GM2_OPT_GRAD_BUCKETS"):
+                native.wait_grad_bucket(ws, 2, s)
+        native.grad_norm(ws, m.params, grads, sc, loss)
+        torch.cuda.synchronize()
+        outs.append((grads.cpu(), loss.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("G,zero_copy", [(20480, True), (20000, False)])
 def test_split_tail_close_and_deterministic(G, zero_copy):
     """GM2_OPT_TAIL_SPLIT: the weight-gradient GEMMs' short last round (G = 20480: 320 tiles on 256
