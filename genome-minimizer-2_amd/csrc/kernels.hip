@@ -466,7 +466,14 @@ __global__ __launch_bounds__(256) void k_fwd_tail(const float* __restrict__ lpar
       const float* part = k < 2 ? lpart + k : kpart;
       const int cnt = k < 2 ? nl : nk, stride = k < 2 ? 2 : 1;
       double s = 0.0;
-      for (int i = threadIdx.x; i < cnt; i += 256) s += (double)part[(int64_t)i * stride];
+      for (int b = threadIdx.x; b < cnt; b += 256 * 8) {  // loads 8 at a time, added in order
+        float q[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) q[j] = b + 256 * j < cnt ? part[(int64_t)(b + 256 * j) * stride] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (b + 256 * j < cnt) s += (double)q[j];
+      }
       s = wave_sum_d(s);
       if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
       __syncthreads();
@@ -618,9 +625,31 @@ __global__ __launch_bounds__(256) void k_grad_finalize(const double* __restrict_
                                                      double* __restrict__ l1abs, NormAhead na) {
   __shared__ double red[2][4];
   double ss = 0.0, ab = 0.0;
-  for (int i = threadIdx.x; i < nb; i += 256) { ss += part[2 * i]; ab += part[2 * i + 1]; }
-  if (use_ahead(na, scal))
-    for (int i = threadIdx.x; i < na.hdr[1]; i += 256) ss += na.sq[i];
+  // (each thread's strided terms are loaded 8 at a time before they are added, in the same order:
+  // one workgroup, so the latency of dependent loads would be the kernel's whole time)
+  for (int b = threadIdx.x; b < nb; b += 256 * 8) {
+    double qs[8], qa[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = b + 256 * j;
+      qs[j] = i < nb ? part[2 * i] : 0.0;
+      qa[j] = i < nb ? part[2 * i + 1] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (b + 256 * j < nb) { ss += qs[j]; ab += qa[j]; }
+  }
+  if (use_ahead(na, scal)) {
+    const int cnt = na.hdr[1];
+    for (int b = threadIdx.x; b < cnt; b += 256 * 8) {
+      double q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] = b + 256 * j < cnt ? na.sq[b + 256 * j] : 0.0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (b + 256 * j < cnt) ss += q[j];
+    }
+  }
   ss = wave_sum_d(ss);
   ab = wave_sum_d(ab);
   if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = ss; red[1][threadIdx.x >> 6] = ab; }
