@@ -99,8 +99,8 @@ def parse():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5-shaped (G=20,000) step line")
     ap.add_argument("--defer-adam", type=int, default=None,
                     help="output layer's Adam update launched beside the next step's hidden layers on this many "
-                         "workgroups per CU, 0 = not deferred (GM2_OPT_DEFER_OUTPUT_ADAM; bit-identical; default 1 on one "
-                         "GPU: 3.34 -> 3.25 ms/step, profiles/r03_schedule_ab.txt; 0 under DDP, as the trainer)")
+                         "workgroups per CU, 0 = not deferred (GM2_OPT_DEFER_OUTPUT_ADAM; bit-identical; default 1, as the "
+                         "trainer: 3.34 -> 3.25 ms/step on one GPU, profiles/r03_schedule_ab.txt)")
     ap.add_argument("--no-zero-copy", action="store_true",
                     help="gather each step's rows instead of reading the resident operands in place")
     ap.add_argument("--dw9-last", type=int, choices=[0, 1], default=None,
@@ -262,7 +262,7 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         ws.set_option(native.OPT_GRID_CAP, a.grid_cap)
     # the output layer's Adam update queued and launched beside the next step's hidden layers
     # (bit-identical; the timed region ends with ws.join(), which launches / waits for the last one)
-    ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, a.defer_adam if a.defer_adam is not None else (1 if world == 1 else 0))
+    ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, a.defer_adam if a.defer_adam is not None else 1)
     # gradient-bucket events only where an exchange waits on them (GM2_OPT_GRAD_BUCKETS)
     ws.set_option(native.OPT_GRAD_BUCKETS, 1 if world > 1 else a.grad_buckets)
     if a.side_priority is not None:

@@ -320,10 +320,12 @@ class VAETrainer:
         rec = torch.zeros(max(nb, 1), native.LOSS_SLOTS, dtype=torch.float64, device=self.device)
         sync = self._grad_sync(dist) if dist else None
         sync_bn = dist is not None and self.sync_bn
-        # one process: the output layer's Adam update runs beside the next batch's hidden layers
+        # the output layer's Adam update runs beside the next batch's hidden layers
         # (GM2_OPT_DEFER_OUTPUT_ADAM, bit-identical; the loop below joins it before touching the
-        # gradient buffer itself and at the end of the epoch)
-        ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, 0 if dist else 1)
+        # gradient buffer itself and at the end of the epoch). Under DDP too: the queued update reads
+        # the exchanged gradient, and the next backward's output-layer bucket is written only after
+        # the library has joined it (before the loss GEMM)
+        ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, 1)
         # (one process exchanges no gradients: no bucket events, GM2_OPT_GRAD_BUCKETS)
         ws.set_option(native.OPT_GRAD_BUCKETS, 1 if dist else 0)
         if sync:
