@@ -7,6 +7,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -689,6 +690,30 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   auto fork = [&] {
     if (sr) st.order(c.s, w.s);
   };
+  // The side-stream work of the first hidden layers (5, 4, 3 and the heads) would queue behind dW9
+  // on the side stream anyway: it is enqueued at the fork of layer 2 instead, one ordering event in
+  // place of five (each costs the main stream ~7 us; -7..-11 us per step, profiles/r03_fork_batch_ab.txt;
+  // holding layer 2 as well measured +15 us). Env GM2_FORK_HOLD = the first layer whose own fork is
+  // taken (6 = every layer forks), for A/Bs.
+  static const int hold_from = [] {
+    const char* e = std::getenv("GM2_FORK_HOLD");
+    return e ? std::max(1, std::atoi(e)) : 3;
+  }();
+  const bool fork_batch = true;
+  std::vector<std::function<void()>> held;
+  auto side_work = [&](bool hold, std::function<void()> f) {
+    if (hold && sr && fork_batch) {
+      held.push_back(std::move(f));
+      return;
+    }
+    f();
+  };
+  auto fork_flush = [&](bool hold) {
+    if (hold && sr && fork_batch) return;
+    fork();
+    for (auto& f : held) f();
+    held.clear();
+  };
   // output layer: dW9[g][h] = sum_b dL[b][g] A5[b][h] ; dA5[b][h] = sum_g dL[b][g] W9[g][h]
   // (its bias gradient was summed in the forward's recon epilogue, before the fork)
   // Written as dW9^T[h][g] = sum_b A5^T[h][b] dL[b][g] with A5^T K-major (a transposed copy made
@@ -754,8 +779,9 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     launch_bn_bwd_apply<T>(sum ? c.f(l.DA) : c.f(c.slab_off), c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train,
                            c.f(l.save[i]), prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]], gr + d.off[kBlk[i][2]],
                            gr + d.off[kBlk[i][3]], c.t(l.dY[i]), colp, c.s, sync ? syncb : nullptr);
-    fork();
-    launch_colsum(colp, Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, w.s);
+    const bool hold = i >= hold_from;
+    fork_flush(hold);
+    side_work(hold, [&, colp, i] { launch_colsum(colp, Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, w.s); });
     const T* dY = c.t(l.dY[i]);
     if (i == 0) {  // input layer: weight gradient only (on the main stream: nothing left to overlap)
       // dWe0[h][g] = sum_b dY0^T[h][b] X[b][g]: dY0^T (K-major copy) x X (MN-major)
@@ -805,19 +831,23 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       break;
     }
     if (i == 3) {  // decoder input layer, then back through the reparameterisation and the heads
-      gemm_to<T>(w, dY, H, H, c.t(l.Z), Lr, Lr, H, L, Bp, gr + d.off[D0W], nullptr, 0, L, 0, 0);
+      side_work(3 >= hold_from, [&, dY] { gemm_to<T>(w, dY, H, H, c.t(l.Z), Lr, Lr, H, L, Bp, gr + d.off[D0W], nullptr, 0, L, 0, 0); });
       S = gemm_to_slabs<T>(c, dY, H, Bp, c.t(l.sD0), Lr, Lr, B, L, H, L, 1, 0);
       float* colh = c.f(l.colbwd) + 6 * l.colbwd_cap;
       launch_reparam_bwd<T>(c.f(c.slab_off), S, (int64_t)Bp * L, L, c.f(l.HD), b->eps, scal, B, Bp, L, c.t(l.dH),
                             L2r, dmu_ext, dlv_ext, colh, c.s);
-      fork();
-      launch_colsum(colh, Bp / kReparamRows, 2 * L, 2 * L, gr + d.off[MUB], gr + d.off[LVB], L, w.s);
-      gemm_to<T>(w, c.t(l.dH), L2r, L2r, c.t(l.A[2]), H, H, 2 * L, H, Bp, gr + d.off[MUW], gr + d.off[LVW], L, H, 0,
-                 0);
+      fork_flush(3 >= hold_from);
+      side_work(3 >= hold_from, [&, colh] {
+        launch_colsum(colh, Bp / kReparamRows, 2 * L, 2 * L, gr + d.off[MUB], gr + d.off[LVB], L, w.s);
+        gemm_to<T>(w, c.t(l.dH), L2r, L2r, c.t(l.A[2]), H, H, 2 * L, H, Bp, gr + d.off[MUW], gr + d.off[LVW], L, H,
+                   0, 0);
+      });
       S = dx_pre_bn(c.t(l.dH), L2r, c.t(l.sHD), H, (int)d.K2L, 2);
       continue;
     }
-    gemm_to<T>(w, dY, H, H, c.t(l.A[i - 1]), H, H, H, H, Bp, gr + d.off[kBlk[i][0]], nullptr, 0, H, 0, 0);
+    side_work(hold, [&, dY, i] {
+      gemm_to<T>(w, dY, H, H, c.t(l.A[i - 1]), H, H, H, H, Bp, gr + d.off[kBlk[i][0]], nullptr, 0, H, 0, 0);
+    });
     S = dx_pre_bn(dY, H, c.t(shadow_w[i]), H, H, i - 1);
   }
 }
