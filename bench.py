@@ -101,6 +101,8 @@ def parse():
                     help="output layer's Adam update launched beside the next step's hidden layers on this many "
                          "workgroups per CU, 0 = not deferred (GM2_OPT_DEFER_OUTPUT_ADAM; bit-identical; default 1, as the "
                          "trainer: 3.34 -> 3.25 ms/step on one GPU, profiles/r03_schedule_ab.txt)")
+    ap.add_argument("--host-timing", action="store_true",
+                    help="print the host's enqueue time per timed step to stderr (diagnostic)")
     ap.add_argument("--no-zero-copy", action="store_true",
                     help="gather each step's rows instead of reading the resident operands in place")
     ap.add_argument("--dw9-last", type=int, choices=[0, 1], default=None,
@@ -300,10 +302,15 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
     torch.cuda.synchronize()
     native.timing_begin(native.KC_RECON_LOSS)
     t0 = time.perf_counter()
+    host_s = 0.0
     for i in range(a.warmup, nsteps):
+        h0 = time.perf_counter()
         step(i)
+        host_s += time.perf_counter() - h0
     ws.join()
     torch.cuda.synchronize()
+    if a.host_timing:  # (stderr: the host's enqueue time per step, the GPU running asynchronously)
+        print(f"host enqueue {1e3 * host_s / max(1, nsteps - a.warmup):.3f} ms/step", file=sys.stderr)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()

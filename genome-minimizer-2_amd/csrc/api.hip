@@ -776,16 +776,20 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       launch_bn_sync_pack(c.f(l.bnpart), B, H, 1, syncb, c.s);
       st.allreduce(syncb, 2 * H + 2, c.s);
     }
+    // (input layer, bf16: its only consumer is dWe0, which reads dY0 transposed -- written that way
+    // by the same pass instead of through a transpose launch)
+    const bool dyt = i == 0 && sizeof(T) == 2;
     launch_bn_bwd_apply<T>(sum ? c.f(l.DA) : c.f(c.slab_off), c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train,
                            c.f(l.save[i]), prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]], gr + d.off[kBlk[i][2]],
-                           gr + d.off[kBlk[i][3]], c.t(l.dY[i]), colp, c.s, sync ? syncb : nullptr);
+                           gr + d.off[kBlk[i][3]], c.t(l.dY[i]), colp, c.s, sync ? syncb : nullptr,
+                           dyt ? c.t(l.dYT0) : nullptr, Bp);
     const bool hold = i >= hold_from;
     fork_flush(hold);
     side_work(hold, [&, colp, i] { launch_colsum(colp, Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, w.s); });
     const T* dY = c.t(l.dY[i]);
     if (i == 0) {  // input layer: weight gradient only (on the main stream: nothing left to overlap)
       // dWe0[h][g] = sum_b dY0^T[h][b] X[b][g]: dY0^T (K-major copy) x X (MN-major)
-      launch_transpose<T>(dY, H, Bp, H, c.t(l.dYT0), Bp, c.s);
+      if (!dyt) launch_transpose<T>(dY, H, Bp, H, c.t(l.dYT0), Bp, c.s);
       // bucket 1 (every hidden-layer weight gradient) is final when the side stream's queue so far
       // is; dWe0 starts without waiting for it (the join follows the dWe0 launch: the side stream's
       // last small GEMM / column sums run beside dWe0's first tiles instead of before them)

@@ -241,7 +241,8 @@ void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, i
 template <typename T>
 void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const float* part, int B, int Bp, int H,
                          int train, const float* save, const float* gamma, const float* beta, float* dgamma,
-                         float* dbeta, T* dY, float* colpart, hipStream_t s, const double* sync = nullptr);
+                         float* dbeta, T* dY, float* colpart, hipStream_t s, const double* sync = nullptr,
+                         T* dYT = nullptr, int64_t ldt = 0);
 // SyncBN: this rank's [sum | sum of squares (mode 0) or sum (y-mean)do (mode 1) | rows, 0] (2H + 2 doubles)
 void launch_bn_sync_pack(const float* part, int B, int H, int mode, double* out, hipStream_t s);
 // SyncBN, a rank with no rows: the running-statistics update from the all-reduced sums

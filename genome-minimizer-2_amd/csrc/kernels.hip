@@ -940,9 +940,15 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                     T* __restrict__ dY, float* __restrict__ colpart,
-                                                    const double* __restrict__ sync) {
+                                                    const double* __restrict__ sync, T* __restrict__ dYT,
+                                                    int64_t ldt) {
   __shared__ float4 cf4[5][64];  // [mean, alpha, beta', grad_mean, proj_scale][column / 4]
   __shared__ float4 red[4][64];
+  // dYT (bf16 only): the output written transposed, dYT [H][ldt] (the input layer's K-major
+  // weight-gradient operand), instead of dY: each thread then takes 16 CONSECUTIVE rows
+  // (rg * 16 + i instead of rg + 4 i), so each of its 4 columns leaves as two 16-B row runs of dYT
+  // (no LDS: the launch keeps room beside a co-running GEMM workgroup)
+  const bool blk = sizeof(T) == 2 && dYT != nullptr;
   float* cf = (float*)cf4;
   const int c0 = blockIdx.x * 256;
   const int cg = threadIdx.x & 63, rg = threadIdx.x >> 6;
@@ -992,14 +998,14 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
     float4 av[16], yv[16];  // (rows >= B re-read row B-1, unused)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int64_t o = (int64_t)min(r0 + rg + 4 * i, B - 1) * ld + c;
+      const int64_t o = (int64_t)min(r0 + (blk ? rg * 16 + i : rg + 4 * i), B - 1) * ld + c;
       av[i] = *(const float4*)(da + o);
       yv[i] = *(const float4*)(Y + o);
     }
     const float4 mean = cf4[0][cg], al = cf4[1][cg], be = cf4[2][cg], gm = cf4[3][cg], ps = cf4[4][cg];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int r = r0 + rg + 4 * i;
+      const int r = r0 + (blk ? rg * 16 + i : rg + 4 * i);
       float4 dx = make_float4(0.f, 0.f, 0.f, 0.f);
       if (r < B) {
         const float4 a = av[i];
@@ -1014,7 +1020,34 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
         dx.w = (d3 - gm.w - (y.w - mean.w) * ps.w) * al.w;
       }
       acc.x += dx.x; acc.y += dx.y; acc.z += dx.z; acc.w += dx.w;
+      if (blk) {
+        av[i] = dx;  // (kept for the transposed stores below)
+        continue;
+      }
       store4<T>(dY + (int64_t)r * ld + c, dx.x, dx.y, dx.z, dx.w);
+    }
+    if constexpr (sizeof(T) == 2) {
+      if (blk) {  // column c + u: rows r0 + rg*16 .. +15 as two 16-B runs
+        T* dst = dYT + (int64_t)c * ldt + r0 + rg * 16;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            float e[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float4 v = av[h * 8 + j];
+              e[j] = u == 0 ? v.x : u == 1 ? v.y : u == 2 ? v.z : v.w;
+            }
+            uint4 pk;
+            pk.x = f2bf2(e[0], e[1]);
+            pk.y = f2bf2(e[2], e[3]);
+            pk.z = f2bf2(e[4], e[5]);
+            pk.w = f2bf2(e[6], e[7]);
+            *(uint4*)(dst + (int64_t)u * ldt + h * 8) = pk;
+          }
+        }
+      }
     }
   }
   red[rg][cg] = acc;
@@ -1233,10 +1266,12 @@ void launch_bn_sync_running(const double* sync, int H, float* rmean, float* rvar
 template <typename T>
 void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const float* part, int B, int Bp, int H,
                          int train, const float* save, const float* gamma, const float* beta, float* dgamma,
-                         float* dbeta, T* dY, float* colpart, hipStream_t s, const double* sync) {
+                         float* dbeta, T* dY, float* colpart, hipStream_t s, const double* sync, T* dYT,
+                         int64_t ldt) {
   if (H % 128 || ld % 4 || Bp % 64 || B <= 0) throw Gm2Error("bn_bwd_apply: H %% 128, ld %% 4, Bp %% 64, B > 0");
+  if (dYT && (sizeof(T) != 2 || ldt % 8 || ldt < Bp)) throw Gm2Error("bn_bwd_apply: transposed output (bf16, ldt)");
   hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3((H + 255) / 256, Bp / 64), dim3(256), 0, s, da, Y, ld,
-                     (const float2*)part, B, H, train, save, gamma, beta, dgamma, dbeta, dY, colpart, sync);
+                     (const float2*)part, B, H, train, save, gamma, beta, dgamma, dbeta, dY, colpart, sync, dYT, ldt);
   GM2_CHECK_LAUNCH();
 }
 
@@ -1319,7 +1354,7 @@ void launch_grad_finalize(const double* part, int nblocks, const float* scal, fl
                                        const float*, float*, float*, float*, T*, hipStream_t, const double*);    \
   template void launch_bn_bwd_apply<T>(const float*, const float*, int64_t, const float*, int, int, int, int,    \
                                        const float*, const float*, const float*, float*, float*, T*, float*,    \
-                                       hipStream_t, const double*);                                             \
+                                       hipStream_t, const double*, T*, int64_t);                                \
   template void launch_transpose<T>(const T*, int64_t, int, int, T*, int64_t, hipStream_t);                    \
   template void launch_adam_fused<T>(const TensorTable&, const float*, float*, float*, float*, const float*,    \
                                      const float*, hipStream_t, int, float*);
