@@ -2,16 +2,20 @@
 
 The golden vectors were produced by tests/golden/make_golden.py importing /root/reference
 (torch 2.10 CPU, 1 thread, MKL_CBWR=COMPATIBLE; the fixture meta records the CPU model and ISA).
-The oracle restates the algorithm with the same fp32 ops in the same order, so at one thread and on
-the same MKL code path (tests/conftest.py selects it) it must match BIT FOR BIT on any x86 host; the explicit-gradient restatement (the math the
-HIP kernels implement) is checked against autograd within fp32 rounding.
+The oracle restates the algorithm with the same fp32 ops in the same order, so at one thread, on
+the same MKL code path (tests/conftest.py selects it) and on the fixture's CPU model it must match
+BIT FOR BIT. On another CPU model torch's pointwise Adam update rounds ~0.3 % of parameters 1 ulp
+differently (losses, gradients and Adam moments stay exact): golden_io.bit_pinned then switches
+to the stated tolerances below, and the integer parts (RNG streams, epochs, counters) stay exact.
+The explicit-gradient restatement (the math the HIP kernels implement) is checked against
+autograd within fp32 rounding.
 """
 import numpy as np
 import pytest
 import torch
 from sklearn.model_selection import train_test_split
 
-from golden_io import assert_pinned, load, require_pinned
+from golden_io import assert_pinned, bit_pinned, load, require_pinned
 from oracle import vae_oracle as O
 
 
@@ -97,10 +101,24 @@ def test_preset_trainer_bit_exact(preset):
     P = O.init_params(G, H, L)
     S = O.init_bn_state(H)
     tr, va, ep = O.run_preset(P, S, _preset(preset), NEP, data[g["train_idx"]], data[g["val_idx"]], BS)
-    assert_pinned(np.array(tr), g[f"{preset}_train_losses"], g, "train losses")
-    assert_pinned(np.array(va), g[f"{preset}_val_losses"], g, "val losses")
     assert ep == int(g[f"{preset}_epochs"][0])
-    assert_pinned(O.flatten(P), g[f"{preset}_params"], g, "params")
+    if bit_pinned(g):
+        np.testing.assert_array_equal(np.array(tr), g[f"{preset}_train_losses"])
+        np.testing.assert_array_equal(np.array(va), g[f"{preset}_val_losses"])
+        np.testing.assert_array_equal(O.flatten(P), g[f"{preset}_params"])
+    else:
+        # Off the fixture's host the 1-ulp differences of the Adam update (golden_io.bit_pinned)
+        # compound over the epochs. Stated trajectory bars: per-epoch losses within 1e-4 relative
+        # (observed 1.4e-5 on an Intel Xeon); parameters: the median within 1e-6 and the 99th
+        # percentile within 5e-4 (observed 1e-7 / 1.3e-4), and every one within 2 x steps x lr --
+        # weights of all-zero input columns and biases feeding a BatchNorm have pure-noise
+        # gradients that Adam turns into O(lr) steps of either sign.
+        np.testing.assert_allclose(np.array(tr), g[f"{preset}_train_losses"], rtol=1e-4)
+        np.testing.assert_allclose(np.array(va), g[f"{preset}_val_losses"], rtol=1e-4)
+        d = np.abs(O.flatten(P) - g[f"{preset}_params"])
+        steps = NEP * -(-len(g["train_idx"]) // BS)
+        assert np.median(d) <= 1e-6 and np.quantile(d, 0.99) <= 5e-4
+        assert d.max() <= 2 * steps * 1e-3
     # the RNG stream position is exact integer state: bit-exact on every host
     np.testing.assert_array_equal(torch.rand(3).numpy(), g[f"{preset}_rng_after"])
     assert all(int(S[b + ".num_batches_tracked"]) == n for b, n in zip(O.BNS, g[f"{preset}_nbt"]))
