@@ -114,6 +114,8 @@ def parse():
                          "(GM2_OPT_TAIL_SPLIT)")
     ap.add_argument("--side-priority", type=int, choices=[-1, 0, 1], default=None,
                     help="priority of the workspace's side stream (GM2_OPT_SIDE_PRIORITY)")
+    ap.add_argument("--side-cus", type=int, default=None,
+                    help="CU mask of the workspace's side stream: this many CUs, 0 = all (GM2_OPT_SIDE_CUS)")
     ap.add_argument("--c5-strains", type=int, default=12500,
                     help="strains resident per rank for the C5 line (the 1/8 shard of 100,000)")
     return ap.parse_args()
@@ -269,6 +271,8 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
     ws.set_option(native.OPT_GRAD_BUCKETS, 1 if world > 1 else a.grad_buckets)
     if a.side_priority is not None:
         ws.set_option(native.OPT_SIDE_PRIORITY, a.side_priority)
+    if a.side_cus is not None:
+        ws.set_option(native.OPT_SIDE_CUS, a.side_cus)
     if a.dw9_last is not None:
         ws.set_option(native.OPT_DW9_LAST, a.dw9_last)
     if a.tail_split is not None:
@@ -333,6 +337,7 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
             "side_priority": ws.get_option(native.OPT_SIDE_PRIORITY),
             "dw9_last": ws.get_option(native.OPT_DW9_LAST), "tail_split": ws.get_option(native.OPT_TAIL_SPLIT),
             "grad_buckets": ws.get_option(native.OPT_GRAD_BUCKETS),
+            "side_cus": ws.get_option(native.OPT_SIDE_CUS),
             "zero_copy": res is not None,
             "x": x if (rank == 0 and world == 1) else None, "mat": mat}
     del model, opt, ws, grads, sync
@@ -402,7 +407,7 @@ def main():
                    "input_prefetch": info["prefetch"], "deferred_output_adam": info["defer_adam"],
                    "side_priority": info["side_priority"], "dw9_last": info["dw9_last"],
                    "tail_split": info["tail_split"], "grad_bucket_events": info["grad_buckets"],
-                   "zero_copy_rows": info["zero_copy"]},
+                   "zero_copy_rows": info["zero_copy"], "side_cus": info["side_cus"]},
         "train_tflops": round(value * train_flops_per_vector(G, H, L) / 1e12, 2),
         "nonfinite_steps": 0,
         # dominant kernel: decoder output layer GEMM [B,H]x[H,G] + fused BCE/abundance/dlogits epilogue

@@ -276,6 +276,7 @@ struct WsState {
   hipEvent_t adam9_done = nullptr;  // a deferred output-layer Adam update (GM2_OPT_DEFER_OUTPUT_ADAM)
   bool adam9_pending = false;       // launched on the side stream, not yet joined
   int side_prio = 0;                // priority the side stream was created with
+  int side_cus = 0;                 // CU-mask size the side stream was created with (0 = all CUs)
   int cus = 0;                      // compute units of dev
   // the queued (not yet launched) output-layer update: launched by kick() beside the next training
   // call's hidden layers, or by join() on the joining stream
@@ -309,7 +310,7 @@ struct WsState {
   // re-created after draining when that option changed), else nullptr
   hipStream_t side_stream() {
     if (!opt.side_stream) return nullptr;
-    if (side && side_prio != opt.side_priority) {
+    if (side && (side_prio != opt.side_priority || side_cus != opt.side_cus)) {
       HIP_OK(hipStreamSynchronize(side));
       HIP_OK(hipStreamDestroy(side));
       side = nullptr;
@@ -318,8 +319,17 @@ struct WsState {
       int least = 0, greatest = 0;
       HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
       const int prio = opt.side_priority > 0 ? least : opt.side_priority < 0 ? greatest : 0;
-      HIP_OK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, std::min(std::max(prio, greatest), least)));
+      if (opt.side_cus > 0 && opt.side_cus < cus) {
+        // the lowest n bits: the driver deals mask bits round-robin over the XCDs (and their shader
+        // engines), so every XCD keeps the same share of CUs for the caller's stream
+        std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+        for (int i = 0; i < opt.side_cus; ++i) mask[i / 32] |= 1u << (i % 32);
+        HIP_OK(hipExtStreamCreateWithCUMask(&side, (uint32_t)mask.size(), mask.data()));
+      } else {
+        HIP_OK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, std::min(std::max(prio, greatest), least)));
+      }
       side_prio = opt.side_priority;
+      side_cus = opt.side_cus;
       if (ev.empty()) {
         ev.resize(64);
         for (auto& e : ev) HIP_OK(hipEventCreateWithFlags(&e, order_event_flags()));
@@ -345,7 +355,8 @@ struct WsState {
     order(s, sd);
     // a few workgroups per CU, looping over the blocks: room stays for the hidden layers' GEMM
     // workgroups (an uncapped grid fills every CU and serialises them behind it)
-    launch_queued(sd, std::max(1, opt.defer_adam) * std::max(1, cus));
+    const int scus = opt.side_cus > 0 && opt.side_cus < cus ? opt.side_cus : cus;
+    launch_queued(sd, std::max(1, opt.defer_adam) * std::max(1, scus));
     HIP_OK(hipEventRecord(adam9_done, sd));
     adam9_pending = true;
   }

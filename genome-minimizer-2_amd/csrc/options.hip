@@ -73,6 +73,10 @@ void option_set(Options& o, int key, int value) {
       o.tail_split = value;
       break;
     case GM2_OPT_GRAD_BUCKETS: o.grad_buckets = value ? 1 : 0; break;
+    case GM2_OPT_SIDE_CUS:
+      if (value < 0 || value > 4096) throw Gm2Error("side CUs %d: 0..4096", value);
+      o.side_cus = value;
+      break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -94,6 +98,7 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_DW9_LAST: return o.dw9_last;
     case GM2_OPT_TAIL_SPLIT: return o.tail_split;
     case GM2_OPT_GRAD_BUCKETS: return o.grad_buckets;
+    case GM2_OPT_SIDE_CUS: return o.side_cus;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

@@ -320,7 +320,14 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *   GM2_OPT_GRAD_BUCKETS (workspace option) 1 = gm2_train_fwd_bwd records the gradient-bucket
  *                       events gm2_wait_grad_bucket waits on (default); 0 = it records none (each
  *                       is a system-scope release on the stream: ~7 us of idle GPU apiece), and
- *                       gm2_wait_grad_bucket fails. For a single process that exchanges nothing. */
+ *                       gm2_wait_grad_bucket fails. For a single process that exchanges nothing.
+ *   GM2_OPT_SIDE_CUS    (workspace option) n > 0 = the side stream is created with a CU mask of n
+ *                       of the device's CUs (hipExtStreamCreateWithCUMask; the mask's bits are
+ *                       interleaved over the XCDs by the driver), so its weight-gradient GEMMs and
+ *                       deferred update leave the other CUs to the caller's critical-path chain;
+ *                       0 = every CU (default). Replaces GM2_OPT_SIDE_PRIORITY while set. Takes
+ *                       effect at the next side-stream use (re-created after draining).
+ *                       Results are bit-identical. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -336,7 +343,8 @@ enum {
   GM2_OPT_SIDE_PRIORITY = 12,
   GM2_OPT_DW9_LAST = 13,
   GM2_OPT_TAIL_SPLIT = 14,
-  GM2_OPT_GRAD_BUCKETS = 15
+  GM2_OPT_GRAD_BUCKETS = 15,
+  GM2_OPT_SIDE_CUS = 16
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);

@@ -476,7 +476,8 @@ def test_capped_grid_bit_identical(G):
 @pytest.mark.parametrize("G", [20480, 16500])
 def test_backward_schedule_options_bit_identical(G):
     """GM2_OPT_DW9_LAST (output-layer weight gradient forked beside the input-layer one) and
-    GM2_OPT_SIDE_PRIORITY (low / high side stream) only reorder launches: gradients, loss record and
+    GM2_OPT_SIDE_PRIORITY (low / high side stream) and GM2_OPT_SIDE_CUS (CU-masked side stream)
+    only reorder launches: gradients, loss record and
     clip statistics are bit-identical to the default schedule, with the one-launch and the
     four-quarter input-layer gradient."""
     H, L, B = 1024, 32, 1024
@@ -486,12 +487,14 @@ def test_backward_schedule_options_bit_identical(G):
     sc = scalars(beta=0.37, wgamma=0.55, lam=0.0)
     sc[native.S_NORM_AHEAD] = 1.0
     outs = []
-    for last, prio, chunks in ((0, 0, 1), (1, 0, 1), (1, 1, 1), (1, -1, 4), (0, 1, 4)):
+    for last, prio, chunks, scus in ((0, 0, 1, 0), (1, 0, 1, 0), (1, 1, 1, 0), (1, -1, 4, 0), (0, 1, 4, 0),
+                                     (0, 0, 1, 192), (1, 0, 4, 64)):
         m = to_model(P, S, G, H, L, native.GM2_BF16)
         mat = ResidentMatrix(X)
         ws = m.workspace(native.GM2_BF16, B)
         ws.set_option(native.OPT_DW9_LAST, last)
         ws.set_option(native.OPT_SIDE_PRIORITY, prio)
+        ws.set_option(native.OPT_SIDE_CUS, scus)
         ws.set_option(native.OPT_INPUT_CHUNKS, chunks)
         grads = torch.zeros_like(m.params)
         loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
