@@ -922,10 +922,13 @@ __device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], con
           bce2 += f32x2_t{l0, l1};  // max(log2, -100/ln 2)
           ps2 += p2;
           const f32x2_t r2 = {bfi(msk0, nomp2.x, p2.x), bfi(msk1, nomp2.y, p2.y)};  // p - x
-          const f32x2_t q2 = nomp2 * f32x2_t{-1e12f, -1e12f} * p2;
-          const f32x2_t s2 = {__builtin_amdgcn_fmed3f(q2.x, 0.0f, 1.0f), __builtin_amdgcn_fmed3f(q2.y, 0.0f, 1.0f)};
+          // -(1 - p) p once (packed); the 1e-12 guard factor is one multiply with the clamp
+          // modifier per element, and the gene-abundance term reuses the product
+          const f32x2_t t2 = nomp2 * p2;
+          const f32x2_t s2 = {__builtin_amdgcn_fmed3f(t2.x * -1e12f, 0.0f, 1.0f),
+                              __builtin_amdgcn_fmed3f(t2.y * -1e12f, 0.0f, 1.0f)};
           f32x2_t dl2 = r2 * s2;
-          if constexpr (WG) dl2 = f32x2_t{-wgam, -wgam} * (nomp2 * p2) + dl2;
+          if constexpr (WG) dl2 = f32x2_t{-wgam, -wgam} * t2 + dl2;
           dl4[2 * h] = dl2.x;
           dl4[2 * h + 1] = dl2.y;
         }
