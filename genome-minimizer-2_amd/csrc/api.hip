@@ -593,7 +593,8 @@ TensorTable table_range(const TensorTable& tt, int lo, int hi) {
 template <typename T>
 void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, int train, int with_grad,
              const float* scal, double* loss, float* grads, float* probs = nullptr, int64_t ld_probs = 0,
-             int* counts = nullptr, float thr = 0.5f, bool norm_hdr = false, bool staged = false) {
+             int* counts = nullptr, float thr = 0.5f, bool norm_hdr = false, bool staged = false,
+             std::function<void(hipStream_t)>* defer_tail = nullptr) {
   const Dims& d = c.d;
   const Layout& l = c.lo;
   const int B = (int)b->n;
@@ -668,9 +669,23 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
     na_ok = bg.direct ? 1 : 0;
     na_n = bg.n9 + bg.n0;
   }
-  launch_fwd_tail(c.f(l.losspart), gemm_recon_grid_blocks<T>(g), c.f(l.klpart), Bp / kReparamRows, loss, c.f(l.colpart),
-                  gemm_recon_row_tiles<T>(g), d.Gp, (int)d.G, with_grad ? grads + d.off[D9B] : nullptr,
-                  norm_hdr ? (int*)(c.ws + l.nahdr) : nullptr, na_ok, na_n, c.s);
+  // 4) loss slot sums + the output bias's gradient (column sums of dL): nothing in the backward
+  // reads them before its final join, so a training call hands the launch to the backward, which
+  // puts it on the side stream behind its first fork (off the critical path, one launch and its
+  // gap fewer on the caller's stream)
+  const float* lpart = c.f(l.losspart);
+  const int nlp = gemm_recon_grid_blocks<T>(g), nkp = Bp / kReparamRows, rt = gemm_recon_row_tiles<T>(g);
+  const float *kpart = c.f(l.klpart), *cpart = c.f(l.colpart);
+  const int64_t Gp = d.Gp, G = d.G;
+  float* bgrad = with_grad ? grads + d.off[D9B] : nullptr;
+  int* hdr = norm_hdr ? (int*)(c.ws + l.nahdr) : nullptr;
+  auto tail = [=](hipStream_t s) {
+    launch_fwd_tail(lpart, nlp, kpart, nkp, loss, cpart, rt, Gp, G, bgrad, hdr, na_ok, na_n, s);
+  };
+  // (env GM2_TAIL_MAIN: on the caller's stream, as before; A/B profiles/r03_fwd_tail_side_ab.txt)
+  static const bool tail_main = std::getenv("GM2_TAIL_MAIN") != nullptr;
+  if (defer_tail && !tail_main) *defer_tail = tail;
+  else tail(c.s);
 }
 
 // The next training batch's gather, staged into the other input slot (gm2_batch.next)
@@ -686,7 +701,7 @@ struct NextStage {
 template <typename T>
 void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, const float* scal,
               const float* dmu_ext = nullptr, const float* dlv_ext = nullptr, int train = 1,
-              const NextStage* nx = nullptr) {
+              const NextStage* nx = nullptr, std::function<void(hipStream_t)>* fwd_tail = nullptr) {
   const Dims& d = c.d;
   const Layout& l = c.lo;
   const int B = (int)b->n, Bp = (int)round_up(B, kTile);
@@ -734,8 +749,16 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   // GPU; first keeps gradient bucket 0 early for the data-parallel exchange.)
   const BigGrads<T> bg = big_grads<T>(c, Bp);
   double* nasq = (double*)(c.ws + l.nasq);
+  // the forward's deferred tail launch (loss sums, output bias gradient): behind the first fork
+  auto tail_on = [&](hipStream_t s) {
+    if (fwd_tail && *fwd_tail) {
+      (*fwd_tail)(s);
+      *fwd_tail = nullptr;
+    }
+  };
   auto output_weight_grad = [&] {
     fork();
+    tail_on(w.s);
     const GemmArgs<T>& g9 = bg.g9;
     if (plan_gemm<T>(g9).splits == 1) {
       // (A5^T here on the side stream; on the main stream before the fork measured ~35 us/step
@@ -753,6 +776,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   // tile rounds interleave (their last rounds fill each other's idle CUs)
   const bool dw9_last = st.opt.dw9_last != 0 && sr;
   if (!dw9_last) output_weight_grad();
+  tail_on(c.s);  // (dW9 forked last: on the caller's stream)
   // dA_j = dY . W (K-major dY, MN-major W) into the slab area; when the plan allows, the GEMM's
   // epilogue also takes BatchNorm j's backward partials (sum do, sum (y-mean) do)
   bool have_part = false;
@@ -961,8 +985,9 @@ void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr
     c.xbres = b->resident_bits;
     c.ld_xbres = b->ld_resident_bits;
     drop_stage(st, c.s);
-    forward<T>(c, b, prm, bn, 1, 1, scal, loss, gr, nullptr, 0, nullptr, 0.5f, true, false);
-    backward<T>(c, b, prm, gr, scal, nullptr, nullptr, 1, nullptr);
+    std::function<void(hipStream_t)> tail;
+    forward<T>(c, b, prm, bn, 1, 1, scal, loss, gr, nullptr, 0, nullptr, 0.5f, true, false, &tail);
+    backward<T>(c, b, prm, gr, scal, nullptr, nullptr, 1, nullptr, &tail);
     return;
   }
   SlotState& ss = st.slot;
@@ -983,8 +1008,9 @@ void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr
     nx.xbo = slot ? lo.XB : lo.XB1;
     nx.done = st.slot_done;
   }
-  forward<T>(c, b, prm, bn, 1, 1, scal, loss, gr, nullptr, 0, nullptr, 0.5f, true, hit);
-  backward<T>(c, b, prm, gr, scal, nullptr, nullptr, 1, nb ? &nx : nullptr);
+  std::function<void(hipStream_t)> tail;
+  forward<T>(c, b, prm, bn, 1, 1, scal, loss, gr, nullptr, 0, nullptr, 0.5f, true, hit, &tail);
+  backward<T>(c, b, prm, gr, scal, nullptr, nullptr, 1, nb ? &nx : nullptr, &tail);
   if (nb) {
     ss.staged = true;
     ss.slot = slot ^ 1;
