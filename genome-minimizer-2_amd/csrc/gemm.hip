@@ -868,25 +868,34 @@ __device__ __forceinline__ void recon_tile(const f32x4 (&acc)[C::FM][C::FN], con
   // strain-major order: one strain column (16 lanes x 4 genes x FM slices) at a time, so only
   // that strain's target words and one LDS row base are live (the image offsets of the FM slices
   // are immediates)
+  // every strain column's target words are loaded up front (the main loop's fragment registers are
+  // free now): one exposed load latency per tile instead of one per strain column
+  uint32_t xwa[C::FN][XW];
+#pragma unroll
+  for (int ni = 0; ni < C::FN; ++ni) {
+    const int sl = wn * C::WTN + ni * 16 + c;
+    // (zero-copy rows: the strain's row of the resident target bits, from the tile's LDS table)
+    const uint32_t* xp = xrow + (int64_t)(xidx ? xidx[sl] : n0 + sl) * ldxb;
+    if (n0 + sl < N) {
+      if constexpr (XW == 4) {
+        const uint4 v = *(const uint4*)xp;
+        xwa[ni][0] = v.x; xwa[ni][1] = v.y; xwa[ni][2] = v.z; xwa[ni][3] = v.w;
+      } else {
+        const uint2 v = *(const uint2*)xp;
+        xwa[ni][0] = v.x; xwa[ni][1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < XW; ++k) xwa[ni][k] = 0u;
+    }
+  }
 #pragma unroll
   for (int ni = 0; ni < C::FN; ++ni) {
     const int sl = wn * C::WTN + ni * 16 + c;  // strain (tile-local)
     const bool sok = n0 + sl < N;
     uint32_t xw[XW];
-    // (zero-copy rows: the strain's row of the resident target bits, from the tile's LDS table)
-    const uint32_t* xp = xrow + (int64_t)(xidx ? xidx[sl] : n0 + sl) * ldxb;
-    if (sok) {
-      if constexpr (XW == 4) {
-        const uint4 v = *(const uint4*)xp;
-        xw[0] = v.x; xw[1] = v.y; xw[2] = v.z; xw[3] = v.w;
-      } else {
-        const uint2 v = *(const uint2*)xp;
-        xw[0] = v.x; xw[1] = v.y;
-      }
-    } else {
 #pragma unroll
-      for (int k = 0; k < XW; ++k) xw[k] = 0u;
-    }
+    for (int k = 0; k < XW; ++k) xw[k] = xwa[ni][k];
     // this lane's genes of word k sit at bits (mi & 1) * 16 + j after the shift by 4q
 #pragma unroll
     for (int k = 0; k < XW; ++k) xw[k] >>= 4 * q;

@@ -11,7 +11,8 @@ import os
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgm2.so")
+# (env GM2_LIB_PATH: another build of the library, for same-box A/Bs of two builds)
+LIB_PATH = os.environ.get("GM2_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgm2.so")
 
 GM2_F32 = 0
 GM2_BF16 = 1
