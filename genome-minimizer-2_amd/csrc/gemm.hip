@@ -35,6 +35,7 @@ namespace gm2 {
 namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 // Diagnostic timestamps (s_memrealtime, 100 MHz) of the store kernel's phases per workgroup; only
 // compiled into the standalone probe tools/stamp_gemm.hip, never into libgm2.
@@ -508,7 +509,6 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
 // not coherent with each other): the slots move through system-coherent (sc1) buffer stores /
 // loads, the stores drained before the count -- no cache-wide writeback or invalidate, which would
 // cost every other workgroup on the XCD its cached operands.
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 constexpr int kSc1 = 16;  // buffer instruction cache policy: sc1
 
 template <class C>
@@ -1091,7 +1091,10 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
     for (int e = 0; e < EPC; ++e) cs[e] = 0.f;
     for (int r = r0; r < C::BN; r += RG) {
       const uint4 v = *(const uint4*)(img + r * PR + cch * EPC);
-      *(uint4*)(dL + (int64_t)(tl.n0 + r) * ldd + tl.m0 + cch * EPC) = v;
+      // (non-temporal: the 451-MB dL stream does not displace the output-layer weights, which
+      // the loss GEMM re-reads from the Infinity Cache across strain tiles)
+      __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w},
+                                  (u32x4_t*)(dL + (int64_t)(tl.n0 + r) * ldd + tl.m0 + cch * EPC));
       if (tl.n0 + r < g.N) {
         if constexpr (sizeof(T) == 2) {
           const uint32_t w[4] = {v.x, v.y, v.z, v.w};
