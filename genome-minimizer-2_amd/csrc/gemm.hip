@@ -47,8 +47,9 @@ __device__ unsigned long long g_stamp[16384][8];
 #define GM2_STAMP(i)
 #endif
 
-template <int BM_, int BN_, int WGM_, int WGN_, int NS_ = 2>
+template <int BM_, int BN_, int WGM_, int WGN_, int NS_ = 2, int MINW_ = 1>
 struct Cfg {
+  static constexpr int MINW = MINW_;                 // min waves per SIMD (launch bounds: VGPR cap)
   static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_;
   static constexpr int NT = 64 * WGM * WGN;          // threads
   static constexpr int WTM = BM / WGM, WTN = BN / WGN;
@@ -70,6 +71,10 @@ using SmallDeep8 = Cfg<128, 128, 2, 4, 4>;
 // Five stages (the whole 160 KB LDS): four K-steps in flight (GM2_OPT_SMALL_STAGES = 5)
 using SmallDeep5 = Cfg<128, 128, 2, 2, 5>;
 using SmallDeep85 = Cfg<128, 128, 2, 4, 5>;
+// Half-width tiles (GM2_OPT_SMALL_TILE = 64; bf16, both operands K-major: the forward's hidden
+// layers): 128x64, 4 waves (64x32 each), 3-stage ring of 24 KB -- 72 KB, two workgroups per CU, so
+// twice the tiles (and requests in flight) per CU at 1.5x the operand bytes per FLOP
+using SmallHalf = Cfg<128, 64, 2, 2, 3, 2>;
 
 struct TileXY {
   int m0, n0, split, t;
@@ -560,7 +565,7 @@ __device__ __forceinline__ bool tail_join(f32x4 (&acc)[C::FM][C::FN], const Stor
 // IDX (zero-copy rows, PP only): 1 = P's rows through g.prow, 2 = Q's k-rows through g.qrow; the
 // tile's slice of the index array sits in an LDS table after the staging ring
 template <class C, typename T, bool AK, bool BK, bool PP, int IDX = 0>
-__global__ __launch_bounds__(C::NT) void k_gemm_store(GemmArgs<T> g, float* __restrict__ C0, float* __restrict__ C1,
+__global__ __launch_bounds__(C::NT, C::MINW) void k_gemm_store(GemmArgs<T> g, float* __restrict__ C0, float* __restrict__ C1,
                                                     int msplit, int64_t ldc, int64_t slab,
                                                     const float* __restrict__ bias, StoreEpi bn) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1374,6 +1379,15 @@ static auto small_cfg(F&& f) {
   return w8 ? f(SmallDeep8{}) : f(SmallDeep{});
 }
 
+// the half-width tiles where they apply (both operands K-major, bf16), else small_cfg
+template <typename T, class F>
+static auto small_cfg_for(const GemmArgs<T>& g, F&& f) {
+  if constexpr (sizeof(T) == 2) {
+    if (opts().small_tile == 64 && g.pk && g.qk && g.Np % 64 == 0) return f(SmallHalf{});
+  }
+  return small_cfg(f);
+}
+
 // GM2_OPT_GRID_CAP bits: 1 = the output-layer weight-gradient GEMM (side stream, beside the
 // hidden-layer backward chain), 2 = the input-layer one (beside the side stream's last hidden-layer
 // weight gradients) on a capped grid -- same rounds, the last round's idle CUs free for the rest
@@ -1462,6 +1476,7 @@ static int store_impl(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
   a.k_per_split = (int)(round_up(nkt, splits) / splits) * kt;
   splits = (int)((g.K + a.k_per_split - 1) / a.k_per_split);
   const int tiles = (g.Mp / C::BM) * (g.Np / C::BN) * splits;
+  if (C::BN == 64 && !(g.pk && g.qk)) throw Gm2Error("gemm: 128x64 tiles need K-major operands");
   TimedLaunch tl(kKcGemmStore, s);
   if (g.pk && g.qk) store_launch<C, T, true, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
   else if (g.pk && !g.qk) store_launch<C, T, true, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
@@ -1483,7 +1498,7 @@ int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
     }
   }
   check_gemm(g, 128);
-  return small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s); });
+  return small_cfg_for(g, [&](auto cfg) { return store_impl<decltype(cfg), T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s); });
 }
 
 template <typename T>
@@ -1568,7 +1583,7 @@ bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bi
   const GemmPlan p = plan_gemm(g);
   if (p.tile != 128 || p.splits != 1 || (bn.mode && (g.N % 4 || bn.ldy % 4))) return false;
   check_gemm(g, 128);
-  small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s); });
+  small_cfg_for(g, [&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s); });
   return true;
 }
 

@@ -93,6 +93,7 @@ struct Options {
   int tail_split = 0;    // GM2_OPT_TAIL_SPLIT  split tails of the one-pass weight-gradient GEMMs: 1 dW9, 2 dWe0
   int grad_buckets = 1;  // GM2_OPT_GRAD_BUCKETS  record the gradient-bucket events (gm2_wait_grad_bucket)
   int side_cus = 0;      // GM2_OPT_SIDE_CUS  CU mask of the side stream: this many CUs (0 = all)
+  int small_tile = 128;  // GM2_OPT_SMALL_TILE  N width of the forward's hidden-layer tiles (128 or 64)
 };
 // validated edit of one option (throws on an unknown key or a bad value)
 void option_set(Options& o, int key, int value);

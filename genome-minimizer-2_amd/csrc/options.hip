@@ -77,6 +77,10 @@ void option_set(Options& o, int key, int value) {
       if (value < 0 || value > 4096) throw Gm2Error("side CUs %d: 0..4096", value);
       o.side_cus = value;
       break;
+    case GM2_OPT_SMALL_TILE:
+      if (value != 64 && value != 128) throw Gm2Error("small tile %d: 64 or 128", value);
+      o.small_tile = value;
+      break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -99,6 +103,7 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_TAIL_SPLIT: return o.tail_split;
     case GM2_OPT_GRAD_BUCKETS: return o.grad_buckets;
     case GM2_OPT_SIDE_CUS: return o.side_cus;
+    case GM2_OPT_SMALL_TILE: return o.small_tile;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

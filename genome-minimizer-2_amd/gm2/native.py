@@ -41,6 +41,7 @@ OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE, OPT_SMALL_SPLIT, OPT_BN_EPILOGUE, 
 OPT_INPUT_CHUNKS, OPT_SMALL_STAGES, OPT_GRID_CAP, OPT_SYNC_BN, OPT_DEFER_OUTPUT_ADAM = 7, 8, 9, 10, 11
 OPT_SIDE_PRIORITY, OPT_DW9_LAST, OPT_TAIL_SPLIT, OPT_GRAD_BUCKETS = 12, 13, 14, 15
 OPT_SIDE_CUS = 16
+OPT_SMALL_TILE = 17
 # gm2_allreduce_fn (gm2.h): int (double* buf, int64_t count, void* stream, void* user)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
 

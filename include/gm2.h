@@ -327,7 +327,10 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       deferred update leave the other CUs to the caller's critical-path chain;
  *                       0 = every CU (default). Replaces GM2_OPT_SIDE_PRIORITY while set. Takes
  *                       effect at the next side-stream use (re-created after draining).
- *                       Results are bit-identical. */
+ *                       Results are bit-identical.
+ *   GM2_OPT_SMALL_TILE  N width of the 128-row tiles of the bf16 GEMMs whose operands are both
+ *                       K-major (the forward's hidden layers): 128 (default) or 64 (two 72-KB
+ *                       workgroups per CU). Results are bit-identical. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -344,7 +347,8 @@ enum {
   GM2_OPT_DW9_LAST = 13,
   GM2_OPT_TAIL_SPLIT = 14,
   GM2_OPT_GRAD_BUCKETS = 15,
-  GM2_OPT_SIDE_CUS = 16
+  GM2_OPT_SIDE_CUS = 16,
+  GM2_OPT_SMALL_TILE = 17
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);

@@ -439,6 +439,33 @@ def test_small_tile_ring_depth_bit_identical(prec, waves):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("H", [256, 1024])
+def test_half_width_tiles_bit_identical(H):
+    """GM2_OPT_SMALL_TILE = 64: the forward's hidden-layer GEMMs (both operands K-major) on 128x64
+    tiles, two workgroups per CU; the K order of every output and the 16-row partition of the
+    BatchNorm epilogue sums are those of the 8-wave 128x128 tiles, so the bf16 step (forward,
+    backward, clip statistics, BatchNorm running statistics) is bit-identical."""
+    G, L, B = 1000, 32, 512
+    P, S = perturb_bn(*oracle_state(G, H, L, G + B + 1), seed=24)
+    X = synth_x(B, G, 25)
+    eps = torch.randn(B, L, generator=torch.Generator().manual_seed(26)).cuda()
+    sc = scalars(beta=0.37, wgamma=0.55, lam=0.01)
+    outs = []
+    for tile in (128, 64):
+        m = to_model(P, S, G, H, L, native.GM2_BF16)
+        mat = ResidentMatrix(X)
+        ws = m.workspace(native.GM2_BF16, B)
+        ws.set_option(native.OPT_SMALL_TILE, tile)
+        grads = torch.zeros_like(m.params)
+        loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+        native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, B, eps), m.params, grads, m.bn, sc, loss)
+        native.grad_norm(ws, m.params, grads, sc, loss)
+        torch.cuda.synchronize()
+        outs.append((grads.cpu(), loss.cpu(), m.bn.cpu()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("G", [20480, 20000])
 def test_capped_grid_bit_identical(G):
     """GM2_OPT_GRID_CAP: the output-layer weight-gradient GEMM on a capped grid (workgroups loop over
