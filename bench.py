@@ -118,8 +118,6 @@ def parse():
                     help="CU mask of the workspace's side stream: this many CUs, 0 = all (GM2_OPT_SIDE_CUS)")
     ap.add_argument("--small-tile", type=int, choices=[64, 128], default=None,
                     help="N width of the forward hidden-layer GEMM tiles (GM2_OPT_SMALL_TILE)")
-    ap.add_argument("--l2-touch", type=int, choices=[0, 1, 2, 3], default=None,
-                    help="L2 touch of the K-tile after next: bit 1 store GEMMs, bit 2 loss GEMM (GM2_OPT_L2_TOUCH)")
     ap.add_argument("--c5-strains", type=int, default=12500,
                     help="strains resident per rank for the C5 line (the 1/8 shard of 100,000)")
     return ap.parse_args()
@@ -279,8 +277,6 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         ws.set_option(native.OPT_SIDE_CUS, a.side_cus)
     if a.small_tile is not None:
         ws.set_option(native.OPT_SMALL_TILE, a.small_tile)
-    if a.l2_touch is not None:
-        ws.set_option(native.OPT_L2_TOUCH, a.l2_touch)
     if a.dw9_last is not None:
         ws.set_option(native.OPT_DW9_LAST, a.dw9_last)
     if a.tail_split is not None:

@@ -35,12 +35,6 @@ namespace gm2 {
 namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
-constexpr int kTouchBytes = 2048;  // L2-touch scratch: 512 threads x 4 B (GM2_OPT_L2_TOUCH)
-// The touch is compiled in only with -DGM2_L2_TOUCH=1 (its address registers cost the 256-tile
-// kernels spill slots even when off); without it GM2_OPT_L2_TOUCH is accepted and has no effect.
-#ifndef GM2_L2_TOUCH
-#define GM2_L2_TOUCH 0
-#endif
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 // Diagnostic timestamps (s_memrealtime, 100 MHz) of the store kernel's phases per workgroup; only
@@ -370,8 +364,7 @@ __device__ __forceinline__ void barrier() {
 template <bool AK, bool BK, int IDX = 0>
 __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_t ldp, const bf16_t* __restrict__ Q,
                                             int64_t ldq, int m0, int n0, int kbeg, int nk, char* smem,
-                                            f32x4 (&acc)[8][4], const int* sidx = nullptr,
-                                            char* touch_lds = nullptr) {
+                                            f32x4 (&acc)[8][4], const int* sidx = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // wave-uniform in an SGPR: the stagger barriers below must be branched around, not exec-masked
   const int wm = __builtin_amdgcn_readfirstlane(wid >> 2), wn = wid & 3;
@@ -398,33 +391,6 @@ __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_
     char* r = region(t, h);
     if (h == 0 || h == 3) pp::stage_half<AK, true, IDX == 1>(P, ldp, m0, h == 0 ? 0 : 1, k0, r, tid, h == 0 ? ra0 : ra1);
     else pp::stage_half<BK, false, IDX == 2>(Q, ldq, n0, h == 1 ? 0 : 1, k0, r, tid, rq);
-  };
-  // L2 touch (GM2_OPT_L2_TOUCH): at phase 0 of K-tile t every thread issues one 4-byte LDS-DMA
-  // load of a 128-B line of K-tile t + 2 (threads 0..255 the A half-tiles' lines, 256..511 the
-  // B ones) into a 2-KB scratch nobody reads, so the lines are in the XCD's L2 when the real
-  // stage of t + 2 is issued one K-tile later: the 2-stage LDS ring keeps one K-tile in flight,
-  // the touch a second one. Loads retire in issue order, so the phase-0 and phase-1 waits of a
-  // touching K-tile count one more outstanding load.
-  auto touch = [&](int t) {
-    const int k0 = kbeg + t * 64;
-    const bf16_t* src;
-    if (tid < 256) {
-      if constexpr (AK) {
-        const int64_t row = IDX == 1 ? (int64_t)sidx[tid] : (int64_t)(m0 + tid);
-        src = P + row * ldp + k0;
-      } else {
-        src = P + (int64_t)(k0 + (tid >> 2)) * ldp + m0 + (tid & 3) * 64;
-      }
-    } else {
-      const int j = tid - 256;
-      if constexpr (BK) {
-        src = Q + (int64_t)(n0 + j) * ldq + k0;
-      } else {
-        const int64_t kr = IDX == 2 ? (int64_t)sidx[t * 64 + (j >> 2)] : (int64_t)(k0 + (j >> 2));
-        src = Q + kr * ldq + n0 + (j & 3) * 64;
-      }
-    }
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(touch_lds + (tid & ~63) * 4), 4, 0, 0);
   };
   bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
   auto read_a = [&](int t, int a) {
@@ -467,17 +433,11 @@ __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_
       if (more) pp::idx_rows<false>(sidx, 0, t + 1, tid, rq);
     }
     // phase 0: (a0, b0)
-    const bool tch = GM2_L2_TOUCH && touch_lds != nullptr && t + 2 < nk;
     read_a(t, 0);
     read_b(t, 0, fb0);
     if (more) {
       issue(t + 1, 0);
-      if (tch) {
-        touch(t + 2);
-        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // retires B1(t)
-      } else {
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires B1(t)
-      }
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires B1(t)
     } else {
       asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     }
@@ -490,8 +450,7 @@ __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_
     read_b(t, 1, fb1);
     if (more) {
       issue(t + 1, 1);
-      if (tch) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // retires A1(t)
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");      // retires A1(t)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires A1(t)
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -665,9 +624,7 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
       for (int i = threadIdx.x; i < kend - kbeg; i += C::NT) sidx[i] = g.qrow[kbeg + i];
       __syncthreads();
     }
-    // (the touch scratch follows the ring and the index table)
-    char* tlds = bn.touch ? smem + C::LDS + (IDX == 1 ? C::BM * 4 : IDX == 2 ? g.k_per_split * 4 : 0) : nullptr;
-    mainloop_pp<AK, BK, IDX>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc, sidx, tlds);
+    mainloop_pp<AK, BK, IDX>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc, sidx);
   } else {
     static_assert(IDX == 0, "zero-copy rows: ping-pong main loop only");
     mainloop<C, T, AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
@@ -1058,10 +1015,7 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
                                                 const uint32_t* __restrict__ xbits, int64_t ldxb,
                                                 const float* __restrict__ scal, T* __restrict__ dL, int64_t ldd,
                                                 float* __restrict__ loss_part, float* __restrict__ colpart,
-                                                int64_t ldcol, char* smem, const int32_t* __restrict__ xrows,
-                                                char* touch_lds);
-template <class C, typename T>
-constexpr int recon_lds_bytes();
+                                                int64_t ldcol, char* smem, const int32_t* __restrict__ xrows);
 
 // ntiles > 0: capped grid, workgroup wg takes tiles wg, wg + grid, ... (GM2_OPT_GRID_CAP bit 4)
 template <class C, typename T, bool PP, bool GRAD>
@@ -1070,20 +1024,19 @@ __global__ __launch_bounds__(C::NT) void k_gemm_recon_loss(GemmArgs<T> g, const 
                                                          int ntiles, const float* __restrict__ scal,
                                                          T* __restrict__ dL, int64_t ldd,
                                                          float* __restrict__ loss_part, float* __restrict__ colpart,
-                                                         int64_t ldcol, const int32_t* __restrict__ xrows, int touch) {
+                                                         int64_t ldcol, const int32_t* __restrict__ xrows) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   GM2_STAMP(0);
   const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
-  char* tlds = touch ? smem + recon_lds_bytes<C, T>() : nullptr;
   if (ntiles == 0) {
     recon_loss_tile<C, T, PP, GRAD>(tile_of<C>(tm, tn), g, bias, xbits, ldxb, scal, dL, ldd, loss_part, colpart,
-                                    ldcol, smem, xrows, tlds);
+                                    ldcol, smem, xrows);
     return;
   }
   for (int t = xcd_wg(); t < ntiles; t += gridDim.x) {
     __syncthreads();
     recon_loss_tile<C, T, PP, GRAD>(tile_at<C>(t, tm, tn, 0), g, bias, xbits, ldxb, scal, dL, ldd, loss_part,
-                                    colpart, ldcol, smem, xrows, tlds);
+                                    colpart, ldcol, smem, xrows);
   }
 }
 
@@ -1092,8 +1045,7 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
                                                 const uint32_t* __restrict__ xbits, int64_t ldxb,
                                                 const float* __restrict__ scal, T* __restrict__ dL, int64_t ldd,
                                                 float* __restrict__ loss_part, float* __restrict__ colpart,
-                                                int64_t ldcol, char* smem, const int32_t* __restrict__ xrows,
-                                                char* touch_lds) {
+                                                int64_t ldcol, char* smem, const int32_t* __restrict__ xrows) {
   constexpr bool FAST = sizeof(T) == 2;
   // (m = genes, n = strains)
   // LDS: [0, image / staging) | per-row-group dl sums | BCE, sum(p) slots | bias slice
@@ -1114,7 +1066,7 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
     for (int i = threadIdx.x; i < C::BN; i += C::NT) xidx[i] = xrows[tl.n0 + i];
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP)
-    mainloop_pp<true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc, nullptr, touch_lds);
+    mainloop_pp<true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   else
     mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   GM2_STAMP(2);
@@ -1477,14 +1429,11 @@ static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1
   // (zero-copy rows: the index table after the staging ring -- a tile's rows, or a split's k-rows)
   constexpr int table_max = IDX == 1 ? C::BM * 4 : IDX == 2 ? kMaxIdxRows * 4 : 0;
   static_assert(C::LDS + table_max <= 160 * 1024, "LDS budget");
-  StoreEpi ep = bn;
-  // L2 touch scratch (2 KB after the index table) where it fits the 160-KB LDS
-  const int base = C::LDS + (IDX == 1 ? C::BM * 4 : IDX == 2 ? a.k_per_split * 4 : 0);
-  ep.touch = PP && (opts().l2_touch & 1) && base + kTouchBytes <= 160 * 1024;
-  const int lds = base + (ep.touch ? kTouchBytes : 0);
+  const int lds = C::LDS + (IDX == 1 ? C::BM * 4 : IDX == 2 ? a.k_per_split * 4 : 0);
   if (IDX == 2 && a.k_per_split > kMaxIdxRows) throw Gm2Error("zero-copy rows: %d k-rows per split", a.k_per_split);
-  ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP, IDX>, std::min(160 * 1024, C::LDS + table_max + kTouchBytes));
+  ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP, IDX>, C::LDS + table_max);
   int grid = tiles;
+  StoreEpi ep = bn;
   if (bn.tail_S > 1) {  // split tail: one workgroup per item (plan_tail)
     grid = bn.tail_R + bn.tail_rem * bn.tail_S;
     ep.ntiles = 0;
@@ -1667,12 +1616,10 @@ static void recon_impl_k(const GemmArgs<T>& g, const float* bias, const uint32_t
     grid = (tiles + rounds - 1) / rounds;
     ntiles = grid < tiles ? tiles : 0;
   }
-  // L2 touch scratch after the kernel's own LDS (GM2_OPT_L2_TOUCH bit 2)
-  const int touch = PP && (opts().l2_touch & 2) && lds + kTouchBytes <= 160 * 1024 ? 1 : 0;
   auto go = [&](auto kern) {
-    ensure_lds_attr((const void*)kern, std::min(160 * 1024, lds + kTouchBytes));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(C::NT), lds + touch * kTouchBytes, s, g, bias, X, ldx, ntiles, scal,
-                       dL, ldd, loss_part, colpart, ldcol, xrows, touch);
+    ensure_lds_attr((const void*)kern, lds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(C::NT), lds, s, g, bias, X, ldx, ntiles, scal, dL, ldd, loss_part,
+                       colpart, ldcol, xrows);
   };
   if (with_grad) go(k_gemm_recon_loss<C, T, PP, true>);
   else go(k_gemm_recon_loss<C, T, PP, false>);

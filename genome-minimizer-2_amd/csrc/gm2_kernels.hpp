@@ -94,7 +94,6 @@ struct Options {
   int grad_buckets = 1;  // GM2_OPT_GRAD_BUCKETS  record the gradient-bucket events (gm2_wait_grad_bucket)
   int side_cus = 0;      // GM2_OPT_SIDE_CUS  CU mask of the side stream: this many CUs (0 = all)
   int small_tile = 128;  // GM2_OPT_SMALL_TILE  N width of the forward's hidden-layer tiles (128 or 64)
-  int l2_touch = 0;      // GM2_OPT_L2_TOUCH  bit 1: 256-tile store GEMMs, bit 2: the loss GEMM
 };
 // validated edit of one option (throws on an unknown key or a bad value)
 void option_set(Options& o, int key, int value);
@@ -138,7 +137,6 @@ struct StoreEpi {
   const float* beta = nullptr;
   int H = 0;
   int trans = 0;  // store C^T: C0[n * ldc + m] (no bias, no statistics, one K pass)
-  int touch = 0;  // ping-pong main loop touches K-tile t + 2 into L2 (GM2_OPT_L2_TOUCH; set by the launcher)
   // one K pass only: sq[tile] = sum of the squares of the values the tile stored (fp64), tile =
   // (m0 / BM) * (Np / BN) + n0 / BN -- the clip-norm statistics of a weight gradient taken as it is
   // written (gm2_grad_norm with GM2_S_NORM_AHEAD)

@@ -81,10 +81,6 @@ void option_set(Options& o, int key, int value) {
       if (value != 64 && value != 128) throw Gm2Error("small tile %d: 64 or 128", value);
       o.small_tile = value;
       break;
-    case GM2_OPT_L2_TOUCH:
-      if (value < 0 || value > 3) throw Gm2Error("L2 touch bits %d: 0..3", value);
-      o.l2_touch = value;
-      break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -108,7 +104,6 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_GRAD_BUCKETS: return o.grad_buckets;
     case GM2_OPT_SIDE_CUS: return o.side_cus;
     case GM2_OPT_SMALL_TILE: return o.small_tile;
-    case GM2_OPT_L2_TOUCH: return o.l2_touch;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

@@ -330,11 +330,7 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       Results are bit-identical.
  *   GM2_OPT_SMALL_TILE  N width of the 128-row tiles of the bf16 GEMMs whose operands are both
  *                       K-major (the forward's hidden layers): 128 (default) or 64 (two 72-KB
- *                       workgroups per CU). Results are bit-identical.
- *   GM2_OPT_L2_TOUCH    bit 1 = the 256x256-tile store GEMMs, bit 2 = the loss GEMM: each K-tile
- *                       of the ping-pong main loop also pulls the lines of the K-tile after next
- *                       into L2 (one 4-byte LDS-DMA load per thread into a 2-KB scratch), a
- *                       second K-tile in flight beside the 2-stage LDS ring. Bit-identical. */
+ *                       workgroups per CU). Results are bit-identical. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -352,8 +348,7 @@ enum {
   GM2_OPT_TAIL_SPLIT = 14,
   GM2_OPT_GRAD_BUCKETS = 15,
   GM2_OPT_SIDE_CUS = 16,
-  GM2_OPT_SMALL_TILE = 17,
-  GM2_OPT_L2_TOUCH = 18
+  GM2_OPT_SMALL_TILE = 17
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);

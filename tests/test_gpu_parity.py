@@ -503,8 +503,8 @@ def test_capped_grid_bit_identical(G):
 @pytest.mark.parametrize("G", [20480, 16500])
 def test_backward_schedule_options_bit_identical(G):
     """GM2_OPT_DW9_LAST (output-layer weight gradient forked beside the input-layer one) and
-    GM2_OPT_SIDE_PRIORITY (low / high side stream), GM2_OPT_SIDE_CUS (CU-masked side stream) and
-    GM2_OPT_L2_TOUCH (extra L2 loads in the 256-tile main loops) only reorder launches or loads: gradients, loss record and
+    GM2_OPT_SIDE_PRIORITY (low / high side stream) and GM2_OPT_SIDE_CUS (CU-masked side stream)
+    only reorder launches: gradients, loss record and
     clip statistics are bit-identical to the default schedule, with the one-launch and the
     four-quarter input-layer gradient."""
     H, L, B = 1024, 32, 1024
@@ -514,16 +514,14 @@ def test_backward_schedule_options_bit_identical(G):
     sc = scalars(beta=0.37, wgamma=0.55, lam=0.0)
     sc[native.S_NORM_AHEAD] = 1.0
     outs = []
-    for last, prio, chunks, scus, touch in ((0, 0, 1, 0, 0), (1, 0, 1, 0, 0), (1, 1, 1, 0, 0), (1, -1, 4, 0, 0),
-                                            (0, 1, 4, 0, 0), (0, 0, 1, 192, 0), (1, 0, 4, 64, 0), (0, 0, 1, 0, 3),
-                                            (1, 0, 4, 0, 1)):
+    for last, prio, chunks, scus in ((0, 0, 1, 0), (1, 0, 1, 0), (1, 1, 1, 0), (1, -1, 4, 0), (0, 1, 4, 0),
+                                     (0, 0, 1, 192), (1, 0, 4, 64)):
         m = to_model(P, S, G, H, L, native.GM2_BF16)
         mat = ResidentMatrix(X)
         ws = m.workspace(native.GM2_BF16, B)
         ws.set_option(native.OPT_DW9_LAST, last)
         ws.set_option(native.OPT_SIDE_PRIORITY, prio)
         ws.set_option(native.OPT_SIDE_CUS, scus)
-        ws.set_option(native.OPT_L2_TOUCH, touch)
         ws.set_option(native.OPT_INPUT_CHUNKS, chunks)
         grads = torch.zeros_like(m.params)
         loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
@@ -556,15 +554,12 @@ def test_zero_copy_rows_bit_identical(G, B, rows_none):
     rows = [None if rows_none else torch.randperm(S, generator=gen)[:B].to(torch.int32).cuda() for _ in range(3)]
     eps = [torch.randn(B, L, generator=gen).cuda() for _ in range(3)]
     outs = []
-    # (the third run: the in-place path with the L2 touch of the 256-tile main loops, GM2_OPT_L2_TOUCH,
-    # whose touch addresses go through the same row / k-row tables)
-    for zero_copy, touch in ((False, 0), (True, 0), (True, 3)):
+    for zero_copy in (False, True):
         m = to_model(P, Sb, G, H, L, native.GM2_BF16)
         mat = ResidentMatrix(X)
         res = mat.operands(native.GM2_BF16) if zero_copy else None
         data = torch.zeros_like(mat.data) if zero_copy else mat.data
         ws = m.workspace(native.GM2_BF16, B)
-        ws.set_option(native.OPT_L2_TOUCH, touch)
         grads = torch.zeros_like(m.params)
         mom, vel = torch.zeros_like(m.params), torch.zeros_like(m.params)
         out = []
@@ -580,9 +575,8 @@ def test_zero_copy_rows_bit_identical(G, B, rows_none):
         ws.join()
         torch.cuda.synchronize()
         outs.append(out + [m.params.clone(), m.bn.clone(), mom.clone(), vel.clone()])
-    for o in outs[1:]:
-        for a, b in zip(outs[0], o):
-            assert torch.equal(a, b)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 def test_grad_bucket_events_off_bit_identical():
