@@ -2,6 +2,7 @@
 // train / eval / sample hot path. Host-side only; kernels live in gemm.hip and kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -105,6 +106,11 @@ struct Layout {
   int tails;
 };
 
+#ifdef GM2_DEBUG
+// (offset, bytes) of every region the last make_layout on this thread took (gm2_debug_check_layout)
+thread_local std::vector<std::pair<int64_t, int64_t>> t_regions;
+#endif
+
 Layout make_layout(const gm2_dims* gd, int prec) {
   if (prec != GM2_F32 && prec != GM2_BF16) throw Gm2Error("bad precision %d", prec);
   Layout o;
@@ -113,9 +119,16 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.es = prec == GM2_F32 ? 4 : 2;
   const Dims& d = o.d;
   int64_t cur = 0;
+#ifdef GM2_DEBUG
+  t_regions.clear();
+#endif
   auto take = [&](int64_t bytes) {
     const int64_t at = cur;
+    if (bytes < 0) throw Gm2Error("layout: negative region (%lld bytes)", (long long)bytes);
     cur += round_up(bytes, 256);
+#ifdef GM2_DEBUG
+    t_regions.emplace_back(at, bytes);
+#endif
     return at;
   };
   const int64_t es = o.es, H = d.H, Bm = d.Bm;
@@ -195,6 +208,7 @@ struct Ctx {
   int64_t ld_xres = 0;
   const uint32_t* xbres = nullptr;
   int64_t ld_xbres = 0;
+  int64_t res_rows = 0;  // rows of the resident operands (their zero row included): bounds of ridx
   Ctx(const Layout& l, void* w, void* strm, WsState* state = nullptr)
       : lo(l), ws((char*)w), s((hipStream_t)strm), d(l.d), slab_off(l.slabs), slab_cap(l.slab_cap), xo(l.X),
         xbo(l.XB), st(state) {}
@@ -209,6 +223,7 @@ struct Ctx {
     c.ld_xres = ld_xres;
     c.xbres = xbres;
     c.ld_xbres = ld_xbres;
+    c.res_rows = res_rows;
     return c;
   }
   T* t(int64_t off) const { return (T*)(ws + off); }
@@ -414,7 +429,20 @@ void ws_release(void* ws) {
   std::lock_guard<std::mutex> lk(ws_mutex());
   auto it = ws_map().find(ws);
   if (it == ws_map().end()) return;
-  it->second->destroy();
+  WsState& st = *it->second;
+  // a deferred output-layer update must not be lost (queued) nor outlive the workspace memory it
+  // reads its scalars from (running): launch a queued one and wait for it before the state goes
+  if (st.qadam.queued) {
+    const hipStream_t s = st.side ? st.side : nullptr;
+    st.launch_queued(s);
+    HIP_OK(hipStreamSynchronize(s));
+    st.adam9_pending = false;
+  }
+  if (st.adam9_pending) {
+    HIP_OK(hipEventSynchronize(st.adam9_done));
+    st.adam9_pending = false;
+  }
+  st.destroy();
   ws_map().erase(it);
 }
 
@@ -436,6 +464,7 @@ int gemm_to_slabs(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, 
                   int K, int64_t ldc, int pk = 1, int qk = 1, const int32_t* prow = nullptr) {
   GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0, pk, qk};
   g.prow = prow;
+  if (prow) g.idx_lim = c.res_rows;
   const int S = plan_gemm<T>(g).splits;
   const int64_t slab = (int64_t)Mp * ldc;
   if ((int64_t)S * slab > c.slab_cap) throw Gm2Error("slab capacity exceeded");
@@ -449,6 +478,7 @@ void gemm_to(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, int64
              float* C0, float* C1, int msplit, int64_t ldc, int pk = 1, int qk = 1, const int32_t* qrow = nullptr) {
   GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0, pk, qk};
   g.qrow = qrow;
+  if (qrow) g.idx_lim = c.res_rows;
   int S = plan_gemm<T>(g).splits;
   const int64_t slab = round_up((int64_t)M * N, 4);
   if ((int64_t)S * slab > c.slab_cap) S = 1;
@@ -488,6 +518,7 @@ BigGrads<T> big_grads(const Ctx<T>& c, int Bp) {
     r.g0.Q = c.xres;
     r.g0.ldq = c.ld_xres;
     r.g0.qrow = c.ridx;
+    r.g0.idx_lim = c.res_rows;
   }
   r.direct = plan_gemm<T>(r.g9).splits == 1 && plan_gemm<T>(r.g0).splits == 1;
   r.n9 = gemm_tiles<T>(r.g9);
@@ -657,6 +688,7 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   // deferred output-layer Adam update of the previous step (side stream) must be complete here.
   if (c.st) c.st->join(c.s);
   GemmArgs<T> g{c.t(l.sD3), H, c.t(l.A[5]), H, (int)d.G, B, H, (int)d.Gp, Bp, 0};
+  if (c.ridx) g.idx_lim = c.res_rows;
   if (c.ridx)
     launch_gemm_recon_loss<T>(g, prm + d.off[D9B], c.xbres, c.ld_xbres, with_grad, scal, c.t(l.dL), d.Gp,
                               c.f(l.losspart), c.f(l.colpart), d.Gp, c.s, c.ridx);
@@ -756,9 +788,10 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       *fwd_tail = nullptr;
     }
   };
+  // (the forward tail goes BEHIND dW9 on the side stream: in front of it, starved beside dA5's
+  // workgroups, it held dW9's start ~30 us past dA5's end, profiles/r03_step_timeline_head.txt)
   auto output_weight_grad = [&] {
     fork();
-    tail_on(w.s);
     const GemmArgs<T>& g9 = bg.g9;
     if (plan_gemm<T>(g9).splits == 1) {
       // (A5^T here on the side stream; on the main stream before the fork measured ~35 us/step
@@ -769,6 +802,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     } else {
       gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
     }
+    tail_on(w.s);  // (the output bias gradient: bucket 0 as well)
     if (st.opt.grad_buckets) HIP_OK(hipEventRecord(st.bucket[0], w.s));
   };
   // GM2_OPT_DW9_LAST: forked beside the input-layer dWe0 GEMM instead, so the hidden-layer chain
@@ -984,6 +1018,7 @@ void run_train(const Layout& lo, const gm2_batch* b, const float* prm, float* gr
     c.ld_xres = b->ld_resident;
     c.xbres = b->resident_bits;
     c.ld_xbres = b->ld_resident_bits;
+    c.res_rows = b->resident_rows + 1;
     drop_stage(st, c.s);
     std::function<void(hipStream_t)> tail;
     forward<T>(c, b, prm, bn, 1, 1, scal, loss, gr, nullptr, 0, nullptr, 0.5f, true, false, &tail);
@@ -1395,6 +1430,7 @@ int gm2_reparameterize(int64_t n, const float* mu, const float* logvar, const fl
   return guarded([&] {
     if (!mu || !logvar || !eps || (!z && !dz) || (dz && (!dmu || !dlogvar)))
       throw Gm2Error("reparameterize: bad pointers");
+    if (n < 0) throw Gm2Error("reparameterize: negative n %lld", (long long)n);
     launch_reparameterize(n, mu, logvar, eps, z, dz, dmu, dlogvar, (hipStream_t)stream);
   });
 }
@@ -1452,5 +1488,47 @@ int gm2_timing_begin(int kernel_classes) {
 int gm2_timing_end(double* total_ms, int64_t* launches) {
   return guarded([&] { timing_end(total_ms, launches); });
 }
+
+#ifdef GM2_DEBUG
+// ---- debug build only (include/gm2_debug.h) ----
+int gm2_debug_flags(unsigned* flags) {
+  return guarded([&] {
+    if (!flags) throw Gm2Error("null flags");
+    *flags = dbg_take_kernels() | dbg_take_gemm() | dbg_take_masks();
+  });
+}
+
+int gm2_debug_check_layout(const gm2_dims* d, int precision, int64_t* n_regions, int64_t* total) {
+  return guarded([&] {
+    const Layout o = make_layout(d, precision);
+    auto r = t_regions;
+    std::sort(r.begin(), r.end());
+    int64_t end = 0;
+    for (const auto& x : r) {
+      if (x.first % 256) throw Gm2Error("region at %lld not 256-B aligned", (long long)x.first);
+      if (x.first < end) throw Gm2Error("region at %lld overlaps the previous one (ends %lld)", (long long)x.first, (long long)end);
+      end = x.first + x.second;
+      if (end > o.total) throw Gm2Error("region at %lld (+%lld) past the total %lld", (long long)x.first, (long long)x.second, (long long)o.total);
+    }
+    // every named offset of the layout is one of the regions
+    const int64_t named[] = {o.sE0, o.sE1, o.sE2, o.sHD, o.sD0, o.sD1, o.sD2, o.sD3, o.X, o.XB, o.HD, o.Z, o.dL,
+                             o.slabs, o.side_slabs, o.DA, o.dH, o.AT5, o.dYT0, o.bnpart, o.colpart, o.losspart,
+                             o.klpart, o.gradpart, o.colbwd, o.nahdr, o.nasq, o.clip, o.scal0, o.X1, o.XB1, o.syncb,
+                             o.adamscal, o.ridx, o.tailp9, o.tailc9, o.tailp0, o.tailc0};
+    auto known = [&](int64_t off) {
+      for (const auto& x : r)
+        if (x.first == off) return true;
+      return false;
+    };
+    for (int64_t off : named)
+      if (!known(off)) throw Gm2Error("named offset %lld is not a region start", (long long)off);
+    for (int i = 0; i < 6; ++i)
+      if (!known(o.Y[i]) || !known(o.A[i]) || !known(o.save[i]) || !known(o.dY[i]))
+        throw Gm2Error("layer %d offsets are not region starts", i);
+    if (n_regions) *n_regions = (int64_t)r.size();
+    if (total) *total = o.total;
+  });
+}
+#endif
 
 }  // extern "C"

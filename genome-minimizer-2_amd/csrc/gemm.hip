@@ -614,14 +614,21 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
     kend = min(g.K, kbeg + per * E<T>::KT);
   }
   const int nk = (kend - kbeg) / E<T>::KT;
+  GM2_DBG(tl.m0 + C::BM <= g.Mp && tl.n0 + C::BN <= g.Np && kbeg >= 0 && kend <= g.K, kDbgTile);
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP) {
     int* sidx = (int*)(smem + C::LDS);
     if constexpr (IDX == 1) {
-      for (int i = threadIdx.x; i < C::BM; i += C::NT) sidx[i] = g.prow[tl.m0 + i];
+      for (int i = threadIdx.x; i < C::BM; i += C::NT) {
+        sidx[i] = g.prow[tl.m0 + i];
+        GM2_DBG(sidx[i] >= 0 && (g.idx_lim == 0 || sidx[i] < g.idx_lim), kDbgGemmIdx);
+      }
       __syncthreads();
     } else if constexpr (IDX == 2) {
-      for (int i = threadIdx.x; i < kend - kbeg; i += C::NT) sidx[i] = g.qrow[kbeg + i];
+      for (int i = threadIdx.x; i < kend - kbeg; i += C::NT) {
+        sidx[i] = g.qrow[kbeg + i];
+        GM2_DBG(sidx[i] >= 0 && (g.idx_lim == 0 || sidx[i] < g.idx_lim), kDbgGemmIdx);
+      }
       __syncthreads();
     }
     mainloop_pp<AK, BK, IDX>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc, sidx);
@@ -1063,7 +1070,11 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
     bias_s[i] = FAST ? b * -1.4426950408889634f : b;
   }
   if (xrows)
-    for (int i = threadIdx.x; i < C::BN; i += C::NT) xidx[i] = xrows[tl.n0 + i];
+    for (int i = threadIdx.x; i < C::BN; i += C::NT) {
+      xidx[i] = xrows[tl.n0 + i];
+      GM2_DBG(xidx[i] >= 0 && (g.idx_lim == 0 || xidx[i] < g.idx_lim), kDbgReconRows);
+    }
+  GM2_DBG(tl.m0 + C::BM <= g.Mp && tl.n0 + C::BN <= g.Np, kDbgTile);
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP)
     mainloop_pp<true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
@@ -1712,5 +1723,9 @@ template void launch_gemm_mask<float>(const GemmArgs<float>&, const float*, uint
                                       hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float);
 template void launch_gemm_mask<bf16_t>(const GemmArgs<bf16_t>&, const float*, uint8_t*, int64_t, float*, int64_t,
                                        hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float);
+
+#ifdef GM2_DEBUG
+GM2_DBG_TAKE_FN(dbg_take_gemm)
+#endif
 
 }  // namespace gm2

@@ -55,4 +55,40 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // sigmoid_fp32(l) > 0.5  <=>  l > 0x33C00000 (pinned against the reference in tests/golden)
 constexpr float kMaskLogitThreshold = 8.940696716308594e-08f;
 
+// ---- debug build (build_native.py --variant debug: -DGM2_DEBUG -> gm2/libgm2_debug.so) ----
+// Device-side bounds checks of the index data the kernels follow (gather rows, zero-copy row
+// tables, loss target rows, mask group positions, CSR offsets). A failed check ORs its bit into
+// this translation unit's flag word with a vector atomic (no trap: the kernel finishes and the
+// results are whatever the bad index produced); gm2_debug_flags() reads and clears every unit's word.
+enum DebugBit : unsigned {
+  kDbgResidentRows = 1u,   // k_resident_rows: rows[i] outside [0, S)
+  kDbgGatherRows = 2u,     // k_gather: a negative row index
+  kDbgGemmIdx = 4u,        // GEMM zero-copy row table: entry outside [0, idx_lim)
+  kDbgMaskPos = 8u,        // k_count_groups: group offsets not ascending / position outside the row
+  kDbgCompact = 16u,       // k_compact: an index written outside [off[row], off[row + 1])
+  kDbgReconRows = 32u,     // loss epilogue: target-bit row outside [0, idx_lim)
+  kDbgTile = 64u,          // a GEMM tile origin outside the padded operand extents
+};
+#ifdef GM2_DEBUG
+namespace {
+__device__ unsigned int g_dbg_flags;  // one per translation unit
+}
+#define GM2_DBG(cond, bit)                                                                           \
+  do {                                                                                              \
+    if (!(cond)) __hip_atomic_fetch_or(&g_dbg_flags, (unsigned)(bit), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+  } while (0)
+// host: this unit's flags, cleared (defines `unsigned fn()`)
+#define GM2_DBG_TAKE_FN(fn)                                                                          \
+  unsigned fn() {                                                                                   \
+    unsigned v = 0, z = 0;                                                                          \
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_dbg_flags), sizeof v) != hipSuccess) return 0x80000000u; \
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_flags), &z, sizeof z) != hipSuccess) return 0x80000000u;   \
+    return v;                                                                                       \
+  }
+#else
+#define GM2_DBG(cond, bit) \
+  do {                     \
+  } while (0)
+#endif
+
 }  // namespace gm2

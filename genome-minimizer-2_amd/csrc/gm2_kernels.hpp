@@ -69,6 +69,9 @@ struct GemmArgs {
   // of m / k -- the input layer's GEMMs read the resident matrix's rows in place (gm2_batch.resident)
   const int32_t* prow = nullptr;
   const int32_t* qrow = nullptr;
+  // rows of the buffer prow / qrow (and the loss epilogue's target rows) index: 0 = unknown (the
+  // GM2_DEBUG build's bounds check then tests >= 0 only)
+  int64_t idx_lim = 0;
 };
 
 // ---- tuning options (gm2.h GM2_OPT_*): results are bit-identical under every value but tail_split ----
@@ -327,5 +330,12 @@ void launch_grad_finalize(const double* part, int nblocks, const float* scal, fl
                           double* loss_slots, const NormAhead& na, hipStream_t s);
 
 int grad_stats_blocks(int64_t n);
+
+#ifdef GM2_DEBUG
+// read-and-clear the debug flag word of each translation unit (gm2_common.hpp DebugBit)
+unsigned dbg_take_kernels();
+unsigned dbg_take_gemm();
+unsigned dbg_take_masks();
+#endif
 
 }  // namespace gm2

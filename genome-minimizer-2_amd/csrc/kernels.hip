@@ -51,6 +51,7 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ data
     v[k] = u32x2{0u, 0u};
     if (rd && r < B) {
       const int64_t src = rows ? (int64_t)rows[r] : (int64_t)r;
+      GM2_DBG(src >= 0, kDbgGatherRows);
       v[k] = __builtin_nontemporal_load((const u32x2*)(data + src * ld_data + c));
     }
   }
@@ -1172,6 +1173,7 @@ __global__ __launch_bounds__(256) void k_resident_rows(const int32_t* __restrict
                                                      int32_t* __restrict__ ridx) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < nfill) ridx[i] = i < n ? (rows ? rows[i] : i) : zero_row;
+  if (rows && i < n) GM2_DBG(rows[i] >= 0 && rows[i] < zero_row, kDbgResidentRows);
 }
 
 void launch_resident_rows(const int32_t* rows, int n, int nfill, int64_t S, int32_t* ridx, hipStream_t s) {
@@ -1361,5 +1363,9 @@ void launch_grad_finalize(const double* part, int nblocks, const float* scal, fl
 GM2_INST(float)
 GM2_INST(bf16_t)
 #undef GM2_INST
+
+#ifdef GM2_DEBUG
+GM2_DBG_TAKE_FN(dbg_take_kernels)
+#endif
 
 }  // namespace gm2

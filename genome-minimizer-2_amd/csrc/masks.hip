@@ -33,8 +33,10 @@ __global__ __launch_bounds__(256) void k_count_groups(const uint8_t* __restrict_
   int cnt = 0;
   for (int gi = lane; gi < ngroups; gi += 64) {
     int any = 0;
+    GM2_DBG(goff[gi] >= 0 && goff[gi] <= goff[gi + 1], kDbgMaskPos);
     for (int k = goff[gi]; k < goff[gi + 1] && !any; ++k) {
       const int p = pos[k];
+      GM2_DBG(p >= 0 && (int64_t)(p >> 3) < ldb, kDbgMaskPos);
       any = (r[p >> 3] >> (p & 7)) & 1;
     }
     cnt += any;
@@ -115,6 +117,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ bit
     int64_t dst = out + pre - c;
     while (w) {
       const int b = __builtin_ctz(w);
+      GM2_DBG(dst >= off[row] && dst < off[row + 1], kDbgCompact);
       idx[dst++] = (int32_t)(wi * 32 + b);
       w &= w - 1;
     }
@@ -148,5 +151,9 @@ void launch_compact(const uint8_t* bits, int64_t n, int64_t ldb, const uint8_t* 
   hipLaunchKernelGGL(k_compact, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, bits, n, ldb, keep, offsets, idx);
   GM2_CHECK_LAUNCH();
 }
+
+#ifdef GM2_DEBUG
+GM2_DBG_TAKE_FN(dbg_take_masks)
+#endif
 
 }  // namespace gm2

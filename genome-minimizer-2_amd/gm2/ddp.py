@@ -61,15 +61,70 @@ def rank_share(n, rank, world):
     return (n * rank) // active, (n * (rank + 1)) // active
 
 
+def train_rows_cap(batch_size, world, sync_bn=False):
+    """Rows the training workspace of one rank must hold: the largest share rank_share (or
+    rank_slice under SyncBN) can give for any global batch of n <= batch_size rows. With
+    n >= 2 world the shares are <= ceil(n / world); below that n // 2 ranks share n rows, i.e. 2 or
+    3 each (e.g. a ragged last batch of 3 rows on 16 ranks: one rank gets all 3)."""
+    cap = -(-batch_size // world)
+    return cap if sync_bn or world <= 1 else max(cap, min(3, batch_size))
+
+
+def bf16_exchange_sum(dist, x, scratch=None):
+    """SUM over the ranks of the fp32 vector x (every rank's own), moved as bf16 and accumulated in
+    fp32: each rank rounds its x to bf16 once, sends chunk j to rank j (all-to-all), rank j sums the
+    world's chunks IN RANK ORDER in fp32 and rounds that sum to bf16 once, and an all-gather hands
+    every rank every chunk. Bytes per rank: 2 x (world-1)/world x 2 B per element, the same as a
+    bf16 ring all-reduce; but the error no longer grows with the ring's per-hop bf16 rounding:
+        |result - sum_r x_r| <= 2^-8 (1.001 sum_r |x_r| + |sum_r x_r|)   (elementwise, any world)
+    (bf16 keeps 8 significant bits, unit roundoff 2^-8: each x_r is rounded once, the fp32 sum adds
+    at most world x 2^-24 of sum_r |x_r|, and the sum is rounded once),
+    and every rank gets identical values. Returns the reduced vector (fp32, x's device) in x.
+    `scratch`: optional dict reused across calls for the bf16 buffers.
+    gloo with device tensors (the one-GPU rehearsal tests) stages the two collectives through host
+    memory; RCCL runs them on the device."""
+    world = dist.get_world_size()
+    n = x.numel()
+    c = -(-n // world)
+    sc = scratch if scratch is not None else {}
+    if sc.get("n", 0) < world * c or sc["send"].device != x.device:
+        for k in ("send", "recv", "gath"):
+            sc[k] = torch.empty(world * c, dtype=torch.bfloat16, device=x.device)
+        sc["n"] = world * c
+    send, recv, gath = sc["send"][:world * c], sc["recv"][:world * c], sc["gath"][:world * c]
+    send[:n].copy_(x)
+    send[n:].zero_()
+    host = x.is_cuda and dist.get_backend() == "gloo"
+    if host:
+        hs, hr = send.cpu(), torch.empty(world * c, dtype=torch.bfloat16)
+        dist.all_to_all_single(hr, hs)
+        recv.copy_(hr)
+    else:
+        dist.all_to_all_single(recv, send)
+    parts = recv.view(world, c)
+    acc = parts[0].float()
+    for r in range(1, world):  # rank order: the same value on every rank, run to run
+        acc.add_(parts[r].float())
+    mine = acc.to(torch.bfloat16)
+    if host:
+        hg = [torch.empty(c, dtype=torch.bfloat16) for _ in range(world)]
+        dist.all_gather(hg, mine.cpu())
+        gath.copy_(torch.cat(hg))
+    else:
+        dist.all_gather_into_tensor(gath, mine)
+    x.copy_(gath[:n])
+    return x
+
+
 class GradSync:
     """Bucketed SUM all-reduce of the flat gradient buffer, overlapped with the backward.
 
-    exchange="f32" (default) all-reduces the fp32 gradient as it is. exchange="bf16" sends the two
+    exchange="f32" (default) all-reduces the fp32 gradient as it is. exchange="bf16" moves the two
     big weight gradients (buckets 0 and 2..5: decoder.9 and encoder.0, ~96 % of the bytes of v0) as
-    bf16 and sums them in bf16 over the ranks (half the bytes on xGMI; each element carries the
-    rounding of its per-rank values and of the ring's partial sums, ~2^-9 relative per addition);
-    the hidden/BN bucket stays fp32. The result is identical on every rank, and clip / L1 / Adam run
-    on it in fp32 as before."""
+    bf16 with an fp32 accumulation (bf16_exchange_sum: all-to-all, fp32 sum in rank order, all-gather
+    -- half the bytes on xGMI, and an error bound independent of the world size); the hidden/BN
+    bucket stays fp32. The result is identical on every rank, and clip / L1 / Adam run on it in fp32
+    as before."""
 
     def __init__(self, dist, model, grads, exchange="f32"):
         if exchange not in ("f32", "bf16"):
@@ -77,8 +132,7 @@ class GradSync:
         self.dist = dist
         self.grads = grads
         self.exchange = exchange
-        self.buf = torch.empty(grads.numel(), dtype=torch.bfloat16, device=grads.device) \
-            if exchange == "bf16" else None
+        self.scratch = {}
         self.bounds = native.grad_bucket_bounds(native.dims(model.input_dim, model.hidden_dim,
                                                             model.latent_dim, 1))
         self.stream = torch.cuda.Stream(device=grads.device)
@@ -102,11 +156,8 @@ class GradSync:
             for b, (lo, hi) in enumerate(self.bounds):
                 if ran:
                     native.wait_grad_bucket(ws, b, self.stream)
-                if self.buf is not None and b != 1:
-                    t = self.buf[lo:hi]
-                    t.copy_(self.grads[lo:hi])
-                    self.dist.all_reduce(t)
-                    self.grads[lo:hi].copy_(t)
+                if self.exchange == "bf16" and b != 1:
+                    bf16_exchange_sum(self.dist, self.grads[lo:hi], self.scratch)
                 else:
                     self.dist.all_reduce(self.grads[lo:hi])
         cur.wait_stream(self.stream)

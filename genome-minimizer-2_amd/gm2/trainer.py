@@ -28,6 +28,7 @@ import torch
 from . import native
 from .data import StrainLoader, as_strain_loader
 from .ddp import (GradSync, average_running_stats, enable_sync_bn, get_dist, rank_share, rank_slice, rank_world,
+                  train_rows_cap,
                   reduce_loss_rows)
 from .loss_components import (GeneAbundanceLoss, KLDivergenceLoss, L1RegularizationLoss, LossComponent,
                               ReconstructionLoss, fused_supported)
@@ -260,6 +261,10 @@ class VAETrainer:
         batches = list(loader)
         totals = {name: 0.0 for name in (self.loss_tracker.train_losses if training else self.loss_tracker.val_losses)}
         ws = model.workspace(model.precision, loader.batch_size)
+        # (a fused epoch on this workspace may have left the output-layer update deferred: it would
+        # keep a pointer to model.params.grad, which zero_grad() frees -- run this loop undeferred)
+        ws.join()
+        ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, 0)
         rec = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device=self.device)
         model.requires_grad_(training)
         try:
@@ -287,6 +292,7 @@ class VAETrainer:
                 for k, v in parts.items():
                     totals[k] += v
         finally:
+            ws.join()
             model.requires_grad_(False)
             model.zero_grad()
         if training and batches:
@@ -316,10 +322,11 @@ class VAETrainer:
             pers.append(per)
             srows.append(self._scalar_row(sc, self.optimizer.step_count + bi + 1, norm_ahead=dist is None))
         scal = self._upload(srows)
-        ws = model.workspace(model.precision, (loader.batch_size + world - 1) // world)
+        sync_bn = dist is not None and self.sync_bn
+        # (rank_share gives a rank up to 3 rows of a batch smaller than 2 x world: train_rows_cap)
+        ws = model.workspace(model.precision, train_rows_cap(loader.batch_size, world, sync_bn))
         rec = torch.zeros(max(nb, 1), native.LOSS_SLOTS, dtype=torch.float64, device=self.device)
         sync = self._grad_sync(dist) if dist else None
-        sync_bn = dist is not None and self.sync_bn
         # the output layer's Adam update runs beside the next batch's hidden layers
         # (GM2_OPT_DEFER_OUTPUT_ADAM, bit-identical; the loop below joins it before touching the
         # gradient buffer itself and at the end of the epoch). Under DDP too: the queued update reads
@@ -360,6 +367,11 @@ class VAETrainer:
             model.shadows_current(model.precision)
             self._bump_bn()
         ws.join()  # (a deferred output-layer update, GM2_OPT_DEFER_OUTPUT_ADAM, if one was asked for)
+        # the epoch's options end with it: later calls on this workspace (autograd forward, eval,
+        # sampling on rank 0 only) neither defer an update nor issue SyncBN collectives
+        ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, 0)
+        if sync_bn:
+            ws.set_option(native.OPT_SYNC_BN, 0)
         if dist:
             reduce_loss_rows(dist, rec)
             if not sync_bn:  # (SyncBN: every rank applied the same global-batch updates)

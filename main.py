@@ -93,6 +93,13 @@ def check_data_availability(root):
     return True
 
 
+PRECISION_NOTE = {
+    "bf16": "bf16 GEMM operands, fp32 accumulation; fp32 master weights, BatchNorm, losses and Adam "
+            "(--precision f32: the reference's fp32 arithmetic)",
+    "f32": "fp32 throughout (the reference's arithmetic)",
+}
+
+
 def _precision(args):
     from gm2 import native
     return native.GM2_F32 if args.precision == "f32" else native.GM2_BF16
@@ -106,7 +113,10 @@ def run_single_experiment(args):
         config.n_epochs = args.epochs
     print(f"\n{'=' * 80}\nRunning {config.experiment_name} experiment")
     print(f"Hidden dim: {config.hidden_dim}, Latent dim: {config.latent_dim}")
-    print(f"Epochs: {config.n_epochs}, Trainer: {config.trainer_version}\n{'=' * 80}")
+    print(f"Epochs: {config.n_epochs}, Trainer: {config.trainer_version}")
+    # (not in the reference's header: its arithmetic is fp32 throughout; this build's default is
+    # bf16 GEMMs -- pass --precision f32 for the reference's arithmetic)
+    print(f"Precision: {PRECISION_NOTE[args.precision]}\n{'=' * 80}")
     paths = data_paths(args.project_root)
     runner = IntegratedExperimentRunner(config, project_root=args.project_root, precision=_precision(args),
                                         dataset_csv=paths["Main Dataset"], phylogroups_csv=paths["Phylogroups"])

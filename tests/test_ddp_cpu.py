@@ -159,3 +159,74 @@ def test_gather_rows_reassembles_the_sharded_rows(tmp_path, world, n):
     full = np.arange(n * 5, dtype=np.int32).reshape(n, 5)
     for r in range(world):
         np.testing.assert_array_equal(np.load(tmp_path / f"g{r}.npy"), full)
+
+
+def _bf16_worker(rank, world, port, out_dir, n):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from gm2.ddp import bf16_exchange_sum
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x = _rank_grad(rank, n)
+    scratch = {}
+    for _ in range(2):  # second call reuses the scratch buffers
+        y = bf16_exchange_sum(dist, x.clone(), scratch)
+    np.save(os.path.join(out_dir, f"x{rank}.npy"), y.numpy())
+    dist.destroy_process_group()
+
+
+def _rank_grad(rank, n):
+    """A weight-gradient-like bucket per rank: a shared signal (every rank's share of the batch sees
+    the same trend) plus rank-specific heavy-tailed noise of both signs, so sums cancel in places,
+    and exact zeros (padded rows / columns of the real buckets)."""
+    g = torch.Generator().manual_seed(1000 + rank)
+    base = torch.Generator().manual_seed(7)
+    common = torch.randn(n, generator=base) * 1e-3
+    noise = torch.randn(n, generator=g) * torch.exp(2.0 * torch.randn(n, generator=g)) * 1e-3
+    x = common + noise
+    x[::97] = 0.0
+    return x
+
+
+@pytest.mark.parametrize("world", [8])
+def test_bf16_exchange_eight_ranks_bounded(tmp_path, world):
+    """gm2.ddp.bf16_exchange_sum across 8 processes (the N > 1 bench default moves the big weight
+    buckets this way): every rank ends with identical values; they equal the emulation of the method
+    bit for bit (each rank's bucket rounded to bf16, fp32 sum in rank order, one bf16 rounding); and
+    the stated bound holds elementwise against the fp64 sum of the fp32 buckets:
+        |result - sum_r x_r| <= 2^-8 (1.001 sum_r |x_r| + |sum_r x_r|)
+    -- independent of the world size (a bf16 ring all-reduce rounds its partial sum at each of its
+    world - 1 hops)."""
+    n = (1 << 18) + 13  # not a multiple of the world: the last chunk is padded
+    port = _free_port()
+    mp.spawn(_bf16_worker, args=(world, port, str(tmp_path), n), nprocs=world, join=True)
+    got = [np.load(tmp_path / f"x{r}.npy") for r in range(world)]
+    for r in range(1, world):
+        np.testing.assert_array_equal(got[r], got[0])
+    xs = [_rank_grad(r, n) for r in range(world)]
+    acc = xs[0].to(torch.bfloat16).float()
+    for r in range(1, world):
+        acc = acc + xs[r].to(torch.bfloat16).float()
+    np.testing.assert_array_equal(got[0], acc.to(torch.bfloat16).float().numpy())
+    s = sum(x.double() for x in xs).numpy()
+    a = sum(x.double().abs() for x in xs).numpy()
+    err = np.abs(got[0].astype(np.float64) - s)
+    bound = 2.0 ** -8 * (1.001 * a + np.abs(s))
+    assert np.all(err <= bound), float(np.max(err / np.maximum(bound, 1e-300)))
+    # and the bound is not vacuous: the typical error is far inside it
+    assert np.median(err[a > 0] / bound[a > 0]) < 0.25
+
+
+def test_train_rows_cap_holds_every_share():
+    """The training workspace capacity (gm2.ddp.train_rows_cap) holds every rank's share
+    (rank_share, or rank_slice under SyncBN) of every global batch n <= batch_size -- including a
+    batch smaller than 2 x world, where n // 2 ranks share n rows (ADVICE r03)."""
+    from gm2.ddp import train_rows_cap
+    for world in (1, 2, 3, 8, 16, 32):
+        for bs in (2, 3, 5, 16, 31, 32, 33, 64, 4096):
+            for sync_bn in (False, True):
+                cap = train_rows_cap(bs, world, sync_bn)
+                for n in range(2, bs + 1):
+                    f = rank_slice if sync_bn else rank_share
+                    assert max(hi - lo for lo, hi in (f(n, r, world) for r in range(world))) <= cap, (world, bs, n)
+    assert train_rows_cap(32, 16) == 3 and train_rows_cap(32, 32) == 3 and train_rows_cap(4096, 8) == 512
