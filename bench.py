@@ -120,6 +120,8 @@ def parse():
                     help="N width of the forward hidden-layer GEMM tiles (GM2_OPT_SMALL_TILE)")
     ap.add_argument("--recon-tile", type=int, choices=[0, 128, 256], default=None,
                     help="tile of the output-layer loss GEMM: 0 plan, 128 / 256 force (GM2_OPT_RECON_TILE)")
+    ap.add_argument("--bn-fin", type=int, choices=[0, 1], default=None,
+                    help="GM2_OPT_BN_FIN: BatchNorm coefficients finalised by the statistics' producer (A/B)")
     ap.add_argument("--c5-strains", type=int, default=12500,
                     help="strains resident per rank for the C5 line (the 1/8 shard of 100,000)")
     return ap.parse_args()
@@ -281,6 +283,8 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         ws.set_option(native.OPT_SMALL_TILE, a.small_tile)
     if a.recon_tile is not None:
         ws.set_option(native.OPT_RECON_TILE, a.recon_tile)
+    if a.bn_fin is not None:
+        ws.set_option(native.OPT_BN_FIN, a.bn_fin)
     if a.dw9_last is not None:
         ws.set_option(native.OPT_DW9_LAST, a.dw9_last)
     if a.tail_split is not None:

@@ -801,14 +801,18 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
       const float nr = (float)min(C::BM, g.M - tl.m0);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
+        float2 v;
         if (bn.mode == 1) {
           const float dm = av[u] / nr;
-          o[u] = make_float2(sh[u] + dm, fmaxf(fmaf(-av[u], dm, qv[u]), 0.f));
+          v = make_float2(sh[u] + dm, fmaxf(fmaf(-av[u], dm, qv[u]), 0.f));
         } else {
-          o[u] = make_float2(av[u], qv[u]);
+          v = make_float2(av[u], qv[u]);
         }
+        if (bn.fin.mode) st_sc1_f2(o + u, v);  // (write-through: the last arriver merges them)
+        else o[u] = v;
       }
     }
+    if (bn.fin.mode) bn_fin_arrive(bn.fin, tl.n0 / C::BN, g.Mp / C::BM, tl.n0, C::BN, (int*)smem);
   }
   if (bn.sq) {  // (one K pass: checked on the host) fixed-order block sum, one fp64 per tile
     double* red = (double*)smem;
@@ -1594,6 +1598,11 @@ bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bi
   const GemmPlan p = plan_gemm(g);
   if (p.tile != 128 || p.splits != 1 || (bn.mode && (g.N % 4 || bn.ldy % 4))) return false;
   check_gemm(g, 128);
+  const BnFin& f = bn.fin;
+  if (f.mode && (f.mode != bn.mode || f.part != bn.part || bn.ldp != f.H || f.H != g.N || f.B != g.M || !f.cnt ||
+                 !f.coef || !f.gamma || !f.beta || !f.save || (f.mode == 1 && (!f.rmean || !f.rvar)) ||
+                 (f.mode == 2 && (!f.dgamma || !f.dbeta))))
+    throw Gm2Error("gemm_bn: inconsistent BatchNorm finalisation");
   small_cfg_for(g, [&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s); });
   return true;
 }

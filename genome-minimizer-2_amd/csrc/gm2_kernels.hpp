@@ -9,6 +9,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "bn_common.hpp"
 #include "gm2_common.hpp"
 
 namespace gm2 {
@@ -97,6 +98,7 @@ struct Options {
   int grad_buckets = 1;  // GM2_OPT_GRAD_BUCKETS  record the gradient-bucket events (gm2_wait_grad_bucket)
   int side_cus = 0;      // GM2_OPT_SIDE_CUS  CU mask of the side stream: this many CUs (0 = all)
   int small_tile = 128;  // GM2_OPT_SMALL_TILE  N width of the forward's hidden-layer tiles (128 or 64)
+  int bn_fin = 1;        // GM2_OPT_BN_FIN  BatchNorm coefficients finalised by the statistics' producer
 };
 // validated edit of one option (throws on an unknown key or a bad value)
 void option_set(Options& o, int key, int value);
@@ -157,6 +159,10 @@ struct StoreEpi {
   int tail_R = 0, tail_cus = 0, tail_rem = 0, tail_S = 1;
   float* tail_part = nullptr;
   int* tail_cnt = nullptr;
+  // mode 1 / 2 with fin.mode == mode: the partials go out write-through and the column block's
+  // last-arriving row tile finalises its columns (bn_common.hpp BnFin: coefficient table, side
+  // outputs), so the apply pass that follows is elementwise only. part must be fin.part, ldp == H.
+  BnFin fin;
 };
 // split-tail scratch of one GEMM: at most kTailItems tile parts of 256 x 256 fp32 + counters
 constexpr int kTailItems = 256;
@@ -228,26 +234,27 @@ void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* row
 
 // BN forward: y = sum of S slabs + bias -> Y; per-chunk (mean, M2) partials
 void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, const float* bias, int B, int H,
-                           float* Y, float* part, hipStream_t s);
+                           float* Y, float* part, hipStream_t s, const BnFin* fin = nullptr);
 // BN backward: partials of sum(do), sum((y-mean)*do) with do = dA * [bn_out > 0]; optionally
 // writes the summed split-K dA (dsum) so the apply pass reads one slab instead of S
 void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
                            const float* gamma, const float* beta, int B, int H, float* part, float* dsum,
-                           hipStream_t s);
+                           hipStream_t s, const BnFin* fin = nullptr);
 // dst[c][r] = src[r][c] for an R x Cn block (multiples of 64)
 template <typename T>
 void launch_transpose(const T* src, int64_t lds_, int R, int Cn, T* dst, int64_t ldd, hipStream_t s);
 // BatchNorm finalize (chunk merge per column) + elementwise apply in one launch per layer
-// (sync != nullptr: SyncBN, the global batch's all-reduced sums from launch_bn_sync_pack)
+// (sync != nullptr: SyncBN, the global batch's all-reduced sums from launch_bn_sync_pack); with
+// `coef` (the table a BnFin producer finalised: bn_common.hpp) the pass is elementwise only
 template <typename T>
 void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
                          const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,
-                         hipStream_t s, const double* sync = nullptr);
+                         hipStream_t s, const double* sync = nullptr, const float* coef = nullptr);
 template <typename T>
 void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const float* part, int B, int Bp, int H,
                          int train, const float* save, const float* gamma, const float* beta, float* dgamma,
                          float* dbeta, T* dY, float* colpart, hipStream_t s, const double* sync = nullptr,
-                         T* dYT = nullptr, int64_t ldt = 0);
+                         T* dYT = nullptr, int64_t ldt = 0, const float* coef = nullptr);
 // SyncBN: this rank's [sum | sum of squares (mode 0) or sum (y-mean)do (mode 1) | rows, 0] (2H + 2 doubles)
 void launch_bn_sync_pack(const float* part, int B, int H, int mode, double* out, hipStream_t s);
 // SyncBN, a rank with no rows: the running-statistics update from the all-reduced sums

@@ -2,6 +2,7 @@
 // reparameterization + KL, deterministic reductions, clip-norm statistics, Adam, GEMM shadows.
 // All are HBM/latency-bound streaming kernels over [B,H]-sized (or P-sized) data; they keep
 // every padded element of their outputs at zero (the GEMM operand contract, gemm.hip).
+#include "bn_common.hpp"
 #include "gm2_common.hpp"
 #include "gm2_kernels.hpp"
 
@@ -9,8 +10,7 @@ namespace gm2 {
 
 namespace {
 
-constexpr double kBnEps = 1e-5;       // nn.BatchNorm1d default eps
-constexpr double kBnMomentum = 0.1;   // nn.BatchNorm1d default momentum
+static_assert(kBnChunk == kBnRowChunk, "BatchNorm chunk size");
 
 // ---------------------------------------------------------------------------------------------
 // gather: X[r][c] = data[rows[r]][c] (u8, nonzero -> 1, as T) and the row-major target bits of the
@@ -97,7 +97,7 @@ __device__ __forceinline__ float4 f4add(float4 a, float4 b) { return make_float4
 
 __global__ __launch_bounds__(256) void k_bn_fwd_partial(const float* __restrict__ slabs, int S, int64_t slab,
                                                       int64_t ld, const float* __restrict__ bias, int B, int H,
-                                                      float* __restrict__ Y, float2* __restrict__ part) {
+                                                      float* __restrict__ Y, float2* __restrict__ part, BnFin fin) {
   __shared__ float4 red[16][16];
   const int cg = threadIdx.x & 15, rg = threadIdx.x >> 4;
   const int col = blockIdx.x * 64 + cg * 4;
@@ -166,55 +166,25 @@ __global__ __launch_bounds__(256) void k_bn_fwd_partial(const float* __restrict_
     float4 q = zero;
 #pragma unroll
     for (int k = 0; k < 16; ++k) q = f4add(q, red[k][cg]);
-    float4* o = (float4*)(part + (int64_t)blockIdx.y * H + col);
-    o[0] = make_float4(mean.x, q.x, mean.y, q.y);
-    o[1] = make_float4(mean.z, q.z, mean.w, q.w);
+    float2* o = part + (int64_t)blockIdx.y * H + col;
+    if (fin.mode) {  // write-through for the last arriver's merge
+      st_sc1_f2(o, make_float2(mean.x, q.x));
+      st_sc1_f2(o + 1, make_float2(mean.y, q.y));
+      st_sc1_f2(o + 2, make_float2(mean.z, q.z));
+      st_sc1_f2(o + 3, make_float2(mean.w, q.w));
+    } else {
+      ((float4*)o)[0] = make_float4(mean.x, q.x, mean.y, q.y);
+      ((float4*)o)[1] = make_float4(mean.z, q.z, mean.w, q.w);
+    }
   }
+  if (fin.mode) bn_fin_arrive(fin, blockIdx.x, gridDim.y, blockIdx.x * 64, 64, (int*)red);
 }
 
 // Chan's parallel merge of per-chunk (mean, M2) -> batch mean and biased variance, in two passes
 // (mean = sum n_c mean_c / B ; M2 = sum M2_c + n_c (mean_c - mean)^2), fp64. Up to 32 chunks
 // (B <= 4096) the partials are loaded once, all in flight, and both passes run from registers.
 __device__ __forceinline__ void bn_merge(const float2* __restrict__ part, int B, int H, int col, double& mean, double& var) {
-  const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
-  double s = 0.0, mu, M2 = 0.0;
-  if (nch <= 32) {
-    // branch-free: chunks past nch re-read the last chunk with weight 0 (exact no-ops), so all 32
-    // loads of each pass are independent and in flight together
-#pragma unroll
-    for (int ch = 0; ch < 32; ++ch) {
-      const int cc = min(ch, nch - 1);
-      const double nb = (double)max(0, min(kBnRowChunk, B - ch * kBnRowChunk));
-      s += nb * (double)part[(int64_t)cc * H + col].x;
-    }
-    mu = s / (double)B;
-#pragma unroll
-    for (int ch = 0; ch < 32; ++ch) {
-      const int cc = min(ch, nch - 1);
-      const double nb = (double)max(0, min(kBnRowChunk, B - ch * kBnRowChunk));
-      const float2 p = part[(int64_t)cc * H + col];
-      const double dlt = (double)p.x - mu;
-      M2 += (ch < nch ? (double)p.y : 0.0) + nb * dlt * dlt;
-    }
-    mean = mu;
-    var = M2 / (double)B;
-    return;
-  }
-#pragma unroll 8
-  for (int ch = 0; ch < nch; ++ch) {
-    const double nb = (double)min(kBnRowChunk, B - ch * kBnRowChunk);
-    s += nb * (double)part[(int64_t)ch * H + col].x;
-  }
-  mu = s / (double)B;
-#pragma unroll 8
-  for (int ch = 0; ch < nch; ++ch) {
-    const double nb = (double)min(kBnRowChunk, B - ch * kBnRowChunk);
-    const float2 p = part[(int64_t)ch * H + col];
-    const double dlt = (double)p.x - mu;
-    M2 += (double)p.y + nb * dlt * dlt;
-  }
-  mean = mu;
-  var = M2 / (double)B;
+  bn_merge_ld([&](int ch) { return part[(int64_t)ch * H + col]; }, B, mean, var);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -225,7 +195,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict_
                                                       const float* __restrict__ Y, int64_t ld,
                                                       const float* __restrict__ save, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, int B, int H,
-                                                      float2* __restrict__ part, float* __restrict__ dsum) {
+                                                      float2* __restrict__ part, float* __restrict__ dsum, BnFin fin) {
   __shared__ float4 red[2][16][16];
   const int cg = threadIdx.x & 15, rg = threadIdx.x >> 4;
   const int col = blockIdx.x * 64 + cg * 4;
@@ -285,10 +255,18 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict_
       a = f4add(a, red[0][k][cg]);
       q = f4add(q, red[1][k][cg]);
     }
-    float4* o = (float4*)(part + (int64_t)blockIdx.y * H + col);
-    o[0] = make_float4(a.x, q.x, a.y, q.y);
-    o[1] = make_float4(a.z, q.z, a.w, q.w);
+    float2* o = part + (int64_t)blockIdx.y * H + col;
+    if (fin.mode) {  // write-through for the last arriver's merge
+      st_sc1_f2(o, make_float2(a.x, q.x));
+      st_sc1_f2(o + 1, make_float2(a.y, q.y));
+      st_sc1_f2(o + 2, make_float2(a.z, q.z));
+      st_sc1_f2(o + 3, make_float2(a.w, q.w));
+    } else {
+      ((float4*)o)[0] = make_float4(a.x, q.x, a.y, q.y);
+      ((float4*)o)[1] = make_float4(a.z, q.z, a.w, q.w);
+    }
   }
+  if (fin.mode) bn_fin_arrive(fin, blockIdx.x, gridDim.y, blockIdx.x * 64, 64, (int*)red);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -870,15 +848,7 @@ __device__ __forceinline__ float2 bn_fwd_coef(const float2* __restrict__ part, i
     double mean, var, n = (double)B;
     if (sync) bn_sync_stats(sync, H, col, mean, var, n);
     else bn_merge(part, B, H, col, mean, var);
-    invstd = (float)(1.0 / sqrt(var + kBnEps));
-    meanf = (float)mean;
-    if (own) {
-      save[col] = meanf;
-      save[H + col] = invstd;
-      const double unb = n > 1.0 ? var * n / (n - 1.0) : var;
-      rmean[col] = (float)(kBnMomentum * mean + (1.0 - kBnMomentum) * (double)rmean[col]);
-      rvar[col] = (float)(kBnMomentum * unb + (1.0 - kBnMomentum) * (double)rvar[col]);
-    }
+    return bn_fwd_train_coef(mean, var, n, H, col, gamma, beta, rmean, rvar, save, own);
   } else {
     // eval transform bit-identical to the reference CPU path (pinned in tests): float
     // invstd = 1/sqrt(rv + eps), alpha = gamma*invstd, beta' = fma(-mean, alpha, beta)
@@ -899,15 +869,18 @@ __global__ __launch_bounds__(256) void k_bn_fwd_apply(const float* __restrict__ 
                                                     const float2* __restrict__ part, int B, int H, int train,
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
                                                     float* rmean, float* rvar, float* save, T* __restrict__ A,
-                                                    const double* __restrict__ sync) {
+                                                    const double* __restrict__ sync, const float2* __restrict__ coef) {
   __shared__ float2 cf[256];
   const int c0 = blockIdx.x * 256;
   const int cl = (threadIdx.x & 63) * 4, rg = threadIdx.x >> 6;
   const int c = c0 + cl;
   const int r0 = blockIdx.y * 64;
+  // coef: the table the statistics' producer finalised (bn_common.hpp BnFin; it also wrote save
+  // and the running statistics) -- this pass is then elementwise only
   if (c0 + (int)threadIdx.x < H)
-    cf[threadIdx.x] = bn_fwd_coef(part, B, H, train, gamma, beta, rmean, rvar, save, c0 + threadIdx.x,
-                                  blockIdx.y == 0, sync);
+    cf[threadIdx.x] = coef ? coef[c0 + threadIdx.x]
+                           : bn_fwd_coef(part, B, H, train, gamma, beta, rmean, rvar, save, c0 + threadIdx.x,
+                                         blockIdx.y == 0, sync);
   __syncthreads();
   if (c >= H) return;  // H % 128 == 0: the last block may cover only 128 of its 256 columns
   const float2 k0 = cf[cl], k1 = cf[cl + 1], k2 = cf[cl + 2], k3 = cf[cl + 3];
@@ -942,7 +915,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                     T* __restrict__ dY, float* __restrict__ colpart,
                                                     const double* __restrict__ sync, T* __restrict__ dYT,
-                                                    int64_t ldt) {
+                                                    int64_t ldt, const float* __restrict__ coef) {
   __shared__ float4 cf4[5][64];  // [mean, alpha, beta', grad_mean, proj_scale][column / 4]
   __shared__ float4 red[4][64];
   // dYT (bf16 only): the output written transposed, dYT [H][ldt] (the input layer's K-major
@@ -958,38 +931,24 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
   const bool ok = c < H;
   {
     const int t = threadIdx.x, col = c0 + t;
-    if (col < H) {
-      double s1 = 0.0, s2 = 0.0;
-      const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
-      if (nch <= 32) {  // every chunk partial in flight at once, summed in chunk order
+    if (col < H && coef) {  // finalised by the statistics' producer (bn_common.hpp BnFin)
 #pragma unroll
-        for (int ch = 0; ch < 32; ++ch) {
-          const float2 p = part[(int64_t)min(ch, nch - 1) * H + col];
-          s1 += ch < nch ? (double)p.x : 0.0;
-          s2 += ch < nch ? (double)p.y : 0.0;
-        }
-      } else {
-#pragma unroll 8
-        for (int ch = 0; ch < nch; ++ch) {
-          const float2 p = part[(int64_t)ch * H + col];
-          s1 += p.x;
-          s2 += p.y;
-        }
-      }
-      const float mean = save[col], invstd = save[H + col];
-      const float alpha = invstd * gamma[col];
+      for (int k = 0; k < 5; ++k) cf[256 * k + t] = coef[(int64_t)k * H + col];
+    } else if (col < H) {
+      double s1, s2;
+      bn_bwd_sums_ld([&](int ch) { return part[(int64_t)ch * H + col]; }, B, s1, s2);
+      const float invstd = save[H + col];
       if (blockIdx.y == 0) {
         dgamma[col] = (float)(s2 * invstd);
         dbeta[col] = (float)s1;
       }
-      cf[t] = mean;
-      cf[256 + t] = alpha;
-      cf[512 + t] = fmaf(-mean, alpha, beta[col]);
       // (SyncBN: the coupling terms use the global batch's sums; dgamma / dbeta above stay this
       // rank's share, which the gradient all-reduce sums)
       const double g1 = sync ? sync[col] : s1, g2 = sync ? sync[H + col] : s2, nb = sync ? sync[2 * H] : (double)B;
-      cf[768 + t] = train ? (float)(g1 / nb) : 0.f;
-      cf[1024 + t] = train ? (float)(g2 * (double)invstd * invstd / nb) : 0.f;
+      float c5[5];
+      bn_bwd_coef(g1, g2, nb, train, H, col, save, gamma, beta, c5);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) cf[256 * k + t] = c5[k];
     }
   }
   __syncthreads();
@@ -1183,21 +1142,25 @@ void launch_resident_rows(const int32_t* rows, int n, int nfill, int64_t S, int3
 }
 
 void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, const float* bias, int B, int H,
-                           float* Y, float* part, hipStream_t s) {
+                           float* Y, float* part, hipStream_t s, const BnFin* fin) {
   if (H % 64) throw Gm2Error("bn: H %% 64");
   const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
+  if (fin && (fin->mode != 1 || fin->part != (const float2*)part || fin->B != B || fin->H != H || !fin->cnt))
+    throw Gm2Error("bn_fwd_partial: inconsistent finalisation");
   hipLaunchKernelGGL(k_bn_fwd_partial, dim3(H / 64, nch), dim3(256), 0, s, slabs, S, slab, ld, bias, B, H, Y,
-                     (float2*)part);
+                     (float2*)part, fin ? *fin : BnFin{});
   GM2_CHECK_LAUNCH();
 }
 
 void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
                            const float* gamma, const float* beta, int B, int H, float* part, float* dsum,
-                           hipStream_t s) {
+                           hipStream_t s, const BnFin* fin) {
   if (H % 64) throw Gm2Error("bn: H %% 64");
   const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
+  if (fin && (fin->mode != 2 || fin->part != (const float2*)part || fin->B != B || fin->H != H || !fin->cnt))
+    throw Gm2Error("bn_bwd_partial: inconsistent finalisation");
   hipLaunchKernelGGL(k_bn_bwd_partial, dim3(H / 64, nch), dim3(256), 0, s, dslabs, S, slab, Y, ld, save, gamma,
-                     beta, B, H, (float2*)part, dsum);
+                     beta, B, H, (float2*)part, dsum, fin ? *fin : BnFin{});
   GM2_CHECK_LAUNCH();
 }
 
@@ -1249,10 +1212,11 @@ void launch_colsum(const float* part, int rows, int64_t ld, int64_t n, float* ou
 template <typename T>
 void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
                          const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,
-                         hipStream_t s, const double* sync) {
+                         hipStream_t s, const double* sync, const float* coef) {
   if (H % 128 || ld % 4 || Bp % 64 || B <= 0) throw Gm2Error("bn_fwd_apply: H %% 128, ld %% 4, Bp %% 64, B > 0");
+  if (coef && (sync || !train)) throw Gm2Error("bn_fwd_apply: a finalised table is train mode without SyncBN");
   hipLaunchKernelGGL(k_bn_fwd_apply<T>, dim3((H + 255) / 256, Bp / 64), dim3(256), 0, s, Y, ld, (const float2*)part,
-                     B, H, train, gamma, beta, rmean, rvar, save, A, sync);
+                     B, H, train, gamma, beta, rmean, rvar, save, A, sync, (const float2*)coef);
   GM2_CHECK_LAUNCH();
 }
 
@@ -1269,11 +1233,13 @@ template <typename T>
 void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const float* part, int B, int Bp, int H,
                          int train, const float* save, const float* gamma, const float* beta, float* dgamma,
                          float* dbeta, T* dY, float* colpart, hipStream_t s, const double* sync, T* dYT,
-                         int64_t ldt) {
+                         int64_t ldt, const float* coef) {
   if (H % 128 || ld % 4 || Bp % 64 || B <= 0) throw Gm2Error("bn_bwd_apply: H %% 128, ld %% 4, Bp %% 64, B > 0");
+  if (coef && sync) throw Gm2Error("bn_bwd_apply: a finalised table is not SyncBN's");
   if (dYT && (sizeof(T) != 2 || ldt % 8 || ldt < Bp)) throw Gm2Error("bn_bwd_apply: transposed output (bf16, ldt)");
   hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3((H + 255) / 256, Bp / 64), dim3(256), 0, s, da, Y, ld,
-                     (const float2*)part, B, H, train, save, gamma, beta, dgamma, dbeta, dY, colpart, sync, dYT, ldt);
+                     (const float2*)part, B, H, train, save, gamma, beta, dgamma, dbeta, dY, colpart, sync, dYT, ldt,
+                     coef);
   GM2_CHECK_LAUNCH();
 }
 
@@ -1353,10 +1319,11 @@ void launch_grad_finalize(const double* part, int nblocks, const float* scal, fl
                                       float*, hipStream_t);                                                     \
   template void launch_shadow_sync<T>(const TensorTable&, const float*, hipStream_t);                          \
   template void launch_bn_fwd_apply<T>(const float*, int64_t, const float*, int, int, int, int, const float*,   \
-                                       const float*, float*, float*, float*, T*, hipStream_t, const double*);    \
+                                       const float*, float*, float*, float*, T*, hipStream_t, const double*,     \
+                                       const float*);                                                           \
   template void launch_bn_bwd_apply<T>(const float*, const float*, int64_t, const float*, int, int, int, int,    \
                                        const float*, const float*, const float*, float*, float*, T*, float*,    \
-                                       hipStream_t, const double*, T*, int64_t);                                \
+                                       hipStream_t, const double*, T*, int64_t, const float*);                  \
   template void launch_transpose<T>(const T*, int64_t, int, int, T*, int64_t, hipStream_t);                    \
   template void launch_adam_fused<T>(const TensorTable&, const float*, float*, float*, float*, const float*,    \
                                      const float*, hipStream_t, int, float*);

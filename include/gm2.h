@@ -330,7 +330,13 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       Results are bit-identical.
  *   GM2_OPT_SMALL_TILE  N width of the 128-row tiles of the bf16 GEMMs whose operands are both
  *                       K-major (the forward's hidden layers): 128 (default) or 64 (two 72-KB
- *                       workgroups per CU). Results are bit-identical. */
+ *                       workgroups per CU). Results are bit-identical.
+ *   GM2_OPT_BN_FIN      1 = train-mode BatchNorm coefficients (forward: batch mean / invstd and
+ *                       the affine pair; backward: the coupling terms, dgamma / dbeta) are
+ *                       finalised by the LAST workgroup of the kernel that produced the statistics
+ *                       (an arrival counter per column block), so the apply pass that follows only
+ *                       reads a table (default); 0 = every apply block merges the partials itself.
+ *                       Results are bit-identical (same fp64 merge order). Not used under SyncBN. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -348,7 +354,8 @@ enum {
   GM2_OPT_TAIL_SPLIT = 14,
   GM2_OPT_GRAD_BUCKETS = 15,
   GM2_OPT_SIDE_CUS = 16,
-  GM2_OPT_SMALL_TILE = 17
+  GM2_OPT_SMALL_TILE = 17,
+  GM2_OPT_BN_FIN = 18
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);
