@@ -799,20 +799,28 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
       const float av[4] = {a.x, a.y, a.z, a.w}, qv[4] = {q.x, q.y, q.z, q.w};
       float2* o = bn.part + (int64_t)(tl.m0 / C::BM) * bn.ldp + n;
       const float nr = (float)min(C::BM, g.M - tl.m0);
+      float2 v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        float2 v;
         if (bn.mode == 1) {
           const float dm = av[u] / nr;
-          v = make_float2(sh[u] + dm, fmaxf(fmaf(-av[u], dm, qv[u]), 0.f));
+          v[u] = make_float2(sh[u] + dm, fmaxf(fmaf(-av[u], dm, qv[u]), 0.f));
         } else {
-          v = make_float2(av[u], qv[u]);
+          v[u] = make_float2(av[u], qv[u]);
         }
-        if (bn.fin.mode) st_sc1_f2(o + u, v);  // (write-through: the last arriver merges them)
-        else o[u] = v;
       }
+      // (always write-through sc1 stores, 16 B each -- n % 4 == 0: two aligned pieces -- so that a
+      // BnFin last arriver on another XCD sees them; 1 KB per tile)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(o, 0, 0x7fffffff, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, make_float4(v[0].x, v[0].y, v[1].x, v[1].y)),
+                                             rs, 0, 0, kSc1);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, make_float4(v[2].x, v[2].y, v[3].x, v[3].y)),
+                                             rs, 16, 0, kSc1);
     }
-    if (bn.fin.mode) bn_fin_arrive(bn.fin, tl.n0 / C::BN, g.Mp / C::BM, tl.n0, C::BN, (int*)smem);
+    if constexpr (C::BM == 128)  // (the BatchNorm GEMMs are 128-row tiles: none of this in the 256 kernels)
+      if (bn.fin.mode)
+        bn_fin_arrive(bn.fin, tl.n0 / C::BN, g.Mp / C::BM, tl.n0, C::BN, (int*)smem, (float2*)(smem + 256),
+                      (C::LDS - 256) / 8);
   }
   if (bn.sq) {  // (one K pass: checked on the host) fixed-order block sum, one fp64 per tile
     double* red = (double*)smem;
@@ -1191,12 +1199,19 @@ struct MaskOut {
   float thr;
 };
 
-template <class C, typename T>
+// PP: the 256x256 bf16 ping-pong main loop (the bf16x3 sampling decode: three bf16 GEMMs in one
+// K' = 3H pass, decode_chain)
+template <class C, typename T, bool PP = false>
 __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float* __restrict__ bias, MaskOut o) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
   f32x4 acc[C::FM][C::FN];
-  mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+  if constexpr (PP) {
+    static_assert(std::is_same_v<C, Big> && sizeof(T) == 2, "ping-pong: 256x256 bf16");
+    mainloop_pp<true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+  } else {
+    mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+  }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   constexpr int PI = C::BN + 16;  // u8 image pitch
   uint8_t* img = (uint8_t*)smem;  // [BM][PI] (mainloop staging is free after its last barrier)
@@ -1699,13 +1714,26 @@ bool gemm_idx_ok(const GemmArgs<T>& g) {
 template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs, int64_t ldpr,
                       hipStream_t s, uint8_t* bits, int64_t ldb, int* counts, const uint32_t* xbits, int64_t ldxb,
-                      float thr) {
-  check_gemm(g, 128);
+                      float thr, bool big) {
+  check_gemm(g, big ? 256 : 128);
   if (bits && ((ldb & 15) || (((uintptr_t)bits) & 15) || ldb * 8 < g.Np))
     throw Gm2Error("mask bits: row pitch %lld must be a multiple of 16 bytes covering the padded genes", (long long)ldb);
   if (counts && (!xbits || ldxb * 32 < g.Np)) throw Gm2Error("mask counts: target bits required");
+  if (mask && big && ((uintptr_t)mask & 15)) throw Gm2Error("mask: 16-B aligned rows");
   MaskOut o{mask, ldm, bits, ldb, probs, ldpr, counts, xbits, ldxb, thr};
   TimedLaunch tl(kKcMask, s);
+  if constexpr (sizeof(T) == 2) {
+    if (big) {
+      if (g.Mp % 256 || g.Np % 256 || g.K % 64) throw Gm2Error("mask (256x256): padded extents");
+      constexpr int lds = std::max<int>(Big::LDS, 256 * (256 + 16));
+      ensure_lds_attr((const void*)k_gemm_mask<Big, T, true>, lds);
+      hipLaunchKernelGGL((k_gemm_mask<Big, T, true>), dim3((g.Mp / 256) * (g.Np / 256)), dim3(Big::NT), lds, s, g,
+                         bias, o);
+      GM2_CHECK_LAUNCH();
+      return;
+    }
+  }
+  if (big) throw Gm2Error("mask (256x256): bf16 only");
   hipLaunchKernelGGL((k_gemm_mask<Small, T>), dim3((g.Mp / 128) * (g.Np / 128)), dim3(Small::NT), Small::LDS, s, g,
                      bias, o);
   GM2_CHECK_LAUNCH();
@@ -1729,9 +1757,9 @@ GM2_INST(float)
 GM2_INST(bf16_t)
 #undef GM2_INST
 template void launch_gemm_mask<float>(const GemmArgs<float>&, const float*, uint8_t*, int64_t, float*, int64_t,
-                                      hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float);
+                                      hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float, bool);
 template void launch_gemm_mask<bf16_t>(const GemmArgs<bf16_t>&, const float*, uint8_t*, int64_t, float*, int64_t,
-                                       hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float);
+                                       hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float, bool);
 
 #ifdef GM2_DEBUG
 GM2_DBG_TAKE_FN(dbg_take_gemm)

@@ -1064,6 +1064,50 @@ __global__ __launch_bounds__(256) void k_bn_sync_running(const double* __restric
 // dst[c][r] = src[r][c] over an R x Cn block (both multiples of 64): 64 x 64 tiles through LDS,
 // 16-byte loads and stores (each output row segment = 64 contiguous elements). Used for the small
 // activations whose transposed copy turns a weight-gradient GEMM's MN-major operand K-major.
+// ---------------------------------------------------------------------------------------------
+// bf16x3 split of fp32 rows for the sampling decode's output layer (decode_chain, GM2_OPT_SAMPLE_SPLIT):
+// x = hi + lo + r with hi = bf16(x), lo = bf16(x - hi) (x - hi is exact in fp32), |r| <= 2^-16 |x|.
+// Row r of X [rows][ldx] (K columns) -> out [r][3K] = parts (P0 | P1 | P2), 0 = hi, 1 = lo: the
+// decode's activations as (hi | hi | lo) and the output weights as (hi | lo | hi), so ONE bf16 GEMM
+// with K' = 3K sums hi.hi + hi.lo + lo.hi -- the fp32 product up to 3.02 x 2^-16 |x| |w| per term.
+// Rows in [rows, rows_pad) are zero. The largest row sum of squares (fp32 bits: non-negative floats
+// order as unsigned) goes to *smax by an atomic max (the host's error bound, ||a||_2 ||w||_2).
+// One wave per row, 8 columns per lane per pass.
+// ---------------------------------------------------------------------------------------------
+template <int P0, int P1, int P2>
+__global__ __launch_bounds__(256) void k_split3(const float* __restrict__ X, int64_t ldx, int rows, int rows_pad, int K,
+                                              bf16_t* __restrict__ out, int64_t ldo, unsigned* __restrict__ smax) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows_pad) return;
+  float ss = 0.f;
+  for (int k0 = lane * 8; k0 < K; k0 += 512) {
+    float x[8];
+    if (r < rows) {
+      const float4 a = *(const float4*)(X + (int64_t)r * ldx + k0), b = *(const float4*)(X + (int64_t)r * ldx + k0 + 4);
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = 0.f;
+    }
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float h0 = bf2f(f2bf(x[2 * e])), h1 = bf2f(f2bf(x[2 * e + 1]));
+      hw[e] = f2bf2(x[2 * e], x[2 * e + 1]);
+      lw[e] = f2bf2(x[2 * e] - h0, x[2 * e + 1] - h1);
+      ss = fmaf(x[2 * e], x[2 * e], ss);
+      ss = fmaf(x[2 * e + 1], x[2 * e + 1], ss);
+    }
+    const uint4 hv = make_uint4(hw[0], hw[1], hw[2], hw[3]), lv = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+    bf16_t* o = out + (int64_t)r * ldo + k0;
+    *(uint4*)(o) = P0 ? lv : hv;
+    *(uint4*)(o + K) = P1 ? lv : hv;
+    *(uint4*)(o + 2 * K) = P2 ? lv : hv;
+  }
+  ss = wave_sum(ss);
+  if (lane == 0 && r < rows) atomicMax(smax, __float_as_uint(ss));
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_transpose(const T* __restrict__ src, int64_t lds_, T* __restrict__ dst,
                                                  int64_t ldd) {
@@ -1240,6 +1284,18 @@ void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const floa
   hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3((H + 255) / 256, Bp / 64), dim3(256), 0, s, da, Y, ld,
                      (const float2*)part, B, H, train, save, gamma, beta, dgamma, dbeta, dY, colpart, sync, dYT, ldt,
                      coef);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_split3(const float* X, int64_t ldx, int rows, int rows_pad, int K, bf16_t* out, int64_t ldo, unsigned* smax,
+                   int weights, hipStream_t s) {
+  if (K % 8 || ldx % 4 || ldo % 8 || ldo < 3 * K || rows > rows_pad || rows_pad % 4 || (((uintptr_t)X) & 15) ||
+      (((uintptr_t)out) & 15))
+    throw Gm2Error("split3: K %d, ld %lld / %lld, rows %d / %d", K, (long long)ldx, (long long)ldo, rows, rows_pad);
+  if (weights)
+    hipLaunchKernelGGL((k_split3<0, 1, 0>), dim3(rows_pad / 4), dim3(256), 0, s, X, ldx, rows, rows_pad, K, out, ldo, smax);
+  else
+    hipLaunchKernelGGL((k_split3<0, 0, 1>), dim3(rows_pad / 4), dim3(256), 0, s, X, ldx, rows, rows_pad, K, out, ldo, smax);
   GM2_CHECK_LAUNCH();
 }
 
