@@ -515,6 +515,7 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
     if dist is not None:
         dist.barrier()
     native.timing_begin(native.KC_MASK)
+    n_split0 = ws.stat(native.STAT_SPLIT_DECODES)
     t0 = time.perf_counter()
     run(True)
     if dist is not None:
@@ -526,20 +527,26 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     gps = n_all / dt
-    kflops = 2.0 * chunk * H * G
+    # the output layer ran bf16x3 (GM2_OPT_SAMPLE_SPLIT: one bf16 GEMM over K' = 3H, MFMA peak bf16)
+    # on every chunk, or the exact-fp32 kernel (fp32 matrix peak)
+    split = ws.stat(native.STAT_SPLIT_DECODES) - n_split0 == (n + chunk - 1) // chunk
+    kflops = 2.0 * chunk * H * G * (3 if split else 1)  # executed by one full-chunk launch
     ach = kflops / (k_ms / max(k_n, 1) * 1e-3) / 1e12
+    peak = PEAK_BF16_TFLOPS if split else PEAK_F32_TFLOPS
     # the packed masks that reached the host are the decode's: spot-check the last chunk on device
     last = (n - 1) // chunk * chunk
     assert torch.equal(host_bits[last:n].to(dev), dbits[((n - 1) // chunk) & 1][:n - last])
     traffic, traffic_src = pmc_traffic(a, "k_gemm_mask")
     return {"genomes_per_s": round(gps, 1), "preset": "v1", "genomes": n_all, "n_gpus": world, "chunk": chunk,
-            "dtype": "f32",
+            "dtype": "bf16x3 (fp32 split hi/lo, output layer) + f32 (hidden layers)" if split else "f32",
             "mask_format": "packed bits (numpy packbits, little)", "includes": "z draw, decode, threshold, pack, "
             "essential-gene counts, D2H of packed masks + counts to pinned host memory",
             "decode_tflops": round(gps * decode_flops_per_genome(G, H, L) / 1e12, 2),
             "mean_essential_present": round(float(host_cnt.float().mean()), 2),
-            "roofline": {"bound": "mfma", "kernel": "k_gemm_mask<f32>", "achieved": round(ach, 2),
-                         "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_TFLOPS, 4),
+            "roofline": {"bound": "mfma", "kernel": "k_gemm_mask<bf16, 256x256 pp> (K' = 3H)" if split
+                         else "k_gemm_mask<f32>", "achieved": round(ach, 2),
+                         "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+                         "flops_per_launch": kflops,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "launch_ms": round(k_ms / max(k_n, 1), 4)}}
 

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -99,6 +100,9 @@ struct Layout {
   int64_t X1, XB1;             // second input slot: the next batch's rows, staged under this step's tail
   int64_t syncb;               // SyncBN all-reduce vector: 2H + 2 doubles
   int64_t bncnt, bncoef;       // BatchNorm finalisation (BnFin): arrival counters, coefficient table [5][H]
+  // bf16x3 sampling decode (f32 workspaces; GM2_OPT_SAMPLE_SPLIT): the split activations
+  // [roundup(Bm, 256)][3H] and output weights [roundup(G, 256)][3H] (bf16), the two row-norm maxima
+  int64_t s3a, s3w, s3max;
   int64_t adamscal;            // scalar block of a queued output-layer Adam update
   int64_t ridx;                // zero-copy rows: int32 [roundup(Bm, 256)] resident-matrix row per batch row
   // split-tail scratch of the two one-pass weight-gradient GEMMs (GM2_OPT_TAIL_SPLIT): tile parts
@@ -180,6 +184,10 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.syncb = take((2 * H + 2) * 8);
   o.bncnt = take((H / 64 + 1) * 4);  // (zero from gm2_workspace_init; every launch leaves them zero)
   o.bncoef = take(5 * H * 4);
+  const bool split3 = prec == GM2_F32;
+  o.s3a = take(split3 ? round_up(Bm, 2 * kTile) * 3 * H * 2 : 0);
+  o.s3w = take(split3 ? round_up(d.G, 2 * kTile) * 3 * H * 2 : 0);
+  o.s3max = take(16);
   o.adamscal = take(GM2_NUM_SCALARS * 4);
   o.ridx = take(round_up(Bm, 2 * kTile) * 4);
   // (only where those GEMMs can have more 256x256 tiles than a chip has CUs)
@@ -296,6 +304,8 @@ struct WsState {
   int side_prio = 0;                // priority the side stream was created with
   int side_cus = 0;                 // CU-mask size the side stream was created with (0 = all CUs)
   int cus = 0;                      // compute units of dev
+  int64_t split_decodes = 0;        // sampling decodes that ran the bf16x3 output layer (GM2_STAT_*)
+  int64_t exact_decodes = 0;        // ... and the exact-fp32 one
   // the queued (not yet launched) output-layer update: launched by kick() beside the next training
   // call's hidden layers, or by join() on the joining stream
   struct QueuedAdam {
@@ -979,6 +989,48 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   }
 }
 
+// The sampling decode's output layer as ONE bf16 GEMM over K' = 3H (extras.py:196-201, decode +
+// threshold): activations split (hi | hi | lo), output weights (hi | lo | hi) (launch_split3), so
+// the MFMA sums hi.hi + hi.lo + lo.hi -- each fp32 product a.w up to 3.02 x 2^-16 |a| |w| (the
+// dropped lo.lo term and the two splits' residuals), i.e. per logit at most
+//     e = 4.62e-5 sum_k |a_k| |w_k| <= 4.62e-5 max_r ||a_r||_2 max_g ||w_g||_2
+// (Cauchy-Schwarz; the two maxima come from the split kernels) on top of the fp32 accumulation the
+// exact path has as well. When that bound is at most kSplitBound the mask is the exact-fp32 mask
+// wherever |logit - threshold| > e, i.e. everywhere outside |logit| <= kSplitBound + 9e-8, inside
+// the 1e-3 band the parity tests exempt (fp32 arithmetic itself decides those differently by
+// summation order); otherwise -- weights or activations large enough to need it -- the call falls
+// back to the exact-fp32 kernel. Reading the two maxima is one small device->host copy per call.
+// False: not taken (the caller runs the exact path).
+constexpr double kSplitBound = 2.5e-4;
+constexpr double kSplitUnit = 4.62e-5;  // 3.02 x 2^-16, rounded up
+
+bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, int64_t ldm, uint8_t* bits,
+                   int64_t ldb) {
+  const Dims& d = c.d;
+  const Layout& l = c.lo;
+  const int H = (int)d.H, G = (int)d.G;
+  if (!l.s3a || (bits && ldb * 8 < G)) return false;
+  const int Bq = (int)round_up(n, 2 * kTile), Gq = (int)round_up(G, 2 * kTile);
+  unsigned* smax = (unsigned*)(c.ws + l.s3max);
+  bf16_t* a3 = (bf16_t*)(c.ws + l.s3a);
+  bf16_t* w3 = (bf16_t*)(c.ws + l.s3w);
+  HIP_OK(hipMemsetAsync(smax, 0, 8, c.s));
+  launch_split3(c.f(l.A[5]), H, n, Bq, H, a3, 3 * H, smax, 0, c.s);
+  launch_split3(prm + d.off[D9W], H, G, Gq, H, w3, 3 * H, smax + 1, 1, c.s);
+  unsigned hv[2] = {0u, 0u};
+  HIP_OK(hipMemcpyAsync(hv, smax, 8, hipMemcpyDeviceToHost, c.s));
+  HIP_OK(hipStreamSynchronize(c.s));
+  float a2, w2;
+  std::memcpy(&a2, &hv[0], 4);
+  std::memcpy(&w2, &hv[1], 4);
+  const double bound = kSplitUnit * std::sqrt((double)a2) * std::sqrt((double)w2) * 1.01;
+  if (!(bound <= kSplitBound)) return false;  // (NaN / inf: exact path)
+  GemmArgs<bf16_t> g{a3, 3 * H, w3, 3 * H, n, G, 3 * H, Bq, Gq, 0};
+  launch_gemm_mask<bf16_t>(g, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
+                           true);
+  return true;
+}
+
 template <typename T>
 void decode_chain(const Ctx<T>& c, const float* prm, float* bn, int n, uint8_t* mask, int64_t ldm, float* probs,
                   int64_t ldpr, uint8_t* bits = nullptr, int64_t ldb = 0) {
@@ -1001,6 +1053,13 @@ void decode_chain(const Ctx<T>& c, const float* prm, float* bn, int n, uint8_t* 
     Kin = H;
     ldw = H;
   }
+  if constexpr (std::is_same_v<T, float>) {
+    if (!probs && opts().sample_split && decode_split3(c, prm, n, mask, ldm, bits, ldb)) {
+      if (c.st) c.st->split_decodes++;
+      return;
+    }
+  }
+  if (c.st) c.st->exact_decodes++;
   GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, n, (int)d.G, H, Bp, (int)d.Gp, 0};
   launch_gemm_mask<T>(g, prm + d.off[D9B], mask, ldm, probs, ldpr, c.s, bits, ldb);
 }
@@ -1531,6 +1590,18 @@ int gm2_workspace_set_collective(void* ws, gm2_allreduce_fn fn, void* user) {
   });
 }
 
+int gm2_workspace_stat(void* ws, int key, int64_t* value) {
+  return guarded([&] {
+    if (!value) throw Gm2Error("null value");
+    WsState& st = ws_state(ws);
+    switch (key) {
+      case GM2_STAT_SPLIT_DECODES: *value = st.split_decodes; break;
+      case GM2_STAT_EXACT_DECODES: *value = st.exact_decodes; break;
+      default: throw Gm2Error("unknown statistic %d", key);
+    }
+  });
+}
+
 int gm2_workspace_release(void* ws) {
   return guarded([&] { ws_release(ws); });
 }
@@ -1568,7 +1639,7 @@ int gm2_debug_check_layout(const gm2_dims* d, int precision, int64_t* n_regions,
     const int64_t named[] = {o.sE0, o.sE1, o.sE2, o.sHD, o.sD0, o.sD1, o.sD2, o.sD3, o.X, o.XB, o.HD, o.Z, o.dL,
                              o.slabs, o.side_slabs, o.DA, o.dH, o.AT5, o.dYT0, o.bnpart, o.colpart, o.losspart,
                              o.klpart, o.gradpart, o.colbwd, o.nahdr, o.nasq, o.clip, o.scal0, o.X1, o.XB1, o.syncb,
-                             o.bncnt, o.bncoef,
+                             o.bncnt, o.bncoef, o.s3a, o.s3w, o.s3max,
                              o.adamscal, o.ridx, o.tailp9, o.tailc9, o.tailp0, o.tailc0};
     auto known = [&](int64_t off) {
       for (const auto& x : r)

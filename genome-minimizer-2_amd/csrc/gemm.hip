@@ -1260,6 +1260,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
     static_assert(BPR % 16 == 0, "packed row piece");
     for (int i = threadIdx.x; i < rows * (BPR / 16); i += C::NT) {
       const int r = i / (BPR / 16), cc = i % (BPR / 16);
+      if (tl.n0 / 8 + cc * 16 >= o.ldb) continue;  // (pad genes past the row pitch: all zero)
       uint32_t w[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -1716,10 +1717,10 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
                       hipStream_t s, uint8_t* bits, int64_t ldb, int* counts, const uint32_t* xbits, int64_t ldxb,
                       float thr, bool big) {
   check_gemm(g, big ? 256 : 128);
-  if (bits && ((ldb & 15) || (((uintptr_t)bits) & 15) || ldb * 8 < g.Np))
+  // (the 256-column tiles may reach past the row pitch: their bits stores stop at ldb, past G)
+  if (bits && ((ldb & 15) || (((uintptr_t)bits) & 15) || ldb * 8 < (big ? g.N : g.Np)))
     throw Gm2Error("mask bits: row pitch %lld must be a multiple of 16 bytes covering the padded genes", (long long)ldb);
   if (counts && (!xbits || ldxb * 32 < g.Np)) throw Gm2Error("mask counts: target bits required");
-  if (mask && big && ((uintptr_t)mask & 15)) throw Gm2Error("mask: 16-B aligned rows");
   MaskOut o{mask, ldm, bits, ldb, probs, ldpr, counts, xbits, ldxb, thr};
   TimedLaunch tl(kKcMask, s);
   if constexpr (sizeof(T) == 2) {

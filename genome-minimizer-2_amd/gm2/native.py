@@ -34,7 +34,7 @@ EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_of
            "gm2_workspace_set_option", "gm2_workspace_get_option", "gm2_workspace_release",
            "gm2_workspace_set_collective", "gm2_workspace_join",
            "gm2_resident_layout", "gm2_resident_build",
-           "gm2_timing_begin", "gm2_timing_end"]
+           "gm2_timing_begin", "gm2_timing_end", "gm2_workspace_stat"]
 ABI_VERSION = 4
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
 OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE, OPT_SMALL_SPLIT, OPT_BN_EPILOGUE, OPT_SMALL_WAVES = 1, 2, 3, 4, 5, 6
@@ -43,6 +43,8 @@ OPT_SIDE_PRIORITY, OPT_DW9_LAST, OPT_TAIL_SPLIT, OPT_GRAD_BUCKETS = 12, 13, 14, 
 OPT_SIDE_CUS = 16
 OPT_SMALL_TILE = 17
 OPT_BN_FIN = 18
+OPT_SAMPLE_SPLIT = 19
+STAT_SPLIT_DECODES, STAT_EXACT_DECODES = 1, 2
 # gm2_allreduce_fn (gm2.h): int (double* buf, int64_t count, void* stream, void* user)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
 
@@ -107,6 +109,7 @@ def lib():
         "gm2_workspace_release": (C.c_int, [vp]),
         "gm2_workspace_set_collective": (C.c_int, [vp, ALLREDUCE_FN, vp]),
         "gm2_workspace_join": (C.c_int, [vp, vp]),
+        "gm2_workspace_stat": (C.c_int, [vp, i32, C.POINTER(C.c_int64)]),
         "gm2_resident_layout": (C.c_int, [i64, i64, i32, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                            C.POINTER(C.c_int64), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
         "gm2_resident_build": (C.c_int, [vp, i64, i64, i64, i32, vp, vp, vp]),
@@ -187,6 +190,12 @@ class Workspace:
         """Make torch's current stream wait for work this workspace left running on its side
         stream (a deferred output-layer Adam update, GM2_OPT_DEFER_OUTPUT_ADAM)."""
         check(lib().gm2_workspace_join(self.ptr, stream()), "gm2_workspace_join")
+
+    def stat(self, key: int) -> int:
+        """A counter of this workspace's host-side state (gm2.h GM2_STAT_*)."""
+        v = C.c_int64()
+        check(lib().gm2_workspace_stat(self.ptr, int(key), C.byref(v)), "gm2_workspace_stat")
+        return int(v.value)
 
     def set_collective(self, fn):
         """The SUM all-reduce SyncBN calls (gm2_workspace_set_collective): fn(tensor) reduces a

@@ -336,7 +336,15 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       finalised by the LAST workgroup of the kernel that produced the statistics
  *                       (an arrival counter per column block), so the apply pass that follows only
  *                       reads a table (default); 0 = every apply block merges the partials itself.
- *                       Results are bit-identical (same fp64 merge order). Not used under SyncBN. */
+ *                       Results are bit-identical (same fp64 merge order). Not used under SyncBN.
+ *   GM2_OPT_SAMPLE_SPLIT 1 = gm2_decode_mask / gm2_decode_bits without probs run the output layer as
+ *                       one bf16 GEMM over 3H (the fp32 activations and weights split into bf16
+ *                       hi + lo, summing hi.hi + hi.lo + lo.hi) when the error bound
+ *                       4.62e-5 max||a||_2 max||w||_2 is at most 2.5e-4; the masks then equal the
+ *                       exact-fp32 masks outside |logit| <= 2.5e-4 (inside the 1e-3 band fp32
+ *                       summation order decides anyway), else the call runs the exact path
+ *                       (default). 0 = always the exact-fp32 output layer. probs requests always
+ *                       run exact. Costs one small device->host read per call. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -355,7 +363,8 @@ enum {
   GM2_OPT_GRAD_BUCKETS = 15,
   GM2_OPT_SIDE_CUS = 16,
   GM2_OPT_SMALL_TILE = 17,
-  GM2_OPT_BN_FIN = 18
+  GM2_OPT_BN_FIN = 18,
+  GM2_OPT_SAMPLE_SPLIT = 19
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);
@@ -364,6 +373,10 @@ int gm2_workspace_get_option(void* ws, int key, int* value);
 /* Make `stream` wait for work the workspace left running on its side stream (a deferred output-
  * layer Adam update, GM2_OPT_DEFER_OUTPUT_ADAM); no-op when nothing is pending. */
 int gm2_workspace_join(void* ws, void* stream);
+/* Counters of a workspace's host-side state: GM2_STAT_SPLIT_DECODES = sampling decodes whose output
+ * layer ran bf16x3 (GM2_OPT_SAMPLE_SPLIT), GM2_STAT_EXACT_DECODES = those that ran exact fp32. */
+enum { GM2_STAT_SPLIT_DECODES = 1, GM2_STAT_EXACT_DECODES = 2 };
+int gm2_workspace_stat(void* ws, int key, int64_t* value);
 
 /* The all-reduce SyncBN needs (GM2_OPT_SYNC_BN), supplied by the caller: SUM `count` doubles at the
  * DEVICE pointer `buf` (inside the workspace) across every rank, in place, ordered on `stream` (the

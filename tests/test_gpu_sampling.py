@@ -143,3 +143,63 @@ def test_c3_million_genomes_properties_and_stratified_oracle():
     print(f"mean genome size {sizes.mean():.1f} of {G}; mean essential count {counts.mean():.2f}; "
           f"{len(strata)} stratified rows")
     assert _masks_ok(mask, P, S, zs) == 0
+
+
+def _stats(m):
+    ws = m.workspace(native.GM2_F32, 1)
+    return ws.stat(native.STAT_SPLIT_DECODES), ws.stat(native.STAT_EXACT_DECODES)
+
+
+@pytest.mark.parametrize("G,H,L,N", [(2900, 512, 32, 5000), (1000, 128, 16, 777)])
+def test_split3_decode_equals_exact_outside_its_bound(G, H, L, N):
+    """GM2_OPT_SAMPLE_SPLIT (api.hip decode_split3): the output layer of the sampling decode as one
+    bf16 GEMM over K' = 3H on the (hi | hi | lo) / (hi | lo | hi) splits. The call took that path
+    (workspace counter); its packed masks differ from the exact-fp32 path's only where the fp64 logit
+    is within the path's stated bound of the threshold (|logit64| <= 2.5e-4 + 1e-7), both match the
+    oracle outside the 1e-3 band, and the u8 and packed outputs agree. G = 2900 leaves the last
+    256-gene tile past the packed row pitch (its stores must stop there)."""
+    P, S = perturb_bn(*oracle_state(G, H, L, 80), seed=81)
+    P["decoder.9.bias"] = torch.linspace(-1.0, 0.8, G)
+    m = to_model(P, S, G, H, L, native.GM2_F32)
+    m.eval()
+    z = torch.randn(N, L, generator=torch.Generator().manual_seed(82))
+    out = {}
+    for split in (0, 1):
+        m.workspace(native.GM2_F32, N).set_option(native.OPT_SAMPLE_SPLIT, split)
+        before = _stats(m)
+        pm, _ = m.decode_bits(z)
+        mask, _ = m.decode_mask(z)
+        after = _stats(m)
+        assert (after[0] - before[0], after[1] - before[1]) == ((2, 0) if split else (0, 2)), (before, after)
+        bits = pm.bits.cpu().numpy()
+        unpacked = np.unpackbits(bits, axis=1, bitorder="little")[:, :G]
+        np.testing.assert_array_equal(unpacked, mask.cpu().numpy())
+        # bits past G are zero (the tile past the row pitch wrote nothing there)
+        assert not np.unpackbits(bits, axis=1, bitorder="little")[:, G:].any()
+        out[split] = unpacked.astype(bool)
+        assert _masks_ok(out[split], P, S, z) == 0
+    l64 = O.decode_logits64(P, S, z).numpy()
+    diff = out[0] != out[1]
+    print(f"{int(diff.sum())} split/exact differences, max |logit64| there "
+          f"{float(np.abs(l64[diff]).max()) if diff.any() else 0.0:.3g}")
+    assert np.all(np.abs(l64[diff]) <= 2.5e-4 + 1e-7)
+
+
+def test_split3_decode_falls_back_when_the_bound_is_too_large():
+    """Output weights x 200: the bound 4.62e-5 max||a|| max||w|| exceeds 2.5e-4, so the call runs the
+    exact-fp32 output layer (workspace counter) and its masks are bit-identical to option 0's."""
+    G, H, L, N = 700, 128, 16, 300
+    P, S = perturb_bn(*oracle_state(G, H, L, 90), seed=91)
+    P["decoder.9.weight"] = P["decoder.9.weight"] * 200.0
+    m = to_model(P, S, G, H, L, native.GM2_F32)
+    m.eval()
+    z = torch.randn(N, L, generator=torch.Generator().manual_seed(92))
+    res = []
+    for split in (1, 0):
+        m.workspace(native.GM2_F32, N).set_option(native.OPT_SAMPLE_SPLIT, split)
+        before = _stats(m)
+        mask, _ = m.decode_mask(z)
+        after = _stats(m)
+        assert after[0] == before[0] and after[1] == before[1] + 1
+        res.append(mask.cpu())
+    assert torch.equal(res[0], res[1])
