@@ -22,6 +22,7 @@ holding its 1/8 shard of 12,500 strains) with its own roofline entry. Every time
 finite (losses and gradient norm): a non-finite step fails the run.
 """
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -120,8 +121,8 @@ def parse():
                     help="N width of the forward hidden-layer GEMM tiles (GM2_OPT_SMALL_TILE)")
     ap.add_argument("--recon-tile", type=int, choices=[0, 128, 256], default=None,
                     help="tile of the output-layer loss GEMM: 0 plan, 128 / 256 force (GM2_OPT_RECON_TILE)")
-    ap.add_argument("--bn-fin", type=int, choices=[0, 1], default=None,
-                    help="GM2_OPT_BN_FIN: BatchNorm coefficients finalised by the statistics' producer (A/B)")
+    ap.add_argument("--main-stream", action="store_true",
+                    help="run the steps on a torch stream of their own instead of the NULL stream")
     ap.add_argument("--c5-strains", type=int, default=12500,
                     help="strains resident per rank for the C5 line (the 1/8 shard of 100,000)")
     return ap.parse_args()
@@ -283,8 +284,6 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         ws.set_option(native.OPT_SMALL_TILE, a.small_tile)
     if a.recon_tile is not None:
         ws.set_option(native.OPT_RECON_TILE, a.recon_tile)
-    if a.bn_fin is not None:
-        ws.set_option(native.OPT_BN_FIN, a.bn_fin)
     if a.dw9_last is not None:
         ws.set_option(native.OPT_DW9_LAST, a.dw9_last)
     if a.tail_split is not None:
@@ -309,6 +308,11 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         native.grad_norm(ws, model.params, grads, scal[i], loss[i])
         native.adam_step(ws, model.params, grads, opt.exp_avg, opt.exp_avg_sq, scal[i])
 
+    # the steps on a stream of their own (--main-stream): the CU-masked side stream of
+    # GM2_OPT_SIDE_CUS is a blocking stream, which serialises with the NULL stream only
+    torch.cuda.synchronize()
+    sctx = torch.cuda.stream(torch.cuda.Stream(device=dev)) if a.main_stream else contextlib.nullcontext()
+    sctx.__enter__()
     for i in range(a.warmup):
         step(i)
     ws.join()  # (a queued output-layer update runs before the timed region, the timed steps' inside it)
@@ -325,6 +329,7 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         host_s += time.perf_counter() - h0
     ws.join()
     torch.cuda.synchronize()
+    sctx.__exit__(None, None, None)
     if a.host_timing:  # (stderr: the host's enqueue time per step, the GPU running asynchronously)
         print(f"host enqueue {1e3 * host_s / max(1, nsteps - a.warmup):.3f} ms/step", file=sys.stderr)
     if dist is not None:

@@ -99,7 +99,6 @@ struct Layout {
   int64_t nahdr, nasq;         // norm-ahead header int[4] and per-tile sums of squares (NormAhead)
   int64_t X1, XB1;             // second input slot: the next batch's rows, staged under this step's tail
   int64_t syncb;               // SyncBN all-reduce vector: 2H + 2 doubles
-  int64_t bncnt, bncoef;       // BatchNorm finalisation (BnFin): arrival counters, coefficient table [5][H]
   // bf16x3 sampling decode (f32 workspaces; GM2_OPT_SAMPLE_SPLIT): the split activations
   // [roundup(Bm, 256)][3H] and output weights [roundup(G, 256)][3H] (bf16), the two row-norm maxima
   int64_t s3a, s3w, s3max;
@@ -182,8 +181,6 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.X1 = take(Bm * d.Gp * es);
   o.XB1 = take(Bm * (d.Gp / 32) * 4);
   o.syncb = take((2 * H + 2) * 8);
-  o.bncnt = take((H / 64 + 1) * 4);  // (zero from gm2_workspace_init; every launch leaves them zero)
-  o.bncoef = take(5 * H * 4);
   const bool split3 = prec == GM2_F32;
   o.s3a = take(split3 ? round_up(Bm, 2 * kTile) * 3 * H * 2 : 0);
   o.s3w = take(split3 ? round_up(d.G, 2 * kTile) * 3 * H * 2 : 0);
@@ -550,47 +547,15 @@ const int kBlk[6][4] = {{E0W, E0B, E1G, E1BT}, {E3W, E3B, E4G, E4BT}, {E6W, E6B,
 // tiles (statistics in the store epilogue); otherwise split-K slabs + k_bn_fwd_partial.
 template <typename T>
 void linear_pre_bn(const Ctx<T>& c, const T* in, int64_t ldin, int Bp, const T* W, int64_t ldw, int B, int H, int K,
-                   const float* bias, float* Y, float* part, bool stats, const int32_t* prow = nullptr,
-                   const BnFin* fin = nullptr) {
+                   const float* bias, float* Y, float* part, bool stats, const int32_t* prow = nullptr) {
   GemmArgs<T> g{in, ldin, W, ldw, B, H, K, Bp, H, 0};
   StoreEpi bn;
   bn.mode = stats ? 1 : 0;
   bn.part = (float2*)part;
   bn.ldp = H;
-  if (stats && fin) bn.fin = *fin;
   if (!prow && launch_gemm_bn<T>(g, Y, H, bias, bn, c.s)) return;
   const int S = gemm_to_slabs<T>(c, in, ldin, Bp, W, ldw, H, B, H, K, H, 1, 1, prow);
-  launch_bn_fwd_partial(c.f(c.slab_off), S, (int64_t)Bp * H, H, bias, B, H, Y, part, c.s, stats ? fin : nullptr);
-}
-
-// The BatchNorm finalisation of layer i's statistics by their producer (bn_common.hpp BnFin):
-// train mode without SyncBN, GM2_OPT_BN_FIN on. mode 1 forward, 2 backward.
-template <typename T>
-bool bn_fin_for(const Ctx<T>& c, int mode, int train, int B, int i, const float* prm, float* bn, float* gr,
-                BnFin& f) {
-  const bool sync = train && c.st && c.st->opt.sync_bn;
-  if (!opts().bn_fin || sync || (mode == 1 && !train)) return false;
-  const Layout& l = c.lo;
-  const Dims& d = c.d;
-  const int H = (int)d.H;
-  f.mode = mode;
-  f.train = train;
-  f.B = B;
-  f.H = H;
-  f.part = (const float2*)c.f(l.bnpart);
-  f.cnt = (int*)(c.ws + l.bncnt);
-  f.coef = c.f(l.bncoef);
-  f.gamma = prm + d.off[kBlk[i][2]];
-  f.beta = prm + d.off[kBlk[i][3]];
-  f.save = c.f(l.save[i]);
-  if (mode == 1) {
-    f.rmean = bn + (int64_t)i * 2 * H;
-    f.rvar = bn + (int64_t)i * 2 * H + H;
-  } else {
-    f.dgamma = gr + d.off[kBlk[i][2]];
-    f.dbeta = gr + d.off[kBlk[i][3]];
-  }
-  return true;
+  launch_bn_fwd_partial(c.f(c.slab_off), S, (int64_t)Bp * H, H, bias, B, H, Y, part, c.s);
 }
 
 // Tensor tables. kind 0: the 9 Linear weights with their natural-layout shadow (tile0 counts
@@ -704,10 +669,8 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
       ldin = d.Lr;
       Kin = (int)d.Lp;
     }
-    BnFin fin;
-    const bool fin_on = bn_fin_for<T>(c, 1, train, B, i, prm, bn, nullptr, fin);
     linear_pre_bn<T>(c, in, ldin, Bp, c.t(shadow_in[i]), i == 3 ? d.Lr : Kin, B, H, Kin, prm + d.off[kBlk[i][1]],
-                     c.f(l.Y[i]), c.f(l.bnpart), train != 0, i == 0 ? c.ridx : nullptr, fin_on ? &fin : nullptr);
+                     c.f(l.Y[i]), c.f(l.bnpart), train != 0, i == 0 ? c.ridx : nullptr);
     // a queued output-layer Adam update of the previous step starts here, beside the hidden layers
     // (HBM-bound next to latency-bound small GEMMs; the gather and the input-layer GEMM before this
     // point leave it nothing: one is HBM-bound too, the other holds every CU's registers)
@@ -718,8 +681,7 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
     }
     launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train, prm + d.off[kBlk[i][2]],
                            prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
-                           c.f(l.save[i]), c.t(l.A[i]), c.s, sync ? syncb : nullptr,
-                           fin_on ? c.f(l.bncoef) : nullptr);
+                           c.f(l.save[i]), c.t(l.A[i]), c.s, sync ? syncb : nullptr);
     in = c.t(l.A[i]);
     ldin = H;
     Kin = H;
@@ -870,10 +832,6 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   // dA_j = dY . W (K-major dY, MN-major W) into the slab area; when the plan allows, the GEMM's
   // epilogue also takes BatchNorm j's backward partials (sum do, sum (y-mean) do)
   bool have_part = false;
-  // BatchNorm j's backward coefficients finalised by the producer of its statistics (BnFin): the
-  // dX GEMM's epilogue or, after a split-K GEMM, k_bn_bwd_partial
-  BnFin fin;
-  bool fin_on = false;
   auto dx_pre_bn = [&](const T* dY, int64_t lddy, const T* W, int64_t ldw, int K, int j) {
     GemmArgs<T> g{dY, lddy, W, ldw, B, H, K, Bp, H, 0, 1, 0};
     StoreEpi bn;
@@ -886,9 +844,6 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     bn.gamma = prm + d.off[kBlk[j][2]];
     bn.beta = prm + d.off[kBlk[j][3]];
     bn.H = H;
-    fin = BnFin{};
-    fin_on = bn_fin_for<T>(c, 2, train, B, j, prm, nullptr, gr, fin);
-    if (fin_on) bn.fin = fin;
     have_part = launch_gemm_bn<T>(g, c.f(c.slab_off), H, nullptr, bn, c.s);
     return have_part ? 1 : gemm_to_slabs<T>(c, dY, lddy, Bp, W, ldw, H, B, H, K, H, 1, 0);
   };
@@ -899,8 +854,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     const bool sum = S > 1;
     if (!have_part)
       launch_bn_bwd_partial(c.f(c.slab_off), S, slab, c.f(l.Y[i]), H, c.f(l.save[i]), prm + d.off[kBlk[i][2]],
-                            prm + d.off[kBlk[i][3]], B, H, c.f(l.bnpart), sum ? c.f(l.DA) : nullptr, c.s,
-                            fin_on ? &fin : nullptr);
+                            prm + d.off[kBlk[i][3]], B, H, c.f(l.bnpart), sum ? c.f(l.DA) : nullptr, c.s);
     // bias-gradient partials go to this layer's own slice: their column sum runs on the side stream
     float* colp = c.f(l.colbwd) + (int64_t)i * l.colbwd_cap;
     const bool sync = train && st.opt.sync_bn;
@@ -915,7 +869,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     launch_bn_bwd_apply<T>(sum ? c.f(l.DA) : c.f(c.slab_off), c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train,
                            c.f(l.save[i]), prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]], gr + d.off[kBlk[i][2]],
                            gr + d.off[kBlk[i][3]], c.t(l.dY[i]), colp, c.s, sync ? syncb : nullptr,
-                           dyt ? c.t(l.dYT0) : nullptr, Bp, fin_on ? c.f(l.bncoef) : nullptr);
+                           dyt ? c.t(l.dYT0) : nullptr, Bp);
     const bool hold = i >= hold_from;
     fork_flush(hold);
     side_work(hold, [&, colp, i] { launch_colsum(colp, Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, w.s); });
@@ -1639,7 +1593,7 @@ int gm2_debug_check_layout(const gm2_dims* d, int precision, int64_t* n_regions,
     const int64_t named[] = {o.sE0, o.sE1, o.sE2, o.sHD, o.sD0, o.sD1, o.sD2, o.sD3, o.X, o.XB, o.HD, o.Z, o.dL,
                              o.slabs, o.side_slabs, o.DA, o.dH, o.AT5, o.dYT0, o.bnpart, o.colpart, o.losspart,
                              o.klpart, o.gradpart, o.colbwd, o.nahdr, o.nasq, o.clip, o.scal0, o.X1, o.XB1, o.syncb,
-                             o.bncnt, o.bncoef, o.s3a, o.s3w, o.s3max,
+                             o.s3a, o.s3w, o.s3max,
                              o.adamscal, o.ridx, o.tailp9, o.tailc9, o.tailp0, o.tailc0};
     auto known = [&](int64_t off) {
       for (const auto& x : r)

@@ -799,28 +799,16 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
       const float av[4] = {a.x, a.y, a.z, a.w}, qv[4] = {q.x, q.y, q.z, q.w};
       float2* o = bn.part + (int64_t)(tl.m0 / C::BM) * bn.ldp + n;
       const float nr = (float)min(C::BM, g.M - tl.m0);
-      float2 v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (bn.mode == 1) {
           const float dm = av[u] / nr;
-          v[u] = make_float2(sh[u] + dm, fmaxf(fmaf(-av[u], dm, qv[u]), 0.f));
+          o[u] = make_float2(sh[u] + dm, fmaxf(fmaf(-av[u], dm, qv[u]), 0.f));
         } else {
-          v[u] = make_float2(av[u], qv[u]);
+          o[u] = make_float2(av[u], qv[u]);
         }
       }
-      // (always write-through sc1 stores, 16 B each -- n % 4 == 0: two aligned pieces -- so that a
-      // BnFin last arriver on another XCD sees them; 1 KB per tile)
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(o, 0, 0x7fffffff, 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, make_float4(v[0].x, v[0].y, v[1].x, v[1].y)),
-                                             rs, 0, 0, kSc1);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, make_float4(v[2].x, v[2].y, v[3].x, v[3].y)),
-                                             rs, 16, 0, kSc1);
     }
-    if constexpr (C::BM == 128)  // (the BatchNorm GEMMs are 128-row tiles: none of this in the 256 kernels)
-      if (bn.fin.mode)
-        bn_fin_arrive(bn.fin, tl.n0 / C::BN, g.Mp / C::BM, tl.n0, C::BN, (int*)smem, (float2*)(smem + 256),
-                      (C::LDS - 256) / 8);
   }
   if (bn.sq) {  // (one K pass: checked on the host) fixed-order block sum, one fp64 per tile
     double* red = (double*)smem;
@@ -1614,11 +1602,6 @@ bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bi
   const GemmPlan p = plan_gemm(g);
   if (p.tile != 128 || p.splits != 1 || (bn.mode && (g.N % 4 || bn.ldy % 4))) return false;
   check_gemm(g, 128);
-  const BnFin& f = bn.fin;
-  if (f.mode && (f.mode != bn.mode || f.part != bn.part || bn.ldp != f.H || f.H != g.N || f.B != g.M || !f.cnt ||
-                 !f.coef || !f.gamma || !f.beta || !f.save || (f.mode == 1 && (!f.rmean || !f.rvar)) ||
-                 (f.mode == 2 && (!f.dgamma || !f.dbeta))))
-    throw Gm2Error("gemm_bn: inconsistent BatchNorm finalisation");
   small_cfg_for(g, [&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s); });
   return true;
 }

@@ -9,7 +9,6 @@
 #include <stdexcept>
 #include <string>
 
-#include "bn_common.hpp"
 #include "gm2_common.hpp"
 
 namespace gm2 {
@@ -98,7 +97,6 @@ struct Options {
   int grad_buckets = 1;  // GM2_OPT_GRAD_BUCKETS  record the gradient-bucket events (gm2_wait_grad_bucket)
   int side_cus = 0;      // GM2_OPT_SIDE_CUS  CU mask of the side stream: this many CUs (0 = all)
   int small_tile = 128;  // GM2_OPT_SMALL_TILE  N width of the forward's hidden-layer tiles (128 or 64)
-  int bn_fin = 1;        // GM2_OPT_BN_FIN  BatchNorm coefficients finalised by the statistics' producer
   int sample_split = 1;  // GM2_OPT_SAMPLE_SPLIT  bf16x3 output layer of the sampling decode (bound permitting)
 };
 // validated edit of one option (throws on an unknown key or a bad value)
@@ -160,10 +158,6 @@ struct StoreEpi {
   int tail_R = 0, tail_cus = 0, tail_rem = 0, tail_S = 1;
   float* tail_part = nullptr;
   int* tail_cnt = nullptr;
-  // mode 1 / 2 with fin.mode == mode: the partials go out write-through and the column block's
-  // last-arriving row tile finalises its columns (bn_common.hpp BnFin: coefficient table, side
-  // outputs), so the apply pass that follows is elementwise only. part must be fin.part, ldp == H.
-  BnFin fin;
 };
 // split-tail scratch of one GEMM: at most kTailItems tile parts of 256 x 256 fp32 + counters
 constexpr int kTailItems = 256;
@@ -235,12 +229,12 @@ void launch_gather_rows(const uint8_t* data, int64_t ld_data, const int32_t* row
 
 // BN forward: y = sum of S slabs + bias -> Y; per-chunk (mean, M2) partials
 void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, const float* bias, int B, int H,
-                           float* Y, float* part, hipStream_t s, const BnFin* fin = nullptr);
+                           float* Y, float* part, hipStream_t s);
 // BN backward: partials of sum(do), sum((y-mean)*do) with do = dA * [bn_out > 0]; optionally
 // writes the summed split-K dA (dsum) so the apply pass reads one slab instead of S
 void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
                            const float* gamma, const float* beta, int B, int H, float* part, float* dsum,
-                           hipStream_t s, const BnFin* fin = nullptr);
+                           hipStream_t s);
 // bf16x3 split of fp32 rows (the sampling decode's output layer): out [rows_pad][3K] = (hi | hi | lo)
 // of each row (weights = 0: the activations) or (hi | lo | hi) (weights = 1); rows >= rows zero;
 // atomic max of the row sums of squares (fp32 bits) into *smax
@@ -250,17 +244,16 @@ void launch_split3(const float* X, int64_t ldx, int rows, int rows_pad, int K, b
 template <typename T>
 void launch_transpose(const T* src, int64_t lds_, int R, int Cn, T* dst, int64_t ldd, hipStream_t s);
 // BatchNorm finalize (chunk merge per column) + elementwise apply in one launch per layer
-// (sync != nullptr: SyncBN, the global batch's all-reduced sums from launch_bn_sync_pack); with
-// `coef` (the table a BnFin producer finalised: bn_common.hpp) the pass is elementwise only
+// (sync != nullptr: SyncBN, the global batch's all-reduced sums from launch_bn_sync_pack)
 template <typename T>
 void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
                          const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,
-                         hipStream_t s, const double* sync = nullptr, const float* coef = nullptr);
+                         hipStream_t s, const double* sync = nullptr);
 template <typename T>
 void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const float* part, int B, int Bp, int H,
                          int train, const float* save, const float* gamma, const float* beta, float* dgamma,
                          float* dbeta, T* dY, float* colpart, hipStream_t s, const double* sync = nullptr,
-                         T* dYT = nullptr, int64_t ldt = 0, const float* coef = nullptr);
+                         T* dYT = nullptr, int64_t ldt = 0);
 // SyncBN: this rank's [sum | sum of squares (mode 0) or sum (y-mean)do (mode 1) | rows, 0] (2H + 2 doubles)
 void launch_bn_sync_pack(const float* part, int B, int H, int mode, double* out, hipStream_t s);
 // SyncBN, a rank with no rows: the running-statistics update from the all-reduced sums

@@ -97,7 +97,7 @@ __device__ __forceinline__ float4 f4add(float4 a, float4 b) { return make_float4
 
 __global__ __launch_bounds__(256) void k_bn_fwd_partial(const float* __restrict__ slabs, int S, int64_t slab,
                                                       int64_t ld, const float* __restrict__ bias, int B, int H,
-                                                      float* __restrict__ Y, float2* __restrict__ part, BnFin fin) {
+                                                      float* __restrict__ Y, float2* __restrict__ part) {
   __shared__ float4 red[16][16];
   const int cg = threadIdx.x & 15, rg = threadIdx.x >> 4;
   const int col = blockIdx.x * 64 + cg * 4;
@@ -166,18 +166,10 @@ __global__ __launch_bounds__(256) void k_bn_fwd_partial(const float* __restrict_
     float4 q = zero;
 #pragma unroll
     for (int k = 0; k < 16; ++k) q = f4add(q, red[k][cg]);
-    float2* o = part + (int64_t)blockIdx.y * H + col;
-    if (fin.mode) {  // write-through for the last arriver's merge
-      st_sc1_f2(o, make_float2(mean.x, q.x));
-      st_sc1_f2(o + 1, make_float2(mean.y, q.y));
-      st_sc1_f2(o + 2, make_float2(mean.z, q.z));
-      st_sc1_f2(o + 3, make_float2(mean.w, q.w));
-    } else {
-      ((float4*)o)[0] = make_float4(mean.x, q.x, mean.y, q.y);
-      ((float4*)o)[1] = make_float4(mean.z, q.z, mean.w, q.w);
-    }
+    float4* o = (float4*)(part + (int64_t)blockIdx.y * H + col);
+    o[0] = make_float4(mean.x, q.x, mean.y, q.y);
+    o[1] = make_float4(mean.z, q.z, mean.w, q.w);
   }
-  if (fin.mode) bn_fin_arrive(fin, blockIdx.x, gridDim.y, blockIdx.x * 64, 64, (int*)red);
 }
 
 // Chan's parallel merge of per-chunk (mean, M2) -> batch mean and biased variance, in two passes
@@ -195,7 +187,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict_
                                                       const float* __restrict__ Y, int64_t ld,
                                                       const float* __restrict__ save, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, int B, int H,
-                                                      float2* __restrict__ part, float* __restrict__ dsum, BnFin fin) {
+                                                      float2* __restrict__ part, float* __restrict__ dsum) {
   __shared__ float4 red[2][16][16];
   const int cg = threadIdx.x & 15, rg = threadIdx.x >> 4;
   const int col = blockIdx.x * 64 + cg * 4;
@@ -255,18 +247,10 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict_
       a = f4add(a, red[0][k][cg]);
       q = f4add(q, red[1][k][cg]);
     }
-    float2* o = part + (int64_t)blockIdx.y * H + col;
-    if (fin.mode) {  // write-through for the last arriver's merge
-      st_sc1_f2(o, make_float2(a.x, q.x));
-      st_sc1_f2(o + 1, make_float2(a.y, q.y));
-      st_sc1_f2(o + 2, make_float2(a.z, q.z));
-      st_sc1_f2(o + 3, make_float2(a.w, q.w));
-    } else {
-      ((float4*)o)[0] = make_float4(a.x, q.x, a.y, q.y);
-      ((float4*)o)[1] = make_float4(a.z, q.z, a.w, q.w);
-    }
+    float4* o = (float4*)(part + (int64_t)blockIdx.y * H + col);
+    o[0] = make_float4(a.x, q.x, a.y, q.y);
+    o[1] = make_float4(a.z, q.z, a.w, q.w);
   }
-  if (fin.mode) bn_fin_arrive(fin, blockIdx.x, gridDim.y, blockIdx.x * 64, 64, (int*)red);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -869,18 +853,15 @@ __global__ __launch_bounds__(256) void k_bn_fwd_apply(const float* __restrict__ 
                                                     const float2* __restrict__ part, int B, int H, int train,
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
                                                     float* rmean, float* rvar, float* save, T* __restrict__ A,
-                                                    const double* __restrict__ sync, const float2* __restrict__ coef) {
+                                                    const double* __restrict__ sync) {
   __shared__ float2 cf[256];
   const int c0 = blockIdx.x * 256;
   const int cl = (threadIdx.x & 63) * 4, rg = threadIdx.x >> 6;
   const int c = c0 + cl;
   const int r0 = blockIdx.y * 64;
-  // coef: the table the statistics' producer finalised (bn_common.hpp BnFin; it also wrote save
-  // and the running statistics) -- this pass is then elementwise only
   if (c0 + (int)threadIdx.x < H)
-    cf[threadIdx.x] = coef ? coef[c0 + threadIdx.x]
-                           : bn_fwd_coef(part, B, H, train, gamma, beta, rmean, rvar, save, c0 + threadIdx.x,
-                                         blockIdx.y == 0, sync);
+    cf[threadIdx.x] = bn_fwd_coef(part, B, H, train, gamma, beta, rmean, rvar, save, c0 + threadIdx.x,
+                                  blockIdx.y == 0, sync);
   __syncthreads();
   if (c >= H) return;  // H % 128 == 0: the last block may cover only 128 of its 256 columns
   const float2 k0 = cf[cl], k1 = cf[cl + 1], k2 = cf[cl + 2], k3 = cf[cl + 3];
@@ -915,7 +896,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                     T* __restrict__ dY, float* __restrict__ colpart,
                                                     const double* __restrict__ sync, T* __restrict__ dYT,
-                                                    int64_t ldt, const float* __restrict__ coef) {
+                                                    int64_t ldt) {
   __shared__ float4 cf4[5][64];  // [mean, alpha, beta', grad_mean, proj_scale][column / 4]
   __shared__ float4 red[4][64];
   // dYT (bf16 only): the output written transposed, dYT [H][ldt] (the input layer's K-major
@@ -931,10 +912,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
   const bool ok = c < H;
   {
     const int t = threadIdx.x, col = c0 + t;
-    if (col < H && coef) {  // finalised by the statistics' producer (bn_common.hpp BnFin)
-#pragma unroll
-      for (int k = 0; k < 5; ++k) cf[256 * k + t] = coef[(int64_t)k * H + col];
-    } else if (col < H) {
+    if (col < H) {
       double s1, s2;
       bn_bwd_sums_ld([&](int ch) { return part[(int64_t)ch * H + col]; }, B, s1, s2);
       const float invstd = save[H + col];
@@ -1186,25 +1164,21 @@ void launch_resident_rows(const int32_t* rows, int n, int nfill, int64_t S, int3
 }
 
 void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, const float* bias, int B, int H,
-                           float* Y, float* part, hipStream_t s, const BnFin* fin) {
+                           float* Y, float* part, hipStream_t s) {
   if (H % 64) throw Gm2Error("bn: H %% 64");
   const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
-  if (fin && (fin->mode != 1 || fin->part != (const float2*)part || fin->B != B || fin->H != H || !fin->cnt))
-    throw Gm2Error("bn_fwd_partial: inconsistent finalisation");
   hipLaunchKernelGGL(k_bn_fwd_partial, dim3(H / 64, nch), dim3(256), 0, s, slabs, S, slab, ld, bias, B, H, Y,
-                     (float2*)part, fin ? *fin : BnFin{});
+                     (float2*)part);
   GM2_CHECK_LAUNCH();
 }
 
 void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
                            const float* gamma, const float* beta, int B, int H, float* part, float* dsum,
-                           hipStream_t s, const BnFin* fin) {
+                           hipStream_t s) {
   if (H % 64) throw Gm2Error("bn: H %% 64");
   const int nch = (B + kBnRowChunk - 1) / kBnRowChunk;
-  if (fin && (fin->mode != 2 || fin->part != (const float2*)part || fin->B != B || fin->H != H || !fin->cnt))
-    throw Gm2Error("bn_bwd_partial: inconsistent finalisation");
   hipLaunchKernelGGL(k_bn_bwd_partial, dim3(H / 64, nch), dim3(256), 0, s, dslabs, S, slab, Y, ld, save, gamma,
-                     beta, B, H, (float2*)part, dsum, fin ? *fin : BnFin{});
+                     beta, B, H, (float2*)part, dsum);
   GM2_CHECK_LAUNCH();
 }
 
@@ -1256,11 +1230,10 @@ void launch_colsum(const float* part, int rows, int64_t ld, int64_t n, float* ou
 template <typename T>
 void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
                          const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,
-                         hipStream_t s, const double* sync, const float* coef) {
+                         hipStream_t s, const double* sync) {
   if (H % 128 || ld % 4 || Bp % 64 || B <= 0) throw Gm2Error("bn_fwd_apply: H %% 128, ld %% 4, Bp %% 64, B > 0");
-  if (coef && (sync || !train)) throw Gm2Error("bn_fwd_apply: a finalised table is train mode without SyncBN");
   hipLaunchKernelGGL(k_bn_fwd_apply<T>, dim3((H + 255) / 256, Bp / 64), dim3(256), 0, s, Y, ld, (const float2*)part,
-                     B, H, train, gamma, beta, rmean, rvar, save, A, sync, (const float2*)coef);
+                     B, H, train, gamma, beta, rmean, rvar, save, A, sync);
   GM2_CHECK_LAUNCH();
 }
 
@@ -1277,13 +1250,11 @@ template <typename T>
 void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const float* part, int B, int Bp, int H,
                          int train, const float* save, const float* gamma, const float* beta, float* dgamma,
                          float* dbeta, T* dY, float* colpart, hipStream_t s, const double* sync, T* dYT,
-                         int64_t ldt, const float* coef) {
+                         int64_t ldt) {
   if (H % 128 || ld % 4 || Bp % 64 || B <= 0) throw Gm2Error("bn_bwd_apply: H %% 128, ld %% 4, Bp %% 64, B > 0");
-  if (coef && sync) throw Gm2Error("bn_bwd_apply: a finalised table is not SyncBN's");
   if (dYT && (sizeof(T) != 2 || ldt % 8 || ldt < Bp)) throw Gm2Error("bn_bwd_apply: transposed output (bf16, ldt)");
   hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3((H + 255) / 256, Bp / 64), dim3(256), 0, s, da, Y, ld,
-                     (const float2*)part, B, H, train, save, gamma, beta, dgamma, dbeta, dY, colpart, sync, dYT, ldt,
-                     coef);
+                     (const float2*)part, B, H, train, save, gamma, beta, dgamma, dbeta, dY, colpart, sync, dYT, ldt);
   GM2_CHECK_LAUNCH();
 }
 
@@ -1375,11 +1346,10 @@ void launch_grad_finalize(const double* part, int nblocks, const float* scal, fl
                                       float*, hipStream_t);                                                     \
   template void launch_shadow_sync<T>(const TensorTable&, const float*, hipStream_t);                          \
   template void launch_bn_fwd_apply<T>(const float*, int64_t, const float*, int, int, int, int, const float*,   \
-                                       const float*, float*, float*, float*, T*, hipStream_t, const double*,     \
-                                       const float*);                                                           \
+                                       const float*, float*, float*, float*, T*, hipStream_t, const double*);    \
   template void launch_bn_bwd_apply<T>(const float*, const float*, int64_t, const float*, int, int, int, int,    \
                                        const float*, const float*, const float*, float*, float*, T*, float*,    \
-                                       hipStream_t, const double*, T*, int64_t, const float*);                  \
+                                       hipStream_t, const double*, T*, int64_t);                                \
   template void launch_transpose<T>(const T*, int64_t, int, int, T*, int64_t, hipStream_t);                    \
   template void launch_adam_fused<T>(const TensorTable&, const float*, float*, float*, float*, const float*,    \
                                      const float*, hipStream_t, int, float*);

@@ -81,7 +81,6 @@ void option_set(Options& o, int key, int value) {
       if (value != 64 && value != 128) throw Gm2Error("small tile %d: 64 or 128", value);
       o.small_tile = value;
       break;
-    case GM2_OPT_BN_FIN: o.bn_fin = value ? 1 : 0; break;
     case GM2_OPT_SAMPLE_SPLIT: o.sample_split = value ? 1 : 0; break;
     default: throw Gm2Error("unknown option %d", key);
   }
@@ -106,7 +105,6 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_GRAD_BUCKETS: return o.grad_buckets;
     case GM2_OPT_SIDE_CUS: return o.side_cus;
     case GM2_OPT_SMALL_TILE: return o.small_tile;
-    case GM2_OPT_BN_FIN: return o.bn_fin;
     case GM2_OPT_SAMPLE_SPLIT: return o.sample_split;
     default: throw Gm2Error("unknown option %d", key);
   }

@@ -42,8 +42,7 @@ OPT_INPUT_CHUNKS, OPT_SMALL_STAGES, OPT_GRID_CAP, OPT_SYNC_BN, OPT_DEFER_OUTPUT_
 OPT_SIDE_PRIORITY, OPT_DW9_LAST, OPT_TAIL_SPLIT, OPT_GRAD_BUCKETS = 12, 13, 14, 15
 OPT_SIDE_CUS = 16
 OPT_SMALL_TILE = 17
-OPT_BN_FIN = 18
-OPT_SAMPLE_SPLIT = 19
+OPT_SAMPLE_SPLIT = 18
 STAT_SPLIT_DECODES, STAT_EXACT_DECODES = 1, 2
 # gm2_allreduce_fn (gm2.h): int (double* buf, int64_t count, void* stream, void* user)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)

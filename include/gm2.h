@@ -331,12 +331,6 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *   GM2_OPT_SMALL_TILE  N width of the 128-row tiles of the bf16 GEMMs whose operands are both
  *                       K-major (the forward's hidden layers): 128 (default) or 64 (two 72-KB
  *                       workgroups per CU). Results are bit-identical.
- *   GM2_OPT_BN_FIN      1 = train-mode BatchNorm coefficients (forward: batch mean / invstd and
- *                       the affine pair; backward: the coupling terms, dgamma / dbeta) are
- *                       finalised by the LAST workgroup of the kernel that produced the statistics
- *                       (an arrival counter per column block), so the apply pass that follows only
- *                       reads a table (default); 0 = every apply block merges the partials itself.
- *                       Results are bit-identical (same fp64 merge order). Not used under SyncBN.
  *   GM2_OPT_SAMPLE_SPLIT 1 = gm2_decode_mask / gm2_decode_bits without probs run the output layer as
  *                       one bf16 GEMM over 3H (the fp32 activations and weights split into bf16
  *                       hi + lo, summing hi.hi + hi.lo + lo.hi) when the error bound
@@ -363,8 +357,7 @@ enum {
   GM2_OPT_GRAD_BUCKETS = 15,
   GM2_OPT_SIDE_CUS = 16,
   GM2_OPT_SMALL_TILE = 17,
-  GM2_OPT_BN_FIN = 18,
-  GM2_OPT_SAMPLE_SPLIT = 19
+  GM2_OPT_SAMPLE_SPLIT = 18
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);

@@ -769,40 +769,3 @@ def test_deferred_output_adam_bit_identical(prec):
         for a, b in zip(outs[0], o):
             assert torch.equal(a, b)
 
-
-@pytest.mark.parametrize("prec,G,B", [(1, 16500, 1024), (1, 3000, 1000), (0, 3000, 520)])
-def test_bn_fin_bit_identical(prec, G, B):
-    """GM2_OPT_BN_FIN (bn_common.hpp BnFin): the train-mode BatchNorm coefficients finalised by the
-    LAST workgroup of the kernel that produced the statistics -- the hidden-layer GEMM epilogues and
-    the split-K statistics passes (input layer forward, output layer's input gradient backward), so
-    the apply passes only read a table -- against every apply block merging the partials itself:
-    gradients, loss record, BatchNorm running statistics and batch mean / invstd bit-identical over
-    two steps with Adam (bf16 and f32, ragged batches: a partial last row chunk), and the arrival
-    counters left at zero (the second step would otherwise finalise early)."""
-    H, L = 1024, 32
-    P, S = perturb_bn(*oracle_state(G, H, L, G + 13), seed=71)
-    X = synth_x(B, G, 72)
-    gen = torch.Generator().manual_seed(73)
-    eps = [torch.randn(B, L, generator=gen).cuda() for _ in range(2)]
-    outs = []
-    for fin in (0, 1):
-        m = to_model(P, S, G, H, L, prec)
-        mat = ResidentMatrix(X)
-        ws = m.workspace(prec, B)
-        ws.set_option(native.OPT_BN_FIN, fin)
-        grads = torch.zeros_like(m.params)
-        mom, vel = torch.zeros_like(m.params), torch.zeros_like(m.params)
-        out = []
-        for i in range(2):
-            sc = scalars(beta=0.37, wgamma=0.55, lam=0.01, step=i + 1)
-            loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
-            native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, B, eps[i]), m.params, grads, m.bn, sc,
-                                 loss)
-            native.grad_norm(ws, m.params, grads, sc, loss)
-            out += [grads.clone(), loss.clone(), m.bn.clone()]
-            native.adam_step(ws, m.params, grads, mom, vel, sc)
-        ws.join()
-        torch.cuda.synchronize()
-        outs.append(out + [m.params.clone()])
-    for k, (a, b) in enumerate(zip(*outs)):
-        assert torch.equal(a, b), k
