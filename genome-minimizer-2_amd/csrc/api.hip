@@ -287,6 +287,7 @@ struct WsState {
   Options opt;
   int dev = -1;
   hipStream_t side = nullptr;
+  hipStream_t side9 = nullptr;  // GM2_OPT_SIDE_CUS > 0: the CU-masked stream of the output-layer weight gradient
   std::vector<hipEvent_t> ev;  // fork/join ring
   size_t next = 0;
   hipEvent_t bucket[GM2_GRAD_BUCKETS] = {};
@@ -323,6 +324,8 @@ struct WsState {
   }
   void destroy() {
     if (side) (void)hipStreamDestroy(side);
+    if (side9) (void)hipStreamDestroy(side9);
+    side9 = nullptr;
     for (auto e : ev) (void)hipEventDestroy(e);
     for (auto e : bucket)
       if (e) (void)hipEventDestroy(e);
@@ -335,23 +338,26 @@ struct WsState {
   // re-created after draining when that option changed), else nullptr
   hipStream_t side_stream() {
     if (!opt.side_stream) return nullptr;
-    if (side && (side_prio != opt.side_priority || side_cus != opt.side_cus)) {
-      HIP_OK(hipStreamSynchronize(side));
-      HIP_OK(hipStreamDestroy(side));
-      side = nullptr;
+    if ((side || side9) && (side_prio != opt.side_priority || side_cus != opt.side_cus)) {
+      if (side) HIP_OK(hipStreamSynchronize(side));
+      if (side9) HIP_OK(hipStreamSynchronize(side9));
+      if (side) HIP_OK(hipStreamDestroy(side));
+      if (side9) HIP_OK(hipStreamDestroy(side9));
+      side = side9 = nullptr;
     }
     if (!side) {
       int least = 0, greatest = 0;
       HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
       const int prio = opt.side_priority > 0 ? least : opt.side_priority < 0 ? greatest : 0;
+      HIP_OK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, std::min(std::max(prio, greatest), least)));
       if (opt.side_cus > 0 && opt.side_cus < cus) {
         // the lowest n bits: the driver deals mask bits round-robin over the XCDs (and their shader
-        // engines), so every XCD keeps the same share of CUs for the caller's stream
+        // engines), so every XCD keeps the same share of CUs for the caller's stream. (A CU-masked
+        // stream is a blocking stream: it serialises with the NULL stream, so the caller's work must
+        // run on a stream of its own -- bench.py --main-stream.)
         std::vector<uint32_t> mask((cus + 31) / 32, 0u);
         for (int i = 0; i < opt.side_cus; ++i) mask[i / 32] |= 1u << (i % 32);
-        HIP_OK(hipExtStreamCreateWithCUMask(&side, (uint32_t)mask.size(), mask.data()));
-      } else {
-        HIP_OK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, std::min(std::max(prio, greatest), least)));
+        HIP_OK(hipExtStreamCreateWithCUMask(&side9, (uint32_t)mask.size(), mask.data()));
       }
       side_prio = opt.side_priority;
       side_cus = opt.side_cus;
@@ -361,6 +367,12 @@ struct WsState {
       }
     }
     return side;
+  }
+  // the stream of the output-layer weight gradient: the CU-masked one when GM2_OPT_SIDE_CUS is set,
+  // else the side stream
+  hipStream_t dw9_stream() {
+    hipStream_t s = side_stream();
+    return side9 ? side9 : s;
   }
   void launch_queued(hipStream_t s, int max_grid = 0) {
     QueuedAdam& q = qadam;
@@ -380,8 +392,7 @@ struct WsState {
     order(s, sd);
     // a few workgroups per CU, looping over the blocks: room stays for the hidden layers' GEMM
     // workgroups (an uncapped grid fills every CU and serialises them behind it)
-    const int scus = opt.side_cus > 0 && opt.side_cus < cus ? opt.side_cus : cus;
-    launch_queued(sd, std::max(1, opt.defer_adam) * std::max(1, scus));
+    launch_queued(sd, std::max(1, opt.defer_adam) * std::max(1, cus));
     HIP_OK(hipEventRecord(adam9_done, sd));
     adam9_pending = true;
   }
@@ -807,21 +818,27 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     const char* e = std::getenv("GM2_TAIL_AFTER_DW9");
     return e && e[0] == '1';
   }();
+  // GM2_OPT_SIDE_CUS > 0: the (one-pass) output-layer weight gradient runs on a CU-masked stream
+  // of its own, so the hidden chain keeps the other CUs, and the hidden layers' weight gradients on
+  // the side stream do not queue behind it (split-K plans stay on the side stream: its slabs)
+  hipStream_t s9 = sr ? w.s : c.s;
   auto output_weight_grad = [&] {
-    fork();
-    if (!tail_after) tail_on(w.s);
     const GemmArgs<T>& g9 = bg.g9;
-    if (plan_gemm<T>(g9).splits == 1) {
+    const bool direct9 = plan_gemm<T>(g9).splits == 1;
+    if (sr && direct9) s9 = st.dw9_stream();
+    if (sr) st.order(c.s, s9);
+    if (!tail_after) tail_on(s9);
+    if (direct9) {
       // (A5^T here on the side stream; on the main stream before the fork measured ~35 us/step
       // slower, profiles/r02_a5t_placement_ab.txt)
-      launch_transpose<T>(c.t(l.A[5]), H, Bp, H, c.t(l.AT5), Bp, w.s);
-      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, w.s, bg.direct ? nasq : nullptr, c.tail_part(l.tailp9),
+      launch_transpose<T>(c.t(l.A[5]), H, Bp, H, c.t(l.AT5), Bp, s9);
+      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, s9, bg.direct ? nasq : nullptr, c.tail_part(l.tailp9),
                            c.tail_cnt(l.tailc9));
     } else {
       gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
     }
-    if (tail_after) tail_on(w.s);  // (the output bias gradient: bucket 0 as well)
-    if (st.opt.grad_buckets) HIP_OK(hipEventRecord(st.bucket[0], w.s));
+    if (tail_after) tail_on(s9);  // (the output bias gradient: bucket 0 as well)
+    if (st.opt.grad_buckets) HIP_OK(hipEventRecord(st.bucket[0], s9));
   };
   // GM2_OPT_DW9_LAST: forked beside the input-layer dWe0 GEMM instead, so the hidden-layer chain
   // runs without the 126-us tiles of dW9 holding every CU, and the two big weight-gradient GEMMs'
@@ -903,6 +920,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
         for (int q = 0; q < 4; ++q) st.bucket_ev[2 + q] = 2;
       }
       if (sr) st.order(w.s, c.s);  // join: the caller's stream sees every weight gradient
+      if (sr && s9 != w.s) st.order(s9, c.s);
       if (nx) {  // the next batch's rows -> the other input slot, on the side stream after dWe0 (beside
                  // it, it only slows the GEMM down by its own length): under the data-parallel exchange
                  // of the input-layer gradient, or beside the clip / Adam passes on one GPU
