@@ -283,6 +283,18 @@ unsigned order_event_flags() {
   return f;
 }
 
+// Env GM2_ORDER_VALUE=1: the fork / join ordering between the workspace's streams through stream
+// memory operations (hipStreamWriteValue64 on the producing stream after its work, hipStreamWaitValue64
+// on the consuming one) instead of event records -- an A/B of what each ordering point costs the
+// stream that records it
+bool order_by_value() {
+  static const bool v = [] {
+    const char* e = std::getenv("GM2_ORDER_VALUE");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 struct WsState {
   Options opt;
   int dev = -1;
@@ -298,6 +310,12 @@ struct WsState {
   gm2_allreduce_fn coll = nullptr;  // SyncBN's all-reduce (gm2_workspace_set_collective)
   void* coll_user = nullptr;
   hipEvent_t adam9_done = nullptr;  // a deferred output-layer Adam update (GM2_OPT_DEFER_OUTPUT_ADAM)
+  // GM2_ORDER_VALUE: signal words (hipMallocSignalMemory), one per ordering slot of the ring, each with
+  // its own monotonic value (a word is written by one stream at a time: no out-of-order overwrite),
+  // plus the deferred update's
+  uint64_t* sig = nullptr;
+  uint64_t sig_gen[65] = {};
+  static constexpr int kSigSlots = 64;
   bool adam9_pending = false;       // launched on the side stream, not yet joined
   int side_prio = 0;                // priority the side stream was created with
   int side_cus = 0;                 // CU-mask size the side stream was created with (0 = all CUs)
@@ -321,6 +339,11 @@ struct WsState {
     for (auto& e : bucket) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&slot_done, order_event_flags()));
     HIP_OK(hipEventCreateWithFlags(&adam9_done, order_event_flags()));
+    if (order_by_value()) {
+      HIP_OK(hipExtMallocWithFlags((void**)&sig, (kSigSlots + 1) * sizeof(uint64_t), hipMallocSignalMemory));
+      HIP_OK(hipMemset(sig, 0, (kSigSlots + 1) * sizeof(uint64_t)));
+      HIP_OK(hipDeviceSynchronize());
+    }
   }
   void destroy() {
     if (side) (void)hipStreamDestroy(side);
@@ -331,6 +354,8 @@ struct WsState {
       if (e) (void)hipEventDestroy(e);
     if (slot_done) (void)hipEventDestroy(slot_done);
     if (adam9_done) (void)hipEventDestroy(adam9_done);
+    if (sig) (void)hipFree(sig);
+    sig = nullptr;
     side = nullptr;
     ev.clear();
   }
@@ -393,14 +418,18 @@ struct WsState {
     // a few workgroups per CU, looping over the blocks: room stays for the hidden layers' GEMM
     // workgroups (an uncapped grid fills every CU and serialises them behind it)
     launch_queued(sd, std::max(1, opt.defer_adam) * std::max(1, cus));
-    HIP_OK(hipEventRecord(adam9_done, sd));
+    if (sig) HIP_OK(hipStreamWriteValue64(sd, sig + kSigSlots, ++sig_gen[kSigSlots], 0));
+    else HIP_OK(hipEventRecord(adam9_done, sd));
     adam9_pending = true;
   }
   // make `s` see a deferred output-layer update: a queued one is launched on `s`, a running one
   // waited for
   void join(hipStream_t s) {
     if (qadam.queued) launch_queued(s);
-    if (adam9_pending) HIP_OK(hipStreamWaitEvent(s, adam9_done, 0));
+    if (adam9_pending) {
+      if (sig) HIP_OK(hipStreamWaitValue64(s, sig + kSigSlots, sig_gen[kSigSlots], hipStreamWaitValueGte));
+      else HIP_OK(hipStreamWaitEvent(s, adam9_done, 0));
+    }
     adam9_pending = false;
   }
   // SyncBN: SUM-all-reduce `count` doubles at device pointer `buf` across the ranks, on `s`
@@ -411,6 +440,13 @@ struct WsState {
   }
   // make `to` wait for everything enqueued on `from` so far
   void order(hipStream_t from, hipStream_t to) {
+    if (sig) {
+      const int k = (int)(next++ % kSigSlots);
+      const uint64_t v = ++sig_gen[k];
+      HIP_OK(hipStreamWriteValue64(from, sig + k, v, 0));
+      HIP_OK(hipStreamWaitValue64(to, sig + k, v, hipStreamWaitValueGte));
+      return;
+    }
     hipEvent_t e = ev[next++ % ev.size()];
     HIP_OK(hipEventRecord(e, from));
     HIP_OK(hipStreamWaitEvent(to, e, 0));
@@ -459,8 +495,9 @@ void ws_release(void* ws) {
     HIP_OK(hipStreamSynchronize(s));
     st.adam9_pending = false;
   }
-  if (st.adam9_pending) {
-    HIP_OK(hipEventSynchronize(st.adam9_done));
+  if (st.adam9_pending) {  // (launched on the side stream)
+    if (st.side) HIP_OK(hipStreamSynchronize(st.side));
+    else HIP_OK(hipEventSynchronize(st.adam9_done));
     st.adam9_pending = false;
   }
   st.destroy();
