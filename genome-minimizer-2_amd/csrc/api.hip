@@ -313,9 +313,11 @@ struct WsState {
   // GM2_ORDER_VALUE: signal words (hipMallocSignalMemory), one per ordering slot of the ring, each with
   // its own monotonic value (a word is written by one stream at a time: no out-of-order overwrite),
   // plus the deferred update's
-  uint64_t* sig = nullptr;
-  uint64_t sig_gen[65] = {};
+  // (hipMallocSignalMemory allocates one 8-byte signal per call)
   static constexpr int kSigSlots = 64;
+  bool sig = false;
+  uint64_t* sigw[kSigSlots + 1] = {};
+  uint64_t sig_gen[kSigSlots + 1] = {};
   bool adam9_pending = false;       // launched on the side stream, not yet joined
   int side_prio = 0;                // priority the side stream was created with
   int side_cus = 0;                 // CU-mask size the side stream was created with (0 = all CUs)
@@ -340,9 +342,12 @@ struct WsState {
     HIP_OK(hipEventCreateWithFlags(&slot_done, order_event_flags()));
     HIP_OK(hipEventCreateWithFlags(&adam9_done, order_event_flags()));
     if (order_by_value()) {
-      HIP_OK(hipExtMallocWithFlags((void**)&sig, (kSigSlots + 1) * sizeof(uint64_t), hipMallocSignalMemory));
-      HIP_OK(hipMemset(sig, 0, (kSigSlots + 1) * sizeof(uint64_t)));
+      for (auto& w : sigw) {
+        HIP_OK(hipExtMallocWithFlags((void**)&w, sizeof(uint64_t), hipMallocSignalMemory));
+        HIP_OK(hipMemset(w, 0, sizeof(uint64_t)));
+      }
       HIP_OK(hipDeviceSynchronize());
+      sig = true;
     }
   }
   void destroy() {
@@ -354,8 +359,10 @@ struct WsState {
       if (e) (void)hipEventDestroy(e);
     if (slot_done) (void)hipEventDestroy(slot_done);
     if (adam9_done) (void)hipEventDestroy(adam9_done);
-    if (sig) (void)hipFree(sig);
-    sig = nullptr;
+    for (auto& w : sigw)
+      if (w) (void)hipFree(w);
+    for (auto& w : sigw) w = nullptr;
+    sig = false;
     side = nullptr;
     ev.clear();
   }
@@ -418,7 +425,7 @@ struct WsState {
     // a few workgroups per CU, looping over the blocks: room stays for the hidden layers' GEMM
     // workgroups (an uncapped grid fills every CU and serialises them behind it)
     launch_queued(sd, std::max(1, opt.defer_adam) * std::max(1, cus));
-    if (sig) HIP_OK(hipStreamWriteValue64(sd, sig + kSigSlots, ++sig_gen[kSigSlots], 0));
+    if (sig) HIP_OK(hipStreamWriteValue64(sd, sigw[kSigSlots], ++sig_gen[kSigSlots], 0));
     else HIP_OK(hipEventRecord(adam9_done, sd));
     adam9_pending = true;
   }
@@ -427,7 +434,7 @@ struct WsState {
   void join(hipStream_t s) {
     if (qadam.queued) launch_queued(s);
     if (adam9_pending) {
-      if (sig) HIP_OK(hipStreamWaitValue64(s, sig + kSigSlots, sig_gen[kSigSlots], hipStreamWaitValueGte));
+      if (sig) HIP_OK(hipStreamWaitValue64(s, sigw[kSigSlots], sig_gen[kSigSlots], hipStreamWaitValueGte));
       else HIP_OK(hipStreamWaitEvent(s, adam9_done, 0));
     }
     adam9_pending = false;
@@ -443,8 +450,8 @@ struct WsState {
     if (sig) {
       const int k = (int)(next++ % kSigSlots);
       const uint64_t v = ++sig_gen[k];
-      HIP_OK(hipStreamWriteValue64(from, sig + k, v, 0));
-      HIP_OK(hipStreamWaitValue64(to, sig + k, v, hipStreamWaitValueGte));
+      HIP_OK(hipStreamWriteValue64(from, sigw[k], v, 0));
+      HIP_OK(hipStreamWaitValue64(to, sigw[k], v, hipStreamWaitValueGte));
       return;
     }
     hipEvent_t e = ev[next++ % ev.size()];
@@ -869,8 +876,25 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       // (A5^T here on the side stream; on the main stream before the fork measured ~35 us/step
       // slower, profiles/r02_a5t_placement_ab.txt)
       launch_transpose<T>(c.t(l.A[5]), H, Bp, H, c.t(l.AT5), Bp, s9);
-      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, s9, bg.direct ? nasq : nullptr, c.tail_part(l.tailp9),
-                           c.tail_cnt(l.tailc9));
+      // env GM2_DW9_PHASE="W:T" (A/B): tiles [0, T) on a capped grid of W workgroups first -- the
+      // rest of the CUs stay with the hidden chain's first kernels -- then the other tiles on the
+      // full grid behind them
+      static const std::pair<int, int> phase = [] {
+        const char* e = std::getenv("GM2_DW9_PHASE");
+        int w = 0, t = 0;
+        if (e && std::sscanf(e, "%d:%d", &w, &t) != 2) w = t = 0;
+        return std::make_pair(w, t);
+      }();
+      const int tiles9 = bg.n9;
+      if (sizeof(T) == 2 && phase.first > 0 && phase.second > 0 && phase.second < tiles9 && plan_gemm<T>(g9).tile == 256) {
+        launch_gemm_trans<T>(g9, gr + d.off[D9W], H, s9, bg.direct ? nasq : nullptr, nullptr, nullptr, 0, phase.second,
+                             phase.first);
+        launch_gemm_trans<T>(g9, gr + d.off[D9W], H, s9, bg.direct ? nasq : nullptr, nullptr, nullptr, phase.second,
+                             tiles9, tiles9 - phase.second);
+      } else {
+        launch_gemm_trans<T>(g9, gr + d.off[D9W], H, s9, bg.direct ? nasq : nullptr, c.tail_part(l.tailp9),
+                             c.tail_cnt(l.tailc9));
+      }
     } else {
       gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
     }

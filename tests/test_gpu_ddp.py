@@ -413,3 +413,44 @@ def test_two_rank_sharded_sampling_cli(tmp_path):
     ref = O.sample_decode(Pq, Sq, z).numpy() > 0.5
     band = np.abs(O.decode_logits64(Pq, Sq, z).numpy()) <= 1e-3
     assert ((masks.astype(bool) != ref) & ~band).sum() == 0
+
+
+def _small_batch_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gm2 import native
+    from gm2.data import ResidentMatrix, StrainLoader
+    from gm2.loss_components import KLDivergenceLoss, ReconstructionLoss
+    from gm2.model import VAE
+    from gm2.trainer import Adam, StepLR, TrainingConfig, VAETrainer
+
+    P, S = _state()
+    m = VAE(G, H, L, precision=native.GM2_F32, init=False)
+    m.load_state_dict({**P, **S})
+    opt = Adam(m, lr=1e-3)
+    tr = VAETrainer(m, opt, StepLR(opt, 20, 0.5), TrainingConfig(n_epochs=N_EPOCHS, max_norm=1.0), eps_rng="cpu")
+    tr.setup_loss_components([ReconstructionLoss(), KLDivergenceLoss(scheduler_type="linear", min_beta=0.1,
+                                                                     max_beta=1.0)])
+    torch.manual_seed(SEED + 3)
+    # batch_size 4 on 3 ranks, 7 rows: batches of 4 (2 + 2 rows on ranks 0-1) and 3 (all on rank 0)
+    losses = tr.train_epoch(StrainLoader(ResidentMatrix(synth_x(7, G, 9)), None, 4, shuffle=True), 0)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, f"s{rank}.npz"), params=m.params.cpu().numpy(),
+             rec=np.array([losses["reconstruction"], losses["kl_divergence"]]))
+    dist.destroy_process_group()
+
+
+def test_three_rank_batch_smaller_than_two_per_rank(tmp_path):
+    """a global batch of at most 2 x world rows, with a ragged last batch (4, then 3 rows
+    on 3 ranks): rank_share gives one rank all 3 rows of the last batch, more than ceil(4 / 3); the
+    trainer sizes its workspace with gm2.ddp.train_rows_cap, so the epoch runs, and every rank ends
+    with the same parameters and loss record."""
+    port = _free_port()
+    mp.spawn(_small_batch_worker, args=(3, port, str(tmp_path)), nprocs=3, join=True)
+    r = [np.load(tmp_path / f"s{k}.npz") for k in range(3)]
+    for k in (1, 2):
+        np.testing.assert_array_equal(r[0]["params"], r[k]["params"])
+        np.testing.assert_array_equal(r[0]["rec"], r[k]["rec"])
+    assert np.isfinite(r[0]["rec"]).all() and np.isfinite(r[0]["params"]).all()
