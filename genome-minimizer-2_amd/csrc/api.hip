@@ -283,18 +283,6 @@ unsigned order_event_flags() {
   return f;
 }
 
-// Env GM2_ORDER_VALUE=1: the fork / join ordering between the workspace's streams through stream
-// memory operations (hipStreamWriteValue64 on the producing stream after its work, hipStreamWaitValue64
-// on the consuming one) instead of event records -- an A/B of what each ordering point costs the
-// stream that records it
-bool order_by_value() {
-  static const bool v = [] {
-    const char* e = std::getenv("GM2_ORDER_VALUE");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
 struct WsState {
   Options opt;
   int dev = -1;
@@ -310,14 +298,6 @@ struct WsState {
   gm2_allreduce_fn coll = nullptr;  // SyncBN's all-reduce (gm2_workspace_set_collective)
   void* coll_user = nullptr;
   hipEvent_t adam9_done = nullptr;  // a deferred output-layer Adam update (GM2_OPT_DEFER_OUTPUT_ADAM)
-  // GM2_ORDER_VALUE: signal words (hipMallocSignalMemory), one per ordering slot of the ring, each with
-  // its own monotonic value (a word is written by one stream at a time: no out-of-order overwrite),
-  // plus the deferred update's
-  // (hipMallocSignalMemory allocates one 8-byte signal per call)
-  static constexpr int kSigSlots = 64;
-  bool sig = false;
-  uint64_t* sigw[kSigSlots + 1] = {};
-  uint64_t sig_gen[kSigSlots + 1] = {};
   bool adam9_pending = false;       // launched on the side stream, not yet joined
   int side_prio = 0;                // priority the side stream was created with
   int side_cus = 0;                 // CU-mask size the side stream was created with (0 = all CUs)
@@ -341,14 +321,6 @@ struct WsState {
     for (auto& e : bucket) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&slot_done, order_event_flags()));
     HIP_OK(hipEventCreateWithFlags(&adam9_done, order_event_flags()));
-    if (order_by_value()) {
-      for (auto& w : sigw) {
-        HIP_OK(hipExtMallocWithFlags((void**)&w, sizeof(uint64_t), hipMallocSignalMemory));
-        HIP_OK(hipMemset(w, 0, sizeof(uint64_t)));
-      }
-      HIP_OK(hipDeviceSynchronize());
-      sig = true;
-    }
   }
   void destroy() {
     if (side) (void)hipStreamDestroy(side);
@@ -359,10 +331,6 @@ struct WsState {
       if (e) (void)hipEventDestroy(e);
     if (slot_done) (void)hipEventDestroy(slot_done);
     if (adam9_done) (void)hipEventDestroy(adam9_done);
-    for (auto& w : sigw)
-      if (w) (void)hipFree(w);
-    for (auto& w : sigw) w = nullptr;
-    sig = false;
     side = nullptr;
     ev.clear();
   }
@@ -425,18 +393,14 @@ struct WsState {
     // a few workgroups per CU, looping over the blocks: room stays for the hidden layers' GEMM
     // workgroups (an uncapped grid fills every CU and serialises them behind it)
     launch_queued(sd, std::max(1, opt.defer_adam) * std::max(1, cus));
-    if (sig) HIP_OK(hipStreamWriteValue64(sd, sigw[kSigSlots], ++sig_gen[kSigSlots], 0));
-    else HIP_OK(hipEventRecord(adam9_done, sd));
+    HIP_OK(hipEventRecord(adam9_done, sd));
     adam9_pending = true;
   }
   // make `s` see a deferred output-layer update: a queued one is launched on `s`, a running one
   // waited for
   void join(hipStream_t s) {
     if (qadam.queued) launch_queued(s);
-    if (adam9_pending) {
-      if (sig) HIP_OK(hipStreamWaitValue64(s, sigw[kSigSlots], sig_gen[kSigSlots], hipStreamWaitValueGte));
-      else HIP_OK(hipStreamWaitEvent(s, adam9_done, 0));
-    }
+    if (adam9_pending) HIP_OK(hipStreamWaitEvent(s, adam9_done, 0));
     adam9_pending = false;
   }
   // SyncBN: SUM-all-reduce `count` doubles at device pointer `buf` across the ranks, on `s`
@@ -447,13 +411,6 @@ struct WsState {
   }
   // make `to` wait for everything enqueued on `from` so far
   void order(hipStream_t from, hipStream_t to) {
-    if (sig) {
-      const int k = (int)(next++ % kSigSlots);
-      const uint64_t v = ++sig_gen[k];
-      HIP_OK(hipStreamWriteValue64(from, sigw[k], v, 0));
-      HIP_OK(hipStreamWaitValue64(to, sigw[k], v, hipStreamWaitValueGte));
-      return;
-    }
     hipEvent_t e = ev[next++ % ev.size()];
     HIP_OK(hipEventRecord(e, from));
     HIP_OK(hipStreamWaitEvent(to, e, 0));
@@ -876,25 +833,8 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       // (A5^T here on the side stream; on the main stream before the fork measured ~35 us/step
       // slower, profiles/r02_a5t_placement_ab.txt)
       launch_transpose<T>(c.t(l.A[5]), H, Bp, H, c.t(l.AT5), Bp, s9);
-      // env GM2_DW9_PHASE="W:T" (A/B): tiles [0, T) on a capped grid of W workgroups first -- the
-      // rest of the CUs stay with the hidden chain's first kernels -- then the other tiles on the
-      // full grid behind them
-      static const std::pair<int, int> phase = [] {
-        const char* e = std::getenv("GM2_DW9_PHASE");
-        int w = 0, t = 0;
-        if (e && std::sscanf(e, "%d:%d", &w, &t) != 2) w = t = 0;
-        return std::make_pair(w, t);
-      }();
-      const int tiles9 = bg.n9;
-      if (sizeof(T) == 2 && phase.first > 0 && phase.second > 0 && phase.second < tiles9 && plan_gemm<T>(g9).tile == 256) {
-        launch_gemm_trans<T>(g9, gr + d.off[D9W], H, s9, bg.direct ? nasq : nullptr, nullptr, nullptr, 0, phase.second,
-                             phase.first);
-        launch_gemm_trans<T>(g9, gr + d.off[D9W], H, s9, bg.direct ? nasq : nullptr, nullptr, nullptr, phase.second,
-                             tiles9, tiles9 - phase.second);
-      } else {
-        launch_gemm_trans<T>(g9, gr + d.off[D9W], H, s9, bg.direct ? nasq : nullptr, c.tail_part(l.tailp9),
-                             c.tail_cnt(l.tailc9));
-      }
+      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, s9, bg.direct ? nasq : nullptr, c.tail_part(l.tailp9),
+                           c.tail_cnt(l.tailc9));
     } else {
       gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
     }

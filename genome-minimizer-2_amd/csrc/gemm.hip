@@ -594,7 +594,7 @@ __global__ __launch_bounds__(C::NT, C::MINW) void k_gemm_store(GemmArgs<T> g, fl
   // capped grid (one K pass): workgroup wg takes logical tiles wg, wg + grid, ... (every wave of
   // the block runs the same trip count; the LDS is reused after a barrier)
   const int ntile = tm * tn;
-  for (int t = bn.t0 + xcd_wg(); t < bn.ntiles; t += gridDim.x) {
+  for (int t = xcd_wg(); t < bn.ntiles; t += gridDim.x) {
     __syncthreads();
     store_tile<C, T, AK, BK, PP, IDX>(tile_at<C>(t % ntile, tm, tn, t / ntile), g, C0, C1, msplit, ldc, slab, bias,
                                       bn, smem);
@@ -1571,29 +1571,13 @@ bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hip
 
 template <typename T>
 bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, double* sq, float* tail_part,
-                       int* tail_cnt, int part_t0, int part_t1, int part_grid) {
+                       int* tail_cnt) {
   if (plan_gemm(g).splits != 1) return false;
   StoreEpi ep;
   ep.trans = 1;
   ep.sq = sq;
   ep.ntiles = grid_cap_bits() & 1;  // dW9 bit (the launcher sets the count)
   if constexpr (sizeof(T) == 2) {
-    if (use_big(g) && part_grid > 0) {  // one part: tiles [part_t0, part_t1) on part_grid workgroups
-      check_gemm(g, 256);
-      const int tiles = (g.Mp / 256) * (g.Np / 256);
-      if (part_t0 < 0 || part_t1 > tiles || part_t0 >= part_t1) throw Gm2Error("gemm_trans part [%d, %d) of %d", part_t0, part_t1, tiles);
-      ep.t0 = part_t0;
-      ep.ntiles = part_t1;
-      GemmArgs<T> a = g;
-      a.k_per_split = g.K;  // (one K pass)
-      constexpr int lds = Big::LDS;
-      ensure_lds_attr((const void*)k_gemm_store<Big, T, true, false, true, 0>, lds);
-      if (!pp_enabled()) throw Gm2Error("gemm_trans parts: ping-pong main loop only");
-      hipLaunchKernelGGL((k_gemm_store<Big, T, true, false, true, 0>), dim3(std::min(part_grid, part_t1 - part_t0)),
-                         dim3(Big::NT), lds, s, a, C, C, 1 << 30, ldc, (int64_t)0, nullptr, ep);
-      GM2_CHECK_LAUNCH();
-      return true;
-    }
     if (use_big(g)) {
       check_gemm(g, 256);
       if ((opts().tail_split & 1) && pp_enabled())
@@ -1740,8 +1724,7 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
 }
 
 #define GM2_INST(T)                                                                                              \
-  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t, double*, float*, int*, int,  \
-                                     int, int);                                                                 \
+  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t, double*, float*, int*);       \
   template bool launch_gemm_sq<T>(const GemmArgs<T>&, float*, int64_t, double*, hipStream_t, bool, float*, int*);              \
   template int gemm_tiles<T>(const GemmArgs<T>&);                        \
   template bool launch_gemm_bn<T>(const GemmArgs<T>&, float*, int64_t, const float*, const StoreEpi&, hipStream_t);   \

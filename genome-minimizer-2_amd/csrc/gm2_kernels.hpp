@@ -149,8 +149,6 @@ struct StoreEpi {
   // (grid = ceil(tiles / rounds) for the same number of rounds: the idle CUs of the last round
   // become free CUs for the other stream's work for the whole launch)
   int ntiles = 0;
-  // with ntiles: the launch covers logical tiles [t0, ntiles) (a GEMM launched in parts)
-  int t0 = 0;
   // split tail (tail_S > 1; one K pass, 256x256 tiles): one workgroup per item -- the first tail_R
   // tiles whole (whole dispatch rounds of tail_cus workgroups), then the last tail_rem tiles in
   // tail_S K-parts each. The parts meet through tail_part (each part's fp32 accumulators,
@@ -173,11 +171,8 @@ bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bi
 // (tail_part / tail_cnt: split-tail scratch, kTailPartBytes / kTailCntBytes, used when the option
 // GM2_OPT_TAIL_SPLIT selects this GEMM and the tile count leaves a short last round)
 template <typename T>
-// part_t0 / part_t1 / part_grid (> 0): only logical tiles [part_t0, part_t1) on part_grid workgroups
-// (the 256x256 plan; the output-layer weight gradient launched in two parts, GM2_DW9_PHASE)
 bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, double* sq = nullptr,
-                       float* tail_part = nullptr, int* tail_cnt = nullptr, int part_t0 = 0, int part_t1 = 0,
-                       int part_grid = 0);
+                       float* tail_part = nullptr, int* tail_cnt = nullptr);
 // C = P . Q^T in one K pass with the per-tile sum of squares of C into sq (see StoreEpi::sq);
 // false (nothing launched) when the plan splits K
 template <typename T>
