@@ -541,7 +541,8 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
     # the packed masks that reached the host are the decode's: spot-check the last chunk on device
     last = (n - 1) // chunk * chunk
     assert torch.equal(host_bits[last:n].to(dev), dbits[((n - 1) // chunk) & 1][:n - last])
-    traffic, traffic_src = pmc_traffic(a, "k_gemm_mask")
+    # (the bf16x3 kernel is k_gemm_mask<Cfg<256, ...>, unsigned short, true>, the exact one <..., float>)
+    traffic, traffic_src = pmc_traffic(a, "k_gemm_mask<Cfg<256" if split else "k_gemm_mask<Cfg<128")
     return {"genomes_per_s": round(gps, 1), "preset": "v1", "genomes": n_all, "n_gpus": world, "chunk": chunk,
             "dtype": "bf16x3 (fp32 split hi/lo, output layer) + f32 (hidden layers)" if split else "f32",
             "mask_format": "packed bits (numpy packbits, little)", "includes": "z draw, decode, threshold, pack, "
