@@ -594,25 +594,10 @@ __global__ __launch_bounds__(C::NT, C::MINW) void k_gemm_store(GemmArgs<T> g, fl
   // capped grid (one K pass): workgroup wg takes logical tiles wg, wg + grid, ... (every wave of
   // the block runs the same trip count; the LDS is reused after a barrier)
   const int ntile = tm * tn;
-  const int full = bn.ntiles / gridDim.x;  // rounds every workgroup has a tile in
-  const int x = blockIdx.x & 7, members = ((int)gridDim.x - x + 7) >> 3;
-  int r = 0;
-  for (int t = xcd_wg(); t < bn.ntiles; t += gridDim.x, ++r) {
-    if (bn.rbar && r > 0 && r < full) {  // wait for the XCD's workgroups to finish round r - 1
-      if (threadIdx.x == 0)
-        while (__hip_atomic_load(bn.rbar + 32 * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < r * members)
-          __builtin_amdgcn_s_sleep(1);
-    }
+  for (int t = xcd_wg(); t < bn.ntiles; t += gridDim.x) {
     __syncthreads();
     store_tile<C, T, AK, BK, PP, IDX>(tile_at<C>(t % ntile, tm, tn, t / ntile), g, C0, C1, msplit, ldc, slab, bias,
                                       bn, smem);
-    if (bn.rbar && r < full) {  // arrive; the last arrival of the last full round resets the counter
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        const int old = __hip_atomic_fetch_add(bn.rbar + 32 * x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == full * members - 1) __hip_atomic_store(bn.rbar + 32 * x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
   }
 }
 
@@ -1428,13 +1413,6 @@ static auto small_cfg_for(const GemmArgs<T>& g, F&& f) {
 // (default 2, dWe0 only: -18 us/step; bit 1 (dW9) measured 20-40 us/step slower: the chain's
 // 256-tile GEMMs get 41 CUs (6 rounds) while dW9 runs, profiles/r02_grid_cap_ab_*)
 static int grid_cap_bits() { return opts().grid_cap; }
-static bool round_barrier() {
-  static const bool v = [] {
-    const char* e = std::getenv("GM2_ROUND_BARRIER");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
 
 // hipFuncAttributeMaxDynamicSharedMemorySize is per device: remember (device, kernel) pairs
 static void ensure_lds_attr(const void* fn, int bytes) {
@@ -1582,7 +1560,6 @@ bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hip
       check_gemm(g, 256);
       if (!force_big && (opts().tail_split & 2) && pp_enabled())
         plan_tail((g.Mp / 256) * (g.Np / 256), g.K, tail_part, tail_cnt, ep);
-      if (ep.ntiles && ep.tail_S <= 1 && round_barrier()) ep.rbar = tail_cnt;
       store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
       return true;
     }
@@ -1605,7 +1582,6 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
       check_gemm(g, 256);
       if ((opts().tail_split & 1) && pp_enabled())
         plan_tail((g.Mp / 256) * (g.Np / 256), g.K, tail_part, tail_cnt, ep);
-      if (ep.ntiles && ep.tail_S <= 1 && round_barrier()) ep.rbar = tail_cnt;
       store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
       return true;
     }

@@ -158,10 +158,6 @@ struct StoreEpi {
   int tail_R = 0, tail_cus = 0, tail_rem = 0, tail_S = 1;
   float* tail_part = nullptr;
   int* tail_cnt = nullptr;
-  // capped grid (ntiles > 0), env GM2_ROUND_BARRIER=1 (A/B): the workgroups of one XCD (equal
-  // blockIdx % 8) start each full round of tiles together -- counters rbar[32 * x], zero between
-  // launches (the last arrival resets its XCD's), no data exchanged
-  int* rbar = nullptr;
 };
 // split-tail scratch of one GEMM: at most kTailItems tile parts of 256 x 256 fp32 + counters
 constexpr int kTailItems = 256;

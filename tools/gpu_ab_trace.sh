@@ -6,8 +6,8 @@ mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
 T=$1; K=$2; R=$3; shift 3
 if [ "$K" != "skip" ]; then
-  if [ "$K" = "all" ]; then sel=""; else sel="-k $K"; fi
-  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread -rf $sel > gpurun_out/gpu_tests_$T.log 2>&1
+  if [ "$K" = "all" ]; then sel=(); else sel=(-k "$K"); fi
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread -rf "${sel[@]}" > gpurun_out/gpu_tests_$T.log 2>&1
   rc=$?; echo "pytest rc=$rc" >> gpurun_out/gpu_tests_$T.log
   [ $rc -ne 0 ] && exit $rc
 fi
