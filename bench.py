@@ -119,6 +119,8 @@ def parse():
                     help="CU mask of the workspace's side stream: this many CUs, 0 = all (GM2_OPT_SIDE_CUS)")
     ap.add_argument("--small-tile", type=int, choices=[64, 128], default=None,
                     help="N width of the forward hidden-layer GEMM tiles (GM2_OPT_SMALL_TILE)")
+    ap.add_argument("--bn-fuse", type=int, choices=[0, 1], default=None,
+                    help="forward hidden GEMMs form relu(BatchNorm(Y)) on load (GM2_OPT_BN_FUSE)")
     ap.add_argument("--recon-tile", type=int, choices=[0, 128, 256], default=None,
                     help="tile of the output-layer loss GEMM: 0 plan, 128 / 256 force (GM2_OPT_RECON_TILE)")
     ap.add_argument("--main-stream", action="store_true",
@@ -284,6 +286,8 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         ws.set_option(native.OPT_SMALL_TILE, a.small_tile)
     if a.recon_tile is not None:
         ws.set_option(native.OPT_RECON_TILE, a.recon_tile)
+    if a.bn_fuse is not None:
+        ws.set_option(native.OPT_BN_FUSE, a.bn_fuse)
     if a.dw9_last is not None:
         ws.set_option(native.OPT_DW9_LAST, a.dw9_last)
     if a.tail_split is not None:
@@ -534,9 +538,13 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
     gps = n_all / dt
     # the output layer ran bf16x3 (GM2_OPT_SAMPLE_SPLIT: one bf16 GEMM over K' = 3H, MFMA peak bf16)
     # on every chunk, or the exact-fp32 kernel (fp32 matrix peak)
-    split = ws.stat(native.STAT_SPLIT_DECODES) - n_split0 == (n + chunk - 1) // chunk
+    n_dec = (n + chunk - 1) // chunk
+    split = ws.stat(native.STAT_SPLIT_DECODES) - n_split0 == n_dec
     kflops = 2.0 * chunk * H * G * (3 if split else 1)  # executed by one full-chunk launch
-    ach = kflops / (k_ms / max(k_n, 1) * 1e-3) / 1e12
+    # every decode launches both output-layer kernels and the device runs the one the error bound
+    # picks (the other's grid exits at once): the executed FLOPs of all n genomes over the time of
+    # every mask-kernel launch
+    ach = 2.0 * n * H * G * (3 if split else 1) / (k_ms * 1e-3) / 1e12
     peak = PEAK_BF16_TFLOPS if split else PEAK_F32_TFLOPS
     # the packed masks that reached the host are the decode's: spot-check the last chunk on device
     last = (n - 1) // chunk * chunk
@@ -554,7 +562,7 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
                          "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                          "flops_per_launch": kflops,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "launch_ms": round(k_ms / max(k_n, 1), 4)}}
+                         "launch_ms": round(k_ms / max(n_dec, 1), 4), "launches": k_n, "decodes": n_dec}}
 
 
 if __name__ == "__main__":

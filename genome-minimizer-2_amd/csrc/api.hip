@@ -303,7 +303,8 @@ struct WsState {
   int side_cus = 0;                 // CU-mask size the side stream was created with (0 = all CUs)
   int cus = 0;                      // compute units of dev
   int64_t split_decodes = 0;        // sampling decodes that ran the bf16x3 output layer (GM2_STAT_*)
-  int64_t exact_decodes = 0;        // ... and the exact-fp32 one
+  int64_t exact_decodes = 0;        // ... and the exact-fp32 one (host-decided: probs requests etc.)
+  const unsigned* gate_counts = nullptr;  // device counters of the gated decodes [split, exact]
   // the queued (not yet launched) output-layer update: launched by kick() beside the next training
   // call's hidden layers, or by join() on the joining stream
   struct QueuedAdam {
@@ -557,14 +558,21 @@ const int kBlk[6][4] = {{E0W, E0B, E1G, E1BT}, {E3W, E3B, E4G, E4BT}, {E6W, E6B,
 // Pre-BatchNorm Linear: Y = in . W^T + bias (fp32 [Bp][H]) and, when `stats`, the per-128-row
 // chunk (mean, M2) partials of Y -> part. One launch when the GEMM plan is a single pass of 128-row
 // tiles (statistics in the store epilogue); otherwise split-K slabs + k_bn_fwd_partial.
+// fuse (GM2_OPT_BN_FUSE): the A operand is relu(BatchNorm(fuse->aY)) formed on load, `in` receives it
+// (the StoreEpi's a* fields; bn_fuse_ok checked the plan)
 template <typename T>
 void linear_pre_bn(const Ctx<T>& c, const T* in, int64_t ldin, int Bp, const T* W, int64_t ldw, int B, int H, int K,
-                   const float* bias, float* Y, float* part, bool stats, const int32_t* prow = nullptr) {
+                   const float* bias, float* Y, float* part, bool stats, const int32_t* prow = nullptr,
+                   const StoreEpi* fuse = nullptr) {
   GemmArgs<T> g{in, ldin, W, ldw, B, H, K, Bp, H, 0};
-  StoreEpi bn;
+  StoreEpi bn = fuse ? *fuse : StoreEpi{};
   bn.mode = stats ? 1 : 0;
   bn.part = (float2*)part;
   bn.ldp = H;
+  if (fuse) {
+    if (!launch_gemm_bn<T>(g, Y, H, bias, bn, c.s)) throw Gm2Error("BatchNorm-fused GEMM: plan changed");
+    return;
+  }
   if (!prow && launch_gemm_bn<T>(g, Y, H, bias, bn, c.s)) return;
   const int S = gemm_to_slabs<T>(c, in, ldin, Bp, W, ldw, H, B, H, K, H, 1, 1, prow);
   launch_bn_fwd_partial(c.f(c.slab_off), S, (int64_t)Bp * H, H, bias, B, H, Y, part, c.s);
@@ -672,6 +680,13 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   int64_t ldin = c.ridx ? c.ld_xres : d.Gp;
   int Kin = (int)d.Gp;
   const int64_t shadow_in[6] = {l.sE0, l.sE1, l.sE2, l.sD0, l.sD1, l.sD2};
+  // GM2_OPT_BN_FUSE: BatchNorm blocks 0, 1, 3, 4 reach their consumer (the next hidden GEMM) as
+  // statistics only (k_bn_fwd_finalize); that GEMM forms relu(BN(Y)) while loading its A operand
+  // and also stores the bf16 A the backward reads. Blocks 2 and 5 feed the heads / the loss GEMM
+  // and keep their apply pass.
+  const bool fuse_on = train && !sync && sizeof(T) == 2 && opts().bn_fuse;
+  StoreEpi fz;
+  bool pend = false;
   for (int i = 0; i < 6; ++i) {
     if (i == 3) {
       const int S = gemm_to_slabs<T>(c, c.t(l.A[2]), H, Bp, c.t(l.sHD), H, (int)d.L2r, B, 2 * L, H, 2 * L);
@@ -682,7 +697,8 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
       Kin = (int)d.Lp;
     }
     linear_pre_bn<T>(c, in, ldin, Bp, c.t(shadow_in[i]), i == 3 ? d.Lr : Kin, B, H, Kin, prm + d.off[kBlk[i][1]],
-                     c.f(l.Y[i]), c.f(l.bnpart), train != 0, i == 0 ? c.ridx : nullptr);
+                     c.f(l.Y[i]), c.f(l.bnpart), train != 0, i == 0 ? c.ridx : nullptr, pend ? &fz : nullptr);
+    pend = false;
     // a queued output-layer Adam update of the previous step starts here, beside the hidden layers
     // (HBM-bound next to latency-bound small GEMMs; the gather and the input-layer GEMM before this
     // point leave it nothing: one is HBM-bound too, the other holds every CU's registers)
@@ -691,9 +707,26 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
       launch_bn_sync_pack(c.f(l.bnpart), B, H, 0, syncb, c.s);
       c.st->allreduce(syncb, 2 * H + 2, c.s);
     }
-    launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train, prm + d.off[kBlk[i][2]],
-                           prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
-                           c.f(l.save[i]), c.t(l.A[i]), c.s, sync ? syncb : nullptr);
+    if (fuse_on && (i == 0 || i == 1 || i == 3 || i == 4) &&
+        bn_fuse_ok<T>(GemmArgs<T>{c.t(l.A[i]), H, c.t(shadow_in[i + 1]), H, B, H, H, Bp, H, 0})) {
+      launch_bn_fwd_finalize(c.f(l.bnpart), B, H, prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
+                             bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, c.f(l.save[i]), c.s);
+      fz = StoreEpi{};
+      fz.aY = c.f(l.Y[i]);
+      fz.ldaY = H;
+      fz.aSave = c.f(l.save[i]);
+      fz.aGamma = prm + d.off[kBlk[i][2]];
+      fz.aBeta = prm + d.off[kBlk[i][3]];
+      fz.aH = H;
+      fz.aRows = B;
+      if constexpr (sizeof(T) == 2) fz.aOut = c.t(l.A[i]);
+      fz.ldaOut = H;
+      pend = true;
+    } else {
+      launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train, prm + d.off[kBlk[i][2]],
+                             prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
+                             c.f(l.save[i]), c.t(l.A[i]), c.s, sync ? syncb : nullptr);
+    }
     in = c.t(l.A[i]);
     ldin = H;
     Kin = H;
@@ -971,11 +1004,13 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
 // exact path has as well. When that bound is at most kSplitBound the mask is the exact-fp32 mask
 // wherever |logit - threshold| > e, i.e. everywhere outside |logit| <= kSplitBound + 9e-8, inside
 // the 1e-3 band the parity tests exempt (fp32 arithmetic itself decides those differently by
-// summation order); otherwise -- weights or activations large enough to need it -- the call falls
-// back to the exact-fp32 kernel. Reading the two maxima is one small device->host copy per call.
-// False: not taken (the caller runs the exact path).
-constexpr double kSplitBound = 2.5e-4;
-constexpr double kSplitUnit = 4.62e-5;  // 3.02 x 2^-16, rounded up
+// summation order); otherwise -- weights or activations large enough to need it -- the exact-fp32
+// kernel runs. The choice is made on the device: both output-layer kernels are launched behind the
+// split kernels and each reads the two maxima (MaskGate) and runs only on its verdict (the other's
+// grid exits at once), so no call waits on the host: a host read of the maxima stalled every
+// chunk behind the previous chunk's mask copy on the DMA engine and drained the queue (sampling
+// 3.0 M genomes/s end to end; gm2_workspace_stat reads the per-path device counters).
+// False: not taken (the caller runs the exact path alone).
 
 bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, int64_t ldm, uint8_t* bits,
                    int64_t ldb) {
@@ -984,23 +1019,19 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
   const int H = (int)d.H, G = (int)d.G;
   if (!l.s3a || (bits && ldb * 8 < G)) return false;
   const int Bq = (int)round_up(n, 2 * kTile), Gq = (int)round_up(G, 2 * kTile);
-  unsigned* smax = (unsigned*)(c.ws + l.s3max);
+  unsigned* smax = (unsigned*)(c.ws + l.s3max);  // [a2, w2 | split count, exact count]
   bf16_t* a3 = (bf16_t*)(c.ws + l.s3a);
   bf16_t* w3 = (bf16_t*)(c.ws + l.s3w);
   HIP_OK(hipMemsetAsync(smax, 0, 8, c.s));
   launch_split3(c.f(l.A[5]), H, n, Bq, H, a3, 3 * H, smax, 0, c.s);
   launch_split3(prm + d.off[D9W], H, G, Gq, H, w3, 3 * H, smax + 1, 1, c.s);
-  unsigned hv[2] = {0u, 0u};
-  HIP_OK(hipMemcpyAsync(hv, smax, 8, hipMemcpyDeviceToHost, c.s));
-  HIP_OK(hipStreamSynchronize(c.s));
-  float a2, w2;
-  std::memcpy(&a2, &hv[0], 4);
-  std::memcpy(&w2, &hv[1], 4);
-  const double bound = kSplitUnit * std::sqrt((double)a2) * std::sqrt((double)w2) * 1.01;
-  if (!(bound <= kSplitBound)) return false;  // (NaN / inf: exact path)
+  if (c.st) c.st->gate_counts = smax + 2;
   GemmArgs<bf16_t> g{a3, 3 * H, w3, 3 * H, n, G, 3 * H, Bq, Gq, 0};
   launch_gemm_mask<bf16_t>(g, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
-                           true);
+                           true, MaskGate{smax, 1, smax + 2});
+  GemmArgs<float> ge{c.f(l.A[5]), H, c.f(l.sD3), H, n, G, H, (int)round_up(n, kTile), (int)d.Gp, 0};
+  launch_gemm_mask<float>(ge, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
+                          false, MaskGate{smax, 2, smax + 3});
   return true;
 }
 
@@ -1027,10 +1058,7 @@ void decode_chain(const Ctx<T>& c, const float* prm, float* bn, int n, uint8_t* 
     ldw = H;
   }
   if constexpr (std::is_same_v<T, float>) {
-    if (!probs && opts().sample_split && decode_split3(c, prm, n, mask, ldm, bits, ldb)) {
-      if (c.st) c.st->split_decodes++;
-      return;
-    }
+    if (!probs && opts().sample_split && decode_split3(c, prm, n, mask, ldm, bits, ldb)) return;
   }
   if (c.st) c.st->exact_decodes++;
   GemmArgs<T> g{c.t(l.A[5]), H, c.t(l.sD3), H, n, (int)d.G, H, Bp, (int)d.Gp, 0};
@@ -1568,8 +1596,16 @@ int gm2_workspace_stat(void* ws, int key, int64_t* value) {
     if (!value) throw Gm2Error("null value");
     WsState& st = ws_state(ws);
     switch (key) {
-      case GM2_STAT_SPLIT_DECODES: *value = st.split_decodes; break;
-      case GM2_STAT_EXACT_DECODES: *value = st.exact_decodes; break;
+      case GM2_STAT_SPLIT_DECODES:
+      case GM2_STAT_EXACT_DECODES: {
+        unsigned dc[2] = {0u, 0u};  // (the gated decodes' device counters: waits for the device)
+        if (st.gate_counts) {
+          HIP_OK(hipDeviceSynchronize());
+          HIP_OK(hipMemcpy(dc, st.gate_counts, 8, hipMemcpyDeviceToHost));
+        }
+        *value = key == GM2_STAT_SPLIT_DECODES ? st.split_decodes + dc[0] : st.exact_decodes + dc[1];
+        break;
+      }
       default: throw Gm2Error("unknown statistic %d", key);
     }
   });

@@ -290,6 +290,120 @@ __device__ __forceinline__ void mainloop(const T* __restrict__ P, int64_t ldp, c
 }
 
 // ---------------------------------------------------------------------------------------------
+// Main loop with the A operand formed on load (IDX 3, GM2_OPT_BN_FUSE; bf16, both operands
+// K-major): A = relu(Y * alpha + beta') rounded to bf16 for rows < aRows, 0 beyond -- the values
+// k_bn_fwd_apply writes, bit for bit -- with Y the previous layer's pre-BatchNorm output (fp32
+// [rows][ldaY]) and (alpha, beta') per K column from its saved (mean, invstd), gamma and beta, in
+// an LDS table past the staging ring. Y goes to registers two K-steps ahead (plain loads), is
+// transformed and written into the A half of its LDS stage at the swizzled chunk positions the
+// fragment reads expect; B (the weight) stays on the LDS-DMA ring. Workgroups of column block cb
+// also store the A chunks of the K-steps t = cb (mod column blocks): the bf16 activation the
+// backward's weight gradients read, each chunk written once in all. The MFMA sequence is the
+// generic main loop's, so the tile's sums are those of the unfused launch.
+// ---------------------------------------------------------------------------------------------
+template <class C>
+__device__ __forceinline__ void mainloop_bnA(const GemmArgs<bf16_t>& g, const StoreEpi& bn, int m0, int n0, int kbeg,
+                                             int nk, char* smem, f32x4 (&acc)[C::FM][C::FN]) {
+  constexpr int CPT = C::BM * 8 / C::NT;  // A chunks (8 k) per thread per K-step
+  constexpr int LPB = C::BN * 8 / C::NT;  // B LDS-DMA loads per thread per K-step
+  constexpr int NS = C::NS;
+  static_assert(NS >= 3 && CPT >= 1 && LPB >= 1 && 2 * CPT + LPB <= 63, "bnA main loop shape");
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / C::WGN, wn = wid % C::WGN;
+#pragma unroll
+  for (int a = 0; a < C::FM; ++a)
+#pragma unroll
+    for (int b = 0; b < C::FN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk <= 0) return;
+  float2* ctab = (float2*)(smem + C::LDS);  // [nk * 64]: (alpha, beta') of this split's K columns
+  for (int i = tid; i < nk * 64; i += C::NT) {
+    const int col = kbeg + i;
+    const float mean = bn.aSave[col], invstd = bn.aSave[bn.aH + col];
+    const float alpha = invstd * bn.aGamma[col];
+    ctab[i] = make_float2(alpha, fmaf(-mean, alpha, bn.aBeta[col]));
+  }
+  const int tn = g.Np / C::BN, cb = n0 / C::BN, t0 = kbeg / 64;
+  auto loadA = [&](int t, float4 (&r)[CPT][2]) {
+#pragma unroll
+    for (int ch = 0; ch < CPT; ++ch) {
+      const int id = ch * C::NT + tid, row = id >> 3, c = id & 7;
+      const float* src = bn.aY + (int64_t)min(m0 + row, bn.aRows - 1) * bn.ldaY + kbeg + t * 64 + c * 8;
+      r[ch][0] = *(const float4*)src;
+      r[ch][1] = *(const float4*)(src + 4);
+    }
+  };
+  auto putA = [&](int t, const float4 (&r)[CPT][2]) {
+    char* sa = smem + (t % NS) * C::STAGE;
+    const bool share = (t0 + t) % tn == cb;
+#pragma unroll
+    for (int ch = 0; ch < CPT; ++ch) {
+      const int id = ch * C::NT + tid, row = id >> 3, c = id & 7;
+      const bool ok = m0 + row < bn.aRows;
+      const float v[8] = {r[ch][0].x, r[ch][0].y, r[ch][0].z, r[ch][0].w, r[ch][1].x, r[ch][1].y, r[ch][1].z, r[ch][1].w};
+      const float2* k2 = ctab + t * 64 + c * 8;
+      uint32_t pk[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float2 ka = k2[2 * e], kb = k2[2 * e + 1];
+        const float a0 = ok ? fmaxf(fmaf(v[2 * e], ka.x, ka.y), 0.f) : 0.f;
+        const float a1 = ok ? fmaxf(fmaf(v[2 * e + 1], kb.x, kb.y), 0.f) : 0.f;
+        pk[e] = f2bf2(a0, a1);
+      }
+      const uint4 w = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      *(uint4*)(sa + frag_off(row, c)) = w;
+      if (share) *(uint4*)(bn.aOut + (int64_t)(m0 + row) * bn.ldaOut + kbeg + t * 64 + c * 8) = w;
+    }
+  };
+  auto stageB = [&](int t) {
+    stage_kmajor<C, bf16_t, C::BN>(g.Q, g.ldq, n0, kbeg + t * 64, smem + (t % NS) * C::STAGE + C::BM * 128, wid, lane);
+  };
+  float4 ra[CPT][2], rb[CPT][2];
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st)
+    if (st < nk) stageB(st);
+  loadA(0, ra);
+  if (nk > 1) loadA(1, rb);
+  __syncthreads();  // (the coefficient table)
+  putA(0, ra);
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * CPT) : "memory");  // B(0), older than A(0)
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // one K-step: next loads, MFMAs on stage t, step t + 1's A into its stage, barrier. `cur` holds
+  // A(t) (consumed) and receives A(t + 2); `nxt` holds A(t + 1)
+  auto step = [&](int t, float4 (&cur)[CPT][2], float4 (&nxt)[CPT][2]) {
+    const bool mb = t + NS - 1 < nk, ma = t + 2 < nk;
+    if (mb) stageB(t + NS - 1);
+    if (ma) loadA(t + 2, cur);
+    const char* sA = smem + (t % NS) * C::STAGE;
+    const char* sB = sA + C::BM * 128;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 b[C::FN];
+#pragma unroll
+      for (int ni = 0; ni < C::FN; ++ni) b[ni] = frag_bf16<true, C::BN>(sB, wn * C::WTN + ni * 16, s, lane);
+#pragma unroll
+      for (int mi = 0; mi < C::FM; ++mi) {
+        const bf16x8 a = frag_bf16<true, C::BM>(sA, wm * C::WTM + mi * 16, s, lane);
+#pragma unroll
+        for (int ni = 0; ni < C::FN; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[ni], acc[mi][ni], 0, 0, 0);
+      }
+    }
+    if (t + 1 < nk) putA(t + 1, nxt);
+    // everything older than this step's own issues has landed (B(t + 1) before A(t + 1))
+    if (mb && ma) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPB + 2 * CPT) : "memory");
+    else if (mb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPB) : "memory");
+    else if (ma) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * CPT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  for (int t = 0; t < nk; t += 2) {
+    step(t, ra, rb);
+    if (t + 1 < nk) step(t + 1, rb, ra);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Ping-pong main loop for the 256x256 bf16 tile (8 waves = two groups of four, one wave of each
 // group per SIMD). Each K-tile (64 k) is consumed in 4 phases, one 64x32 quadrant of each wave's
 // 128x64 sub-tile per phase (16 MFMAs): (a0,b0) (a0,b1) (a1,b0) (a1,b1), where a = which 64 of
@@ -632,6 +746,9 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
       __syncthreads();
     }
     mainloop_pp<AK, BK, IDX>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc, sidx);
+  } else if constexpr (IDX == 3) {
+    static_assert(sizeof(T) == 2 && AK && BK, "BatchNorm-fused A operand: bf16, K-major");
+    mainloop_bnA<C>(g, bn, tl.m0, tl.n0, kbeg, nk, smem, acc);
   } else {
     static_assert(IDX == 0, "zero-copy rows: ping-pong main loop only");
     mainloop<C, T, AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
@@ -1185,6 +1302,7 @@ struct MaskOut {
   float* probs; int64_t ldpr;
   int* counts; const uint32_t* xbits; int64_t ldxb;
   float thr;
+  MaskGate gate;
 };
 
 // PP: the 256x256 bf16 ping-pong main loop (the bf16x3 sampling decode: three bf16 GEMMs in one
@@ -1192,6 +1310,10 @@ struct MaskOut {
 template <class C, typename T, bool PP = false>
 __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float* __restrict__ bias, MaskOut o) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (o.gate.run) {  // (uniform: every workgroup of the launch takes the same branch)
+    if (split_bound_ok(o.gate.maxima) != (o.gate.run == 1)) return;
+    if (o.gate.count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(o.gate.count, 1u);
+  }
   const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP) {
@@ -1446,9 +1568,11 @@ template <class C, typename T, bool AK, bool BK, bool PP, int IDX = 0>
 static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
                            const float* bias, const StoreEpi& bn, hipStream_t s) {
   // (zero-copy rows: the index table after the staging ring -- a tile's rows, or a split's k-rows)
-  constexpr int table_max = IDX == 1 ? C::BM * 4 : IDX == 2 ? kMaxIdxRows * 4 : 0;
+  // (IDX 3: the (alpha, beta') table of the split's K columns, 8 bytes each)
+  constexpr int table_max = IDX == 1 ? C::BM * 4 : IDX == 2 ? kMaxIdxRows * 4 : IDX == 3 ? 160 * 1024 - C::LDS : 0;
   static_assert(C::LDS + table_max <= 160 * 1024, "LDS budget");
-  const int lds = C::LDS + (IDX == 1 ? C::BM * 4 : IDX == 2 ? a.k_per_split * 4 : 0);
+  const int lds = C::LDS + (IDX == 1 ? C::BM * 4 : IDX == 2 ? a.k_per_split * 4 : IDX == 3 ? a.k_per_split * 8 : 0);
+  if (lds > 160 * 1024) throw Gm2Error("gemm: %d bytes of LDS", lds);
   if (IDX == 2 && a.k_per_split > kMaxIdxRows) throw Gm2Error("zero-copy rows: %d k-rows per split", a.k_per_split);
   ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP, IDX>, C::LDS + table_max);
   int grid = tiles;
@@ -1595,6 +1719,17 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
 // plan is one pass of 128-row tiles (the statistics chunk), else the caller runs the separate pass
 
 
+// whether linear_pre_bn can take its A operand as BatchNorm(Y) on load (GM2_OPT_BN_FUSE): bf16, the
+// one-pass 128-tile plan with the statistics epilogue, both operands K-major, and the coefficient
+// table beside the staging ring
+template <typename T>
+bool bn_fuse_ok(const GemmArgs<T>& g) {
+  if (sizeof(T) != 2 || !opts().bn_fuse || !opts().bn_epilogue || !g.pk || !g.qk) return false;
+  const GemmPlan p = plan_gemm(g);
+  if (p.tile != 128 || p.splits != 1 || g.N % 4) return false;
+  return small_cfg([&](auto cfg) { return decltype(cfg)::LDS + g.K * 8 <= 160 * 1024; });
+}
+
 template <typename T>
 bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const StoreEpi& bn, hipStream_t s) {
   static_assert(Small::BM == kBnRowChunk, "statistics chunk = row tile");
@@ -1602,6 +1737,22 @@ bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bi
   const GemmPlan p = plan_gemm(g);
   if (p.tile != 128 || p.splits != 1 || (bn.mode && (g.N % 4 || bn.ldy % 4))) return false;
   check_gemm(g, 128);
+  if (bn.aY) {  // the A operand formed from the previous layer's Y (bn_fuse_ok checked the shape)
+    if constexpr (sizeof(T) == 2) {
+      small_cfg([&](auto cfg) {
+        using Cf = decltype(cfg);
+        GemmArgs<T> a = g;
+        a.k_per_split = g.K;
+        TimedLaunch tl(kKcGemmStore, s);
+        store_launch_k<Cf, T, true, true, false, 3>(a, (g.Mp / Cf::BM) * (g.Np / Cf::BN), C, nullptr, 0, ldc, 0, bias,
+                                                    bn, s);
+        GM2_CHECK_LAUNCH();
+        return 0;
+      });
+      return true;
+    }
+    throw Gm2Error("BatchNorm-fused A operand: bf16 only");
+  }
   small_cfg_for(g, [&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s); });
   return true;
 }
@@ -1698,13 +1849,13 @@ bool gemm_idx_ok(const GemmArgs<T>& g) {
 template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs, int64_t ldpr,
                       hipStream_t s, uint8_t* bits, int64_t ldb, int* counts, const uint32_t* xbits, int64_t ldxb,
-                      float thr, bool big) {
+                      float thr, bool big, MaskGate gate) {
   check_gemm(g, big ? 256 : 128);
   // (the 256-column tiles may reach past the row pitch: their bits stores stop at ldb, past G)
   if (bits && ((ldb & 15) || (((uintptr_t)bits) & 15) || ldb * 8 < (big ? g.N : g.Np)))
     throw Gm2Error("mask bits: row pitch %lld must be a multiple of 16 bytes covering the padded genes", (long long)ldb);
   if (counts && (!xbits || ldxb * 32 < g.Np)) throw Gm2Error("mask counts: target bits required");
-  MaskOut o{mask, ldm, bits, ldb, probs, ldpr, counts, xbits, ldxb, thr};
+  MaskOut o{mask, ldm, bits, ldb, probs, ldpr, counts, xbits, ldxb, thr, gate};
   TimedLaunch tl(kKcMask, s);
   if constexpr (sizeof(T) == 2) {
     if (big) {
@@ -1728,6 +1879,7 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
   template bool launch_gemm_sq<T>(const GemmArgs<T>&, float*, int64_t, double*, hipStream_t, bool, float*, int*);              \
   template int gemm_tiles<T>(const GemmArgs<T>&);                        \
   template bool launch_gemm_bn<T>(const GemmArgs<T>&, float*, int64_t, const float*, const StoreEpi&, hipStream_t);   \
+  template bool bn_fuse_ok<T>(const GemmArgs<T>&);                                                              \
   template int launch_gemm_store<T>(const GemmArgs<T>&, int, float*, float*, int, int64_t, int64_t, const float*, \
                                     hipStream_t);                                                                \
   template int gemm_recon_grid_blocks<T>(const GemmArgs<T>&);                                                   \
@@ -1741,9 +1893,11 @@ GM2_INST(float)
 GM2_INST(bf16_t)
 #undef GM2_INST
 template void launch_gemm_mask<float>(const GemmArgs<float>&, const float*, uint8_t*, int64_t, float*, int64_t,
-                                      hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float, bool);
+                                      hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float, bool,
+                                      MaskGate);
 template void launch_gemm_mask<bf16_t>(const GemmArgs<bf16_t>&, const float*, uint8_t*, int64_t, float*, int64_t,
-                                       hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float, bool);
+                                       hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float, bool,
+                                       MaskGate);
 
 #ifdef GM2_DEBUG
 GM2_DBG_TAKE_FN(dbg_take_gemm)

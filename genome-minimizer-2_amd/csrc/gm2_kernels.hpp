@@ -98,6 +98,7 @@ struct Options {
   int side_cus = 0;      // GM2_OPT_SIDE_CUS  CU mask of the side stream: this many CUs (0 = all)
   int small_tile = 128;  // GM2_OPT_SMALL_TILE  N width of the forward's hidden-layer tiles (128 or 64)
   int sample_split = 1;  // GM2_OPT_SAMPLE_SPLIT  bf16x3 output layer of the sampling decode (bound permitting)
+  int bn_fuse = 0;       // GM2_OPT_BN_FUSE  forward hidden GEMMs form their A operand as BatchNorm+ReLU of Y on load
 };
 // validated edit of one option (throws on an unknown key or a bad value)
 void option_set(Options& o, int key, int value);
@@ -158,6 +159,15 @@ struct StoreEpi {
   int tail_R = 0, tail_cus = 0, tail_rem = 0, tail_S = 1;
   float* tail_part = nullptr;
   int* tail_cnt = nullptr;
+  // A operand formed on load (GM2_OPT_BN_FUSE, launch_gemm_bn): A = relu(BatchNorm(aY)) in bf16 from
+  // the previous layer's pre-BN output aY [rows][ldaY] fp32 and its saved (mean, invstd) aSave
+  // [2][aH], gamma, beta; rows >= aRows are 0. The bf16 A is also stored to aOut [rows][ldaOut]
+  const float* aY = nullptr;
+  int64_t ldaY = 0;
+  const float *aSave = nullptr, *aGamma = nullptr, *aBeta = nullptr;
+  int aH = 0, aRows = 0;
+  bf16_t* aOut = nullptr;
+  int64_t ldaOut = 0;
 };
 // split-tail scratch of one GEMM: at most kTailItems tile parts of 256 x 256 fp32 + counters
 constexpr int kTailItems = 256;
@@ -167,6 +177,8 @@ constexpr int64_t kTailCntBytes = kTailItems * 4;
 // 128-row tiles); returns false (nothing launched) otherwise
 template <typename T>
 bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const StoreEpi& bn, hipStream_t s);
+template <typename T>
+bool bn_fuse_ok(const GemmArgs<T>& g);
 // C^T = (P . Q^T)^T into C [N][ldc] in one launch when the plan is one K pass; false otherwise
 // (tail_part / tail_cnt: split-tail scratch, kTailPartBytes / kTailCntBytes, used when the option
 // GM2_OPT_TAIL_SPLIT selects this GEMM and the tile count leaves a short last round)
@@ -207,11 +219,31 @@ void launch_gemm_recon_loss(const GemmArgs<T>& g, const float* bias, const uint3
 constexpr int kMaxIdxRows = 8192;
 template <typename T>
 bool gemm_idx_ok(const GemmArgs<T>& g);
+// The bf16x3 sampling decode's error bound (api.hip decode_split3): per logit at most
+// kSplitUnit * sqrt(max_r ||a_r||^2) * sqrt(max_g ||w_g||^2) * 1.01; the split output layer runs
+// only while that is <= kSplitBound
+constexpr double kSplitBound = 2.5e-4;
+constexpr double kSplitUnit = 4.62e-5;  // 3.02 x 2^-16, rounded up
+// Device-side choice between the split and the exact output layer (both launched, one runs): the
+// kernel reads the two squared-norm maxima (float bits) and runs when its `run` matches the bound's
+// verdict (1: split taken, 2: exact taken), counting itself in *count (once per launch)
+struct MaskGate {
+  const unsigned* maxima = nullptr;
+  int run = 0;
+  unsigned* count = nullptr;
+};
+__device__ __forceinline__ bool split_bound_ok(const unsigned* maxima) {
+  const double a2 = (double)__uint_as_float(maxima[0]), w2 = (double)__uint_as_float(maxima[1]);
+  const double bound = kSplitUnit * sqrt(a2) * sqrt(w2) * 1.01;
+  return bound <= kSplitBound;  // (NaN / inf: false, the exact path)
+}
+
 // output layer + threshold (sampling / metrics): u8 mask, packed bits, probs, per-row (TP, FP, FN)
 template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs,
                       int64_t ldpr, hipStream_t s, uint8_t* bits = nullptr, int64_t ldb = 0, int* counts = nullptr,
-                      const uint32_t* xbits = nullptr, int64_t ldxb = 0, float thr = 0.5f, bool big = false);
+                      const uint32_t* xbits = nullptr, int64_t ldxb = 0, float thr = 0.5f, bool big = false,
+                      MaskGate gate = {});
 
 // ---- kernels.hip ----
 constexpr int kBnRowChunk = 128;  // rows per BatchNorm partial-statistics chunk
@@ -245,6 +277,10 @@ template <typename T>
 void launch_transpose(const T* src, int64_t lds_, int R, int Cn, T* dst, int64_t ldd, hipStream_t s);
 // BatchNorm finalize (chunk merge per column) + elementwise apply in one launch per layer
 // (sync != nullptr: SyncBN, the global batch's all-reduced sums from launch_bn_sync_pack)
+// train-mode BatchNorm statistics of the chunk partials -> save (mean, invstd) and the running
+// statistics, without the apply pass (its consumer forms A on load: GM2_OPT_BN_FUSE)
+void launch_bn_fwd_finalize(const float* part, int B, int H, const float* gamma, const float* beta, float* rmean,
+                            float* rvar, float* save, hipStream_t s);
 template <typename T>
 void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
                          const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,

@@ -847,6 +847,17 @@ __device__ __forceinline__ float2 bn_fwd_coef(const float2* __restrict__ part, i
   return make_float2(alpha, fmaf(-meanf, alpha, beta[col]));
 }
 
+// train-mode statistics of column blockIdx.x * 256 + threadIdx.x from the chunk partials: save and
+// running statistics exactly as k_bn_fwd_apply's row-block-0 threads write them (its consumer, a
+// GEMM with the BatchNorm-fused A operand, reads save / gamma / beta)
+__global__ __launch_bounds__(256) void k_bn_fwd_finalize(const float2* __restrict__ part, int B, int H,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* rmean, float* rvar,
+                                                         float* save) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col < H) (void)bn_fwd_coef(part, B, H, 1, gamma, beta, rmean, rvar, save, col, true, nullptr);
+}
+
 // A = relu(y*alpha + beta') for rows < B, 0 for rows in [B, Bp). Grid: (ceil(H/256), Bp/64).
 template <typename T>
 __global__ __launch_bounds__(256) void k_bn_fwd_apply(const float* __restrict__ Y, int64_t ld,
@@ -1224,6 +1235,14 @@ void launch_colsum(const float* part, int rows, int64_t ld, int64_t n, float* ou
   if ((n + 63) / 64 > INT32_MAX) throw Gm2Error("colsum: %lld columns", (long long)n);
   hipLaunchKernelGGL(k_colsum2, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, part, rows, ld, n, out0, out1 ? out1 : out0,
                      out1 ? nsplit : n);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_bn_fwd_finalize(const float* part, int B, int H, const float* gamma, const float* beta, float* rmean,
+                            float* rvar, float* save, hipStream_t s) {
+  if (B <= 0) throw Gm2Error("bn_fwd_finalize: B > 0");
+  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((H + 255) / 256), dim3(256), 0, s, (const float2*)part, B, H, gamma, beta,
+                     rmean, rvar, save);
   GM2_CHECK_LAUNCH();
 }
 

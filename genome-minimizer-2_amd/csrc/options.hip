@@ -82,6 +82,7 @@ void option_set(Options& o, int key, int value) {
       o.small_tile = value;
       break;
     case GM2_OPT_SAMPLE_SPLIT: o.sample_split = value ? 1 : 0; break;
+    case GM2_OPT_BN_FUSE: o.bn_fuse = value ? 1 : 0; break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -106,6 +107,7 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_SIDE_CUS: return o.side_cus;
     case GM2_OPT_SMALL_TILE: return o.small_tile;
     case GM2_OPT_SAMPLE_SPLIT: return o.sample_split;
+    case GM2_OPT_BN_FUSE: return o.bn_fuse;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

@@ -43,6 +43,7 @@ OPT_SIDE_PRIORITY, OPT_DW9_LAST, OPT_TAIL_SPLIT, OPT_GRAD_BUCKETS = 12, 13, 14, 
 OPT_SIDE_CUS = 16
 OPT_SMALL_TILE = 17
 OPT_SAMPLE_SPLIT = 18
+OPT_BN_FUSE = 19
 STAT_SPLIT_DECODES, STAT_EXACT_DECODES = 1, 2
 # gm2_allreduce_fn (gm2.h): int (double* buf, int64_t count, void* stream, void* user)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)

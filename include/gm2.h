@@ -338,7 +338,13 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       exact-fp32 masks outside |logit| <= 2.5e-4 (inside the 1e-3 band fp32
  *                       summation order decides anyway), else the call runs the exact path
  *                       (default). 0 = always the exact-fp32 output layer. probs requests always
- *                       run exact. Costs one small device->host read per call. */
+ *                       run exact.
+ *   GM2_OPT_BN_FUSE     1 = a bf16 training forward forms the A operand of the hidden-layer GEMMs that
+ *                       follow BatchNorm blocks 1, 2, 4, 5 as relu(BatchNorm(Y)) on load (Y the
+ *                       previous layer's fp32 pre-BN output) instead of a separate apply pass; the
+ *                       bf16 activations the backward reads are stored by the same GEMMs. Results
+ *                       bit-identical to 0. Not with SyncBN (its statistics pass through the
+ *                       collective first). */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -357,7 +363,8 @@ enum {
   GM2_OPT_GRAD_BUCKETS = 15,
   GM2_OPT_SIDE_CUS = 16,
   GM2_OPT_SMALL_TILE = 17,
-  GM2_OPT_SAMPLE_SPLIT = 18
+  GM2_OPT_SAMPLE_SPLIT = 18,
+  GM2_OPT_BN_FUSE = 19
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);

@@ -579,6 +579,49 @@ def test_zero_copy_rows_bit_identical(G, B, rows_none):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("G,B,H,zero_copy,waves", [(16384, 1024, 1024, True, 8), (20000, 1000, 512, False, 8),
+                                                     (16500, 4096, 1024, True, 8), (3000, 600, 256, False, 4)])
+def test_bn_fused_operand_bit_identical(G, B, H, zero_copy, waves):
+    """GM2_OPT_BN_FUSE: the hidden GEMMs after BatchNorm blocks 0, 1, 3, 4 form relu(BN(Y)) while
+    loading their A operand (statistics finalised by k_bn_fwd_finalize, no apply pass) and store
+    the bf16 activations the backward reads. Three steps (fwd+bwd, clip statistics, Adam) must equal
+    the unfused run bit for bit: gradients, loss record, BatchNorm running statistics, parameters and
+    Adam moments -- incl. a ragged batch (1000 / 600 rows: pad rows of A are zeros), B = 4096, H = 256 /
+    512 and the 4-wave 128x128 tile (GM2_OPT_SMALL_WAVES = 4)."""
+    L = 32
+    S = 2 * B + 5
+    P, Sb = perturb_bn(*oracle_state(G, H, L, G + B + 17), seed=101)
+    X = synth_x(S, G, 102)
+    gen = torch.Generator().manual_seed(103)
+    rows = [torch.randperm(S, generator=gen)[:B].to(torch.int32).cuda() for _ in range(3)]
+    eps = [torch.randn(B, L, generator=gen).cuda() for _ in range(3)]
+    outs = []
+    for fuse in (0, 1):
+        m = to_model(P, Sb, G, H, L, native.GM2_BF16)
+        mat = ResidentMatrix(X)
+        res = mat.operands(native.GM2_BF16) if zero_copy else None
+        ws = m.workspace(native.GM2_BF16, B)
+        ws.set_option(native.OPT_BN_FUSE, fuse)
+        ws.set_option(native.OPT_SMALL_WAVES, waves)
+        grads = torch.zeros_like(m.params)
+        mom, vel = torch.zeros_like(m.params), torch.zeros_like(m.params)
+        out = []
+        for i in range(3):
+            sc = scalars(beta=0.37, wgamma=0.55, lam=0.01, step=i + 1)
+            sc[native.S_NORM_AHEAD] = 1.0
+            loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+            batch = native.make_batch(mat.data, mat.ld, rows[i], B, eps[i], resident=res)
+            native.train_fwd_bwd(ws, batch, m.params, grads, m.bn, sc, loss)
+            native.grad_norm(ws, m.params, grads, sc, loss)
+            out += [grads.clone(), loss.clone()]
+            native.adam_step(ws, m.params, grads, mom, vel, sc)
+        ws.join()
+        torch.cuda.synchronize()
+        outs.append(out + [m.params.clone(), m.bn.clone(), mom.clone(), vel.clone()])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_grad_bucket_events_off_bit_identical():
     """GM2_OPT_GRAD_BUCKETS = 0 (one process, no exchange): the backward records no bucket events --
     same gradients and loss record bit for bit -- and gm2_wait_grad_bucket then fails loudly; with
