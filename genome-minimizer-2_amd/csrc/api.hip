@@ -184,7 +184,7 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   const bool split3 = prec == GM2_F32;
   o.s3a = take(split3 ? round_up(Bm, 2 * kTile) * 3 * H * 2 : 0);
   o.s3w = take(split3 ? round_up(d.G, 2 * kTile) * 3 * H * 2 : 0);
-  o.s3max = take(16);
+  o.s3max = take((2 * kSplitShards + 2) * 4);  // squared-norm maxima shards, gated-decode counters
   o.adamscal = take(GM2_NUM_SCALARS * 4);
   o.ridx = take(round_up(Bm, 2 * kTile) * 4);
   // (only where those GEMMs can have more 256x256 tiles than a chip has CUs)
@@ -1019,19 +1019,21 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
   const int H = (int)d.H, G = (int)d.G;
   if (!l.s3a || (bits && ldb * 8 < G)) return false;
   const int Bq = (int)round_up(n, 2 * kTile), Gq = (int)round_up(G, 2 * kTile);
-  unsigned* smax = (unsigned*)(c.ws + l.s3max);  // [a2, w2 | split count, exact count]
+  // [a2 shards | w2 shards | split count, exact count]
+  unsigned* smax = (unsigned*)(c.ws + l.s3max);
+  unsigned* cnt = smax + 2 * kSplitShards;
   bf16_t* a3 = (bf16_t*)(c.ws + l.s3a);
   bf16_t* w3 = (bf16_t*)(c.ws + l.s3w);
-  HIP_OK(hipMemsetAsync(smax, 0, 8, c.s));
+  HIP_OK(hipMemsetAsync(smax, 0, 2 * kSplitShards * 4, c.s));
   launch_split3(c.f(l.A[5]), H, n, Bq, H, a3, 3 * H, smax, 0, c.s);
-  launch_split3(prm + d.off[D9W], H, G, Gq, H, w3, 3 * H, smax + 1, 1, c.s);
-  if (c.st) c.st->gate_counts = smax + 2;
+  launch_split3(prm + d.off[D9W], H, G, Gq, H, w3, 3 * H, smax + kSplitShards, 1, c.s);
+  if (c.st) c.st->gate_counts = cnt;
   GemmArgs<bf16_t> g{a3, 3 * H, w3, 3 * H, n, G, 3 * H, Bq, Gq, 0};
   launch_gemm_mask<bf16_t>(g, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
-                           true, MaskGate{smax, 1, smax + 2});
+                           true, MaskGate{smax, 1, cnt});
   GemmArgs<float> ge{c.f(l.A[5]), H, c.f(l.sD3), H, n, G, H, (int)round_up(n, kTile), (int)d.Gp, 0};
   launch_gemm_mask<float>(ge, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
-                          false, MaskGate{smax, 2, smax + 3});
+                          false, MaskGate{smax, 2, cnt + 1});
   return true;
 }
 

@@ -224,16 +224,26 @@ bool gemm_idx_ok(const GemmArgs<T>& g);
 // only while that is <= kSplitBound
 constexpr double kSplitBound = 2.5e-4;
 constexpr double kSplitUnit = 4.62e-5;  // 3.02 x 2^-16, rounded up
+// each squared-norm maximum is kept in kSplitShards words (one atomic max per split workgroup into
+// shard blockIdx % kSplitShards); the maximum is the max over the shards
+constexpr int kSplitShards = 32;
 // Device-side choice between the split and the exact output layer (both launched, one runs): the
-// kernel reads the two squared-norm maxima (float bits) and runs when its `run` matches the bound's
-// verdict (1: split taken, 2: exact taken), counting itself in *count (once per launch)
+// kernel reads the two squared-norm maxima (float bits, kSplitShards shards each: activations then
+// weights) and runs when its `run` matches the bound's verdict (1: split taken, 2: exact taken),
+// counting itself in *count (once per launch)
 struct MaskGate {
   const unsigned* maxima = nullptr;
   int run = 0;
   unsigned* count = nullptr;
 };
 __device__ __forceinline__ bool split_bound_ok(const unsigned* maxima) {
-  const double a2 = (double)__uint_as_float(maxima[0]), w2 = (double)__uint_as_float(maxima[1]);
+  unsigned am = 0u, wm = 0u;  // (non-negative floats order as unsigned)
+#pragma unroll
+  for (int i = 0; i < kSplitShards; ++i) {
+    am = max(am, maxima[i]);
+    wm = max(wm, maxima[kSplitShards + i]);
+  }
+  const double a2 = (double)__uint_as_float(am), w2 = (double)__uint_as_float(wm);
   const double bound = kSplitUnit * sqrt(a2) * sqrt(w2) * 1.01;
   return bound <= kSplitBound;  // (NaN / inf: false, the exact path)
 }
