@@ -536,7 +536,8 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     gps = n_all / dt
-    # the output layer ran bf16x3 (GM2_OPT_SAMPLE_SPLIT: one bf16 GEMM over K' = 3H, MFMA peak bf16)
+    # the output layer ran bf16x3 (GM2_OPT_SAMPLE_SPLIT: one bf16 GEMM over the (hi | lo) split operands,
+    # K' = 2H, three MFMAs per fragment pair: hi.hi + hi.lo + lo.hi; MFMA peak bf16)
     # on every chunk, or the exact-fp32 kernel (fp32 matrix peak)
     n_dec = (n + chunk - 1) // chunk
     split = ws.stat(native.STAT_SPLIT_DECODES) - n_split0 == n_dec
@@ -557,7 +558,7 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
             "essential-gene counts, D2H of packed masks + counts to pinned host memory",
             "decode_tflops": round(gps * decode_flops_per_genome(G, H, L) / 1e12, 2),
             "mean_essential_present": round(float(host_cnt.float().mean()), 2),
-            "roofline": {"bound": "mfma", "kernel": "k_gemm_mask<bf16, 256x256 pp> (K' = 3H)" if split
+            "roofline": {"bound": "mfma", "kernel": "k_gemm_mask<bf16, 256x256 pp> (K' = 2H, 3 products)" if split
                          else "k_gemm_mask<f32>", "achieved": round(ach, 2),
                          "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                          "flops_per_launch": kflops,

@@ -100,7 +100,8 @@ struct Layout {
   int64_t X1, XB1;             // second input slot: the next batch's rows, staged under this step's tail
   int64_t syncb;               // SyncBN all-reduce vector: 2H + 2 doubles
   // bf16x3 sampling decode (f32 workspaces; GM2_OPT_SAMPLE_SPLIT): the split activations
-  // [roundup(Bm, 256)][3H] and output weights [roundup(G, 256)][3H] (bf16), the two row-norm maxima
+  // [roundup(Bm, 256)][2H] and output weights [roundup(G, 256)][2H] (bf16, (hi | lo) per 32 columns),
+  // the two row-norm maxima
   int64_t s3a, s3w, s3max;
   int64_t adamscal;            // scalar block of a queued output-layer Adam update
   int64_t ridx;                // zero-copy rows: int32 [roundup(Bm, 256)] resident-matrix row per batch row
@@ -182,8 +183,8 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.XB1 = take(Bm * (d.Gp / 32) * 4);
   o.syncb = take((2 * H + 2) * 8);
   const bool split3 = prec == GM2_F32;
-  o.s3a = take(split3 ? round_up(Bm, 2 * kTile) * 3 * H * 2 : 0);
-  o.s3w = take(split3 ? round_up(d.G, 2 * kTile) * 3 * H * 2 : 0);
+  o.s3a = take(split3 ? round_up(Bm, 2 * kTile) * 2 * H * 2 : 0);
+  o.s3w = take(split3 ? round_up(d.G, 2 * kTile) * 2 * H * 2 : 0);
   o.s3max = take((2 * kSplitShards + 2) * 4);  // squared-norm maxima shards, gated-decode counters
   o.adamscal = take(GM2_NUM_SCALARS * 4);
   o.ridx = take(round_up(Bm, 2 * kTile) * 4);
@@ -995,10 +996,11 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   }
 }
 
-// The sampling decode's output layer as ONE bf16 GEMM over K' = 3H (extras.py:196-201, decode +
-// threshold): activations split (hi | hi | lo), output weights (hi | lo | hi) (launch_split3), so
-// the MFMA sums hi.hi + hi.lo + lo.hi -- each fp32 product a.w up to 3.02 x 2^-16 |a| |w| (the
-// dropped lo.lo term and the two splits' residuals), i.e. per logit at most
+// The sampling decode's output layer as ONE bf16 GEMM over K' = 2H (extras.py:196-201, decode +
+// threshold): activations and output weights split into bf16 (hi | lo) per 32 columns
+// (launch_split3), and the main loop (mainloop_pp, S3) sums hi.hi + hi.lo + lo.hi -- each fp32
+// product a.w up to 3.02 x 2^-16 |a| |w| (the dropped lo.lo term and the two splits' residuals),
+// i.e. per logit at most
 //     e = 4.62e-5 sum_k |a_k| |w_k| <= 4.62e-5 max_r ||a_r||_2 max_g ||w_g||_2
 // (Cauchy-Schwarz; the two maxima come from the split kernels) on top of the fp32 accumulation the
 // exact path has as well. When that bound is at most kSplitBound the mask is the exact-fp32 mask
@@ -1025,10 +1027,10 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
   bf16_t* a3 = (bf16_t*)(c.ws + l.s3a);
   bf16_t* w3 = (bf16_t*)(c.ws + l.s3w);
   HIP_OK(hipMemsetAsync(smax, 0, 2 * kSplitShards * 4, c.s));
-  launch_split3(c.f(l.A[5]), H, n, Bq, H, a3, 3 * H, smax, 0, c.s);
-  launch_split3(prm + d.off[D9W], H, G, Gq, H, w3, 3 * H, smax + kSplitShards, 1, c.s);
+  launch_split3(c.f(l.A[5]), H, n, Bq, H, a3, 2 * H, smax, c.s);
+  launch_split3(prm + d.off[D9W], H, G, Gq, H, w3, 2 * H, smax + kSplitShards, c.s);
   if (c.st) c.st->gate_counts = cnt;
-  GemmArgs<bf16_t> g{a3, 3 * H, w3, 3 * H, n, G, 3 * H, Bq, Gq, 0};
+  GemmArgs<bf16_t> g{a3, 2 * H, w3, 2 * H, n, G, 2 * H, Bq, Gq, 0};
   launch_gemm_mask<bf16_t>(g, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
                            true, MaskGate{smax, 1, cnt});
   GemmArgs<float> ge{c.f(l.A[5]), H, c.f(l.sD3), H, n, G, H, (int)round_up(n, kTile), (int)d.Gp, 0};

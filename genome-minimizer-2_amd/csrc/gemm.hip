@@ -475,7 +475,10 @@ __device__ __forceinline__ void barrier() {
 }
 }  // namespace pp
 
-template <bool AK, bool BK, int IDX = 0>
+// S3 (the bf16x3 split decode): both operands in launch_split3's layout -- K-substep s = 0 of each
+// K-tile is the hi part, s = 1 the lo part of the same 32 k -- and each fragment pair contributes
+// hi.hi + hi.lo + lo.hi (three MFMAs instead of the two of a plain K-tile; lo.lo is dropped)
+template <bool AK, bool BK, int IDX = 0, bool S3 = false>
 __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_t ldp, const bf16_t* __restrict__ Q,
                                             int64_t ldq, int m0, int n0, int kbeg, int nk, char* smem,
                                             f32x4 (&acc)[8][4], const int* sidx = nullptr) {
@@ -526,11 +529,17 @@ __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
+      for (int ni = 0; ni < 2; ++ni) {
+        f32x4& c = acc[a * 4 + mi][b * 2 + ni];
+        if constexpr (S3) {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi][0], fb[ni][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi][0], fb[ni][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi][1], fb[ni][0], c, 0, 0, 0);
+        } else {
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
-          acc[a * 4 + mi][b * 2 + ni] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi][s], fb[ni][s], acc[a * 4 + mi][b * 2 + ni], 0, 0, 0);
+          for (int s = 0; s < 2; ++s) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi][s], fb[ni][s], c, 0, 0, 0);
+        }
+      }
     __builtin_amdgcn_s_setprio(0);
   };
   // prologue: all four half-tiles of tile 0; A0, B0 retired before the first reads
@@ -1305,9 +1314,9 @@ struct MaskOut {
   MaskGate gate;
 };
 
-// PP: the 256x256 bf16 ping-pong main loop (the bf16x3 sampling decode: three bf16 GEMMs in one
-// K' = 3H pass, decode_chain)
-template <class C, typename T, bool PP = false>
+// PP: the 256x256 bf16 ping-pong main loop in its S3 form (the bf16x3 sampling decode: hi.hi +
+// hi.lo + lo.hi over operands split by launch_split3, K' = 2H, decode_split3)
+template <class C, typename T, bool PP = false, bool BITS = false>
 __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float* __restrict__ bias, MaskOut o) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (o.gate.run) {  // (uniform: every workgroup of the launch takes the same branch)
@@ -1318,11 +1327,50 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP) {
     static_assert(std::is_same_v<C, Big> && sizeof(T) == 2, "ping-pong: 256x256 bf16");
-    mainloop_pp<true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+    mainloop_pp<true, true, 0, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   } else {
     mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
+  if constexpr (BITS) {
+    static_assert(PP, "bit-image epilogue: the split decode's kernel");
+    {
+      // packed bits straight from the fragments: lane l of a 16x16 fragment holds row 4(l>>4) + j,
+      // column l&15, so one ballot per (mi, ni, j) yields 16 gene bits for each of 4 rows; lane r < 4
+      // gathers row r's 64 bits over the wave's 4 column fragments and writes them to a [BM][32 B]
+      // bit image (one ds_write_b64 per (mi, j), where the u8 image took one byte store per logit)
+      float bnv[C::FN];
+#pragma unroll
+      for (int ni = 0; ni < C::FN; ++ni) {
+        const int n = tl.n0 + wn * C::WTN + ni * 16 + (lane & 15);
+        bnv[ni] = n < g.N ? bias[n] : -INFINITY;  // (pad genes: never set)
+      }
+      const int sh = 16 * (lane & 3);
+#pragma unroll
+      for (int mi = 0; mi < C::FM; ++mi)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint64_t rb = 0;
+#pragma unroll
+          for (int ni = 0; ni < C::FN; ++ni) {
+            const uint64_t bal = __ballot(acc[mi][ni][j] + bnv[ni] > kMaskLogitThreshold);
+            rb |= ((bal >> sh) & 0xFFFFull) << (16 * ni);
+          }
+          if (lane < 4)
+            *(uint64_t*)(smem + (wm * C::WTM + mi * 16 + 4 * lane + j) * (C::BN / 8) + wn * (C::WTN / 8)) = rb;
+          __builtin_amdgcn_sched_barrier(0);  // (one row quad at a time: the ballots' SGPR pairs stay few)
+        }
+      __syncthreads();
+      constexpr int BPR = C::BN / 8;
+      const int rows = min(C::BM, g.M - tl.m0);
+      for (int i = threadIdx.x; i < rows * (BPR / 16); i += C::NT) {
+        const int r = i / (BPR / 16), cc = i % (BPR / 16);
+        if (tl.n0 / 8 + cc * 16 >= o.ldb) continue;  // (pad genes past the row pitch: all zero)
+        *(uint4*)(o.bits + (int64_t)(tl.m0 + r) * o.ldb + tl.n0 / 8 + cc * 16) = *(const uint4*)(smem + r * BPR + cc * 16);
+      }
+      return;
+    }
+  }
   constexpr int PI = C::BN + 16;  // u8 image pitch
   uint8_t* img = (uint8_t*)smem;  // [BM][PI] (mainloop staging is free after its last barrier)
   const bool half = o.thr == 0.5f;
@@ -1861,9 +1909,14 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
     if (big) {
       if (g.Mp % 256 || g.Np % 256 || g.K % 64) throw Gm2Error("mask (256x256): padded extents");
       constexpr int lds = std::max<int>(Big::LDS, 256 * (256 + 16));
-      ensure_lds_attr((const void*)k_gemm_mask<Big, T, true>, lds);
-      hipLaunchKernelGGL((k_gemm_mask<Big, T, true>), dim3((g.Mp / 256) * (g.Np / 256)), dim3(Big::NT), lds, s, g,
-                         bias, o);
+      const dim3 grid((g.Mp / 256) * (g.Np / 256));
+      if (bits && !mask && !probs && !counts && thr == 0.5f) {  // packed bits only: ballot epilogue
+        ensure_lds_attr((const void*)k_gemm_mask<Big, T, true, true>, lds);
+        hipLaunchKernelGGL((k_gemm_mask<Big, T, true, true>), grid, dim3(Big::NT), lds, s, g, bias, o);
+      } else {
+        ensure_lds_attr((const void*)k_gemm_mask<Big, T, true>, lds);
+        hipLaunchKernelGGL((k_gemm_mask<Big, T, true>), grid, dim3(Big::NT), lds, s, g, bias, o);
+      }
       GM2_CHECK_LAUNCH();
       return;
     }

@@ -248,7 +248,9 @@ __device__ __forceinline__ bool split_bound_ok(const unsigned* maxima) {
   return bound <= kSplitBound;  // (NaN / inf: false, the exact path)
 }
 
-// output layer + threshold (sampling / metrics): u8 mask, packed bits, probs, per-row (TP, FP, FN)
+// output layer + threshold (sampling / metrics): u8 mask, packed bits, probs, per-row (TP, FP, FN).
+// big (bf16 only): the bf16x3 split decode -- 256x256 ping-pong tiles over operands in
+// launch_split3's interleaved (hi | lo) layout, K = 2 x the hidden width, hi.hi + hi.lo + lo.hi
 template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs,
                       int64_t ldpr, hipStream_t s, uint8_t* bits = nullptr, int64_t ldb = 0, int* counts = nullptr,
@@ -277,11 +279,11 @@ void launch_bn_fwd_partial(const float* slabs, int S, int64_t slab, int64_t ld, 
 void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float* Y, int64_t ld, const float* save,
                            const float* gamma, const float* beta, int B, int H, float* part, float* dsum,
                            hipStream_t s);
-// bf16x3 split of fp32 rows (the sampling decode's output layer): out [rows_pad][3K] = (hi | hi | lo)
-// of each row (weights = 0: the activations) or (hi | lo | hi) (weights = 1); rows >= rows zero;
-// atomic max of the row sums of squares (fp32 bits) into *smax
+// bf16x3 split of fp32 rows (the sampling decode's output layer): out [rows_pad][2K], each 64-column
+// K-tile c = (hi | lo) of columns [32c, 32c + 32) (K % 32 == 0); rows >= rows zero; atomic maxima
+// of the row sums of squares (fp32 bits) into smax[0 .. kSplitShards)
 void launch_split3(const float* X, int64_t ldx, int rows, int rows_pad, int K, bf16_t* out, int64_t ldo, unsigned* smax,
-                   int weights, hipStream_t s);
+                   hipStream_t s);
 // dst[c][r] = src[r][c] for an R x Cn block (multiples of 64)
 template <typename T>
 void launch_transpose(const T* src, int64_t lds_, int R, int Cn, T* dst, int64_t ldd, hipStream_t s);

@@ -1056,16 +1056,18 @@ __global__ __launch_bounds__(256) void k_bn_sync_running(const double* __restric
 // ---------------------------------------------------------------------------------------------
 // bf16x3 split of fp32 rows for the sampling decode's output layer (decode_chain, GM2_OPT_SAMPLE_SPLIT):
 // x = hi + lo + r with hi = bf16(x), lo = bf16(x - hi) (x - hi is exact in fp32), |r| <= 2^-16 |x|.
-// Row r of X [rows][ldx] (K columns) -> out [r][3K] = parts (P0 | P1 | P2), 0 = hi, 1 = lo: the
-// decode's activations as (hi | hi | lo) and the output weights as (hi | lo | hi), so ONE bf16 GEMM
-// with K' = 3K sums hi.hi + hi.lo + lo.hi -- the fp32 product up to 3.02 x 2^-16 |x| |w| per term.
-// Rows in [rows, rows_pad) are zero. The largest row sum of squares (fp32 bits: non-negative floats
-// order as unsigned) goes to smax[0 .. kSplitShards) by atomic maxima, one per workgroup into shard
-// blockIdx % kSplitShards (the error bound, ||a||_2 ||w||_2, reads the max of the shards): with one
-// atomic per row into a single word the launches ran at the word's atomic rate (65,536 rows: 750 us
-// for 0.34 GB). One wave per row at a time (grid-stride), 8 columns per lane per pass.
+// Row r of X [rows][ldx] (K columns, K % 32 == 0) -> out [r][2K], interleaved per 32 columns: the
+// 64-column K-tile c of out holds hi[32c .. 32c+32) then lo[32c .. 32c+32). The decode's
+// activations and output weights both take this layout, and the GEMM's main loop (mainloop_pp, S3)
+// multiplies each K-tile's halves as hi.hi + hi.lo + lo.hi -- the fp32 product up to 3.02 x 2^-16
+// |x| |w| per term -- from 2K columns of operand bytes instead of the 3K of a (hi|hi|lo).(hi|lo|hi)
+// concatenation. Rows in [rows, rows_pad) are zero. The largest row sum of squares (fp32 bits:
+// non-negative floats order as unsigned) goes to smax[0 .. kSplitShards) by atomic maxima, one per
+// workgroup into shard blockIdx % kSplitShards (the error bound, ||a||_2 ||w||_2, reads the max of
+// the shards): with one atomic per row into a single word the launches ran at the word's atomic rate
+// (65,536 rows: 750 us for 0.34 GB). One wave per row at a time (grid-stride), 8 columns per lane
+// per pass.
 // ---------------------------------------------------------------------------------------------
-template <int P0, int P1, int P2>
 __global__ __launch_bounds__(256) void k_split3(const float* __restrict__ X, int64_t ldx, int rows, int rows_pad, int K,
                                               bf16_t* __restrict__ out, int64_t ldo, unsigned* __restrict__ smax) {
   __shared__ float wmax[4];
@@ -1092,10 +1094,9 @@ __global__ __launch_bounds__(256) void k_split3(const float* __restrict__ X, int
       ss = fmaf(x[2 * e + 1], x[2 * e + 1], ss);
     }
     const uint4 hv = make_uint4(hw[0], hw[1], hw[2], hw[3]), lv = make_uint4(lw[0], lw[1], lw[2], lw[3]);
-    bf16_t* o = out + (int64_t)r * ldo + k0;
-    *(uint4*)(o) = P0 ? lv : hv;
-    *(uint4*)(o + K) = P1 ? lv : hv;
-    *(uint4*)(o + 2 * K) = P2 ? lv : hv;
+    bf16_t* o = out + (int64_t)r * ldo + 2 * (k0 & ~31) + (k0 & 31);
+    *(uint4*)(o) = hv;
+    *(uint4*)(o + 32) = lv;
   }
   ss = wave_sum(ss);
   if (r < rows) mx = fmaxf(mx, ss);
@@ -1289,15 +1290,12 @@ void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const floa
 }
 
 void launch_split3(const float* X, int64_t ldx, int rows, int rows_pad, int K, bf16_t* out, int64_t ldo, unsigned* smax,
-                   int weights, hipStream_t s) {
-  if (K % 8 || ldx % 4 || ldo % 8 || ldo < 3 * K || rows > rows_pad || rows_pad % 4 || (((uintptr_t)X) & 15) ||
+                   hipStream_t s) {
+  if (K % 32 || ldx % 4 || ldo % 8 || ldo < 2 * K || rows > rows_pad || rows_pad % 4 || (((uintptr_t)X) & 15) ||
       (((uintptr_t)out) & 15))
     throw Gm2Error("split3: K %d, ld %lld / %lld, rows %d / %d", K, (long long)ldx, (long long)ldo, rows, rows_pad);
   const int grid = std::min(rows_pad / 4, 2048);  // (grid-stride over the rows: 2,048 atomics at most)
-  if (weights)
-    hipLaunchKernelGGL((k_split3<0, 1, 0>), dim3(grid), dim3(256), 0, s, X, ldx, rows, rows_pad, K, out, ldo, smax);
-  else
-    hipLaunchKernelGGL((k_split3<0, 0, 1>), dim3(grid), dim3(256), 0, s, X, ldx, rows, rows_pad, K, out, ldo, smax);
+  hipLaunchKernelGGL(k_split3, dim3(grid), dim3(256), 0, s, X, ldx, rows, rows_pad, K, out, ldo, smax);
   GM2_CHECK_LAUNCH();
 }
 

@@ -153,11 +153,13 @@ def _stats(m):
 @pytest.mark.parametrize("G,H,L,N", [(2900, 512, 32, 5000), (1000, 128, 16, 777)])
 def test_split3_decode_equals_exact_outside_its_bound(G, H, L, N):
     """GM2_OPT_SAMPLE_SPLIT (api.hip decode_split3): the output layer of the sampling decode as one
-    bf16 GEMM over K' = 3H on the (hi | hi | lo) / (hi | lo | hi) splits. The call took that path
-    (workspace counter); its packed masks differ from the exact-fp32 path's only where the fp64 logit
-    is within the path's stated bound of the threshold (|logit64| <= 2.5e-4 + 1e-7), both match the
-    oracle outside the 1e-3 band, and the u8 and packed outputs agree. G = 2900 leaves the last
-    256-gene tile past the packed row pitch (its stores must stop there)."""
+    bf16 GEMM over K' = 2H on the (hi | lo) splits, hi.hi + hi.lo + lo.hi per K-tile. The call took
+    that path (workspace counter); its packed masks differ from the exact-fp32 path's only where the
+    fp64 logit is within the path's stated bound of the threshold (|logit64| <= 2.5e-4 + 1e-7), both
+    match the oracle outside the 1e-3 band, and the u8 and packed outputs agree -- two kernels on
+    the split path: the packed one forms its bits by wave ballots from the MFMA fragments, the u8
+    one through a byte image. G = 2900 leaves the last 256-gene tile past the packed row pitch (its
+    stores must stop there); N = 5000 / 777 end in partial 256-genome tiles."""
     P, S = perturb_bn(*oracle_state(G, H, L, 80), seed=81)
     P["decoder.9.bias"] = torch.linspace(-1.0, 0.8, G)
     m = to_model(P, S, G, H, L, native.GM2_F32)
