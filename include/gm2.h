@@ -332,8 +332,8 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       K-major (the forward's hidden layers): 128 (default) or 64 (two 72-KB
  *                       workgroups per CU). Results are bit-identical.
  *   GM2_OPT_SAMPLE_SPLIT 1 = gm2_decode_mask / gm2_decode_bits without probs run the output layer as
- *                       one bf16 GEMM over 3H (the fp32 activations and weights split into bf16
- *                       hi + lo, summing hi.hi + hi.lo + lo.hi) when the error bound
+ *                       one bf16 GEMM over 2H (the fp32 activations and weights split into bf16
+ *                       hi + lo, summing hi.hi + hi.lo + lo.hi per K-tile) when the error bound
  *                       4.62e-5 max||a||_2 max||w||_2 is at most 2.5e-4; the masks then equal the
  *                       exact-fp32 masks outside |logit| <= 2.5e-4 (inside the 1e-3 band fp32
  *                       summation order decides anyway), else the call runs the exact path
