@@ -412,8 +412,9 @@ __device__ __forceinline__ void mainloop_bnA(const GemmArgs<bf16_t>& g, const St
 //   A_a : the rows {g*128 + a*64 + 0..63 : g = 0,1}   (both groups' a-halves)
 //   B_b : the cols {w*64 + b*32 + 0..31 : w = 0..3}
 // Phase p of tile t: [L] ds_read this quadrant's new fragments from buffer t&1, [G] issue one
-// half-tile of tile t+1 into buffer (t+1)&1 (A0, B0, B1, A1 at p = 0..3), [W] counted vmcnt,
-// barrier, MFMAs, barrier. Group 1 runs one barrier behind group 0, so on every SIMD one wave
+// half-tile into buffer (t+1)&1 (A0, B0, B1, A1 of tile t+1 at p = 0..3; with kPPDeep, the
+// default, B1(t+1), A1(t+1), A0(t+2), B0(t+2): each half-tile as early as the WAR rule allows),
+// [W] counted vmcnt, barrier, MFMAs, barrier. Group 1 runs one barrier behind group 0, so on every SIMD one wave
 // computes while the other reads LDS and issues loads (MI355X_MICROARCH.md "Two waves per SIMD").
 // Ordering (barrier instances counted globally, phase n = 4t+p):
 //  * RAW: a half-tile issued at phase n_i is covered by every wave's vmcnt at phase n_w and read
@@ -423,6 +424,10 @@ __device__ __forceinline__ void mainloop_bnA(const GemmArgs<bf16_t>& g, const St
 //  * WAR: a region of buffer (t+1)&1 is restaged >= 4 phases after its last read in tile t-1
 //    (the rule needs >= 2).
 // ---------------------------------------------------------------------------------------------
+// mainloop_pp issues each half-tile two phases earlier (DEEP below): 4-5 phases between issue and
+// retire instead of 2-3, 8 loads in flight -- the 256-tile kernels are bound by that latency, not
+// by their barriers or L2 -> LDS bytes (profiles/r04_pp_deep_prefetch_ab.txt: -50 us/step)
+constexpr bool kPPDeep = true;
 namespace pp {
 constexpr int REGION = 128 * 128;  // bytes of one half-tile region (128 rows x 128 B, or 64 k x 256 B)
 constexpr int BUF = 4 * REGION;    // one K-tile: A0, A1, B0, B1
@@ -482,6 +487,8 @@ template <bool AK, bool BK, int IDX = 0, bool S3 = false>
 __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_t ldp, const bf16_t* __restrict__ Q,
                                             int64_t ldq, int m0, int n0, int kbeg, int nk, char* smem,
                                             f32x4 (&acc)[8][4], const int* sidx = nullptr) {
+  // DEEP: the longer-prefetch issue order
+  constexpr bool DEEP = kPPDeep;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // wave-uniform in an SGPR: the stagger barriers below must be branched around, not exec-masked
   const int wm = __builtin_amdgcn_readfirstlane(wid >> 2), wn = wid & 3;
@@ -544,61 +551,141 @@ __device__ __forceinline__ void mainloop_pp(const bf16_t* __restrict__ P, int64_
   };
   // prologue: all four half-tiles of tile 0; A0, B0 retired before the first reads
   if constexpr (IDX == 2) pp::idx_rows<false>(sidx, 0, 0, tid, rq);
+  if constexpr (DEEP) {  // tile 0, then A0 and B0 of tile 1 (issued at phases 2 and 3 of tile -1)
 #pragma unroll
-  for (int h = 0; h < 4; ++h) issue(0, h);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    for (int h = 0; h < 4; ++h) issue(0, h);
+    if (nk > 1) {
+      issue(1, 0);
+      if constexpr (IDX == 2) pp::idx_rows<false>(sidx, 0, 1, tid, rq);
+      issue(1, 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0(0), B0(0)
+    } else {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) issue(0, h);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
   pp::barrier();
   GM2_STAMP(1);
   if (wm == 1) pp::barrier();  // stagger: group 1 one barrier behind
-  for (int t = 0; t < nk; ++t) {
-    const bool more = t + 1 < nk;
-    if constexpr (IDX == 2) {
-      if (more) pp::idx_rows<false>(sidx, 0, t + 1, tid, rq);
+  if constexpr (DEEP) {
+    // Issue order two phases earlier than below (each half-tile as soon as the WAR rule allows):
+    // tile t issues B1(t+1) at phase 0, A1(t+1) at 1, A0(t+2) at 2, B0(t+2) at 3, so every half-tile
+    // has four to five phases between its issue and its retire (two to three below). Retire points
+    // are unchanged: B1(t) at phase 0, A1(t) at 1, A0 / B0 (t+1) at 3; 8 loads stay in flight.
+    int rq2[2] = {0, 0};  // IDX 2: the k-rows of B0(t+2), read at phase 1
+    for (int t = 0; t < nk; ++t) {
+      const bool m1 = t + 1 < nk, m2 = t + 2 < nk;
+      if constexpr (IDX == 2) {
+        if (m1) pp::idx_rows<false>(sidx, 0, t + 1, tid, rq);  // B1(t+1)
+      }
+      // phase 0: (a0, b0)
+      read_a(t, 0);
+      read_b(t, 0, fb0);
+      if (m1) {
+        issue(t + 1, 2);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // retires B1(t)
+      } else {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      pp::barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(0, 0, fb0);
+      pp::barrier();
+      // phase 1: (a0, b1)
+      read_b(t, 1, fb1);
+      if constexpr (IDX == 2) {
+        if (m2) pp::idx_rows<false>(sidx, 0, t + 2, tid, rq2);
+      }
+      if (m1) {
+        issue(t + 1, 3);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // retires A1(t)
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      pp::barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(0, 1, fb1);
+      pp::barrier();
+      // phase 2: (a1, b0)
+      read_a(t, 1);
+      if (m2) issue(t + 2, 0);
+      pp::barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(1, 0, fb0);
+      pp::barrier();
+      // phase 3: (a1, b1)
+      if (m2) {
+        if constexpr (IDX == 2) {
+          rq[0] = rq2[0];
+          rq[1] = rq2[1];
+        }
+        issue(t + 2, 1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // retires A0(t+1), B0(t+1)
+      } else if (m1) {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
+      pp::barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      mma(1, 1, fb1);
+      pp::barrier();
     }
-    // phase 0: (a0, b0)
-    read_a(t, 0);
-    read_b(t, 0, fb0);
-    if (more) {
-      issue(t + 1, 0);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires B1(t)
-    } else {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  } else {
+    for (int t = 0; t < nk; ++t) {
+      const bool more = t + 1 < nk;
+      if constexpr (IDX == 2) {
+        if (more) pp::idx_rows<false>(sidx, 0, t + 1, tid, rq);
+      }
+      // phase 0: (a0, b0)
+      read_a(t, 0);
+      read_b(t, 0, fb0);
+      if (more) {
+        issue(t + 1, 0);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires B1(t)
+      } else {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      pp::barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(0, 0, fb0);
+      pp::barrier();
+      // phase 1: (a0, b1)
+      read_b(t, 1, fb1);
+      if (more) {
+        issue(t + 1, 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires A1(t)
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      pp::barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(0, 1, fb1);
+      pp::barrier();
+      // phase 2: (a1, b0)
+      read_a(t, 1);
+      if (more) issue(t + 1, 2);
+      pp::barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(1, 0, fb0);
+      pp::barrier();
+      // phase 3: (a1, b1)
+      if (more) {
+        issue(t + 1, 3);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires A0(t+1), B0(t+1)
+      }
+      pp::barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      mma(1, 1, fb1);
+      pp::barrier();
     }
-    pp::barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    mma(0, 0, fb0);
-    pp::barrier();
-    // phase 1: (a0, b1)
-    read_b(t, 1, fb1);
-    if (more) {
-      issue(t + 1, 1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires A1(t)
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    pp::barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    mma(0, 1, fb1);
-    pp::barrier();
-    // phase 2: (a1, b0)
-    read_a(t, 1);
-    if (more) issue(t + 1, 2);
-    pp::barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    mma(1, 0, fb0);
-    pp::barrier();
-    // phase 3: (a1, b1)
-    if (more) {
-      issue(t + 1, 3);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires A0(t+1), B0(t+1)
-    }
-    pp::barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    mma(1, 1, fb1);
-    pp::barrier();
   }
   if (wm == 0) pp::barrier();  // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
