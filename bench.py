@@ -22,7 +22,6 @@ holding its 1/8 shard of 12,500 strains) with its own roofline entry. Every time
 finite (losses and gradient norm): a non-finite step fails the run.
 """
 import argparse
-import contextlib
 import json
 import math
 import os
@@ -93,8 +92,6 @@ def parse():
                     help="N>1: dtype the big weight gradients are all-reduced in (gm2.ddp.GradSync)")
     ap.add_argument("--grid-cap", type=int, choices=range(8), default=None,
                     help="capped grid bits: output- (1) / input-layer (2) weight-gradient GEMMs, recon (4)")
-    ap.add_argument("--small-stages", type=int, choices=[4, 5], default=None,
-                    help="LDS ring depth of the 128x128 hidden-layer GEMM tiles (GM2_OPT_SMALL_STAGES)")
     ap.add_argument("--input-chunks", type=int, choices=[1, 4], default=None,
                     help="input-layer weight-gradient launches (default: 4 under DDP, else 1)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5-shaped (G=20,000) step line")
@@ -106,25 +103,10 @@ def parse():
                     help="print the host's enqueue time per timed step to stderr (diagnostic)")
     ap.add_argument("--no-zero-copy", action="store_true",
                     help="gather each step's rows instead of reading the resident operands in place")
-    ap.add_argument("--dw9-last", type=int, choices=[0, 1], default=None,
-                    help="output-layer weight gradient beside the input-layer one (GM2_OPT_DW9_LAST)")
     ap.add_argument("--grad-buckets", type=int, choices=[0, 1], default=0,
                     help="record gradient-bucket events on one GPU too (GM2_OPT_GRAD_BUCKETS; always 1 under DDP)")
-    ap.add_argument("--tail-split", type=int, choices=[0, 1, 2, 3], default=None,
-                    help="split the short last tile round of the weight-gradient GEMMs: bit 1 dW9, bit 2 dWe0 "
-                         "(GM2_OPT_TAIL_SPLIT)")
-    ap.add_argument("--side-priority", type=int, choices=[-1, 0, 1], default=None,
-                    help="priority of the workspace's side stream (GM2_OPT_SIDE_PRIORITY)")
-    ap.add_argument("--side-cus", type=int, default=None,
-                    help="CU mask of the workspace's side stream: this many CUs, 0 = all (GM2_OPT_SIDE_CUS)")
-    ap.add_argument("--small-tile", type=int, choices=[64, 128], default=None,
-                    help="N width of the forward hidden-layer GEMM tiles (GM2_OPT_SMALL_TILE)")
-    ap.add_argument("--bn-fuse", type=int, choices=[0, 1], default=None,
-                    help="forward hidden GEMMs form relu(BatchNorm(Y)) on load (GM2_OPT_BN_FUSE)")
     ap.add_argument("--recon-tile", type=int, choices=[0, 128, 256], default=None,
                     help="tile of the output-layer loss GEMM: 0 plan, 128 / 256 force (GM2_OPT_RECON_TILE)")
-    ap.add_argument("--main-stream", action="store_true",
-                    help="run the steps on a torch stream of their own instead of the NULL stream")
     ap.add_argument("--c5-strains", type=int, default=12500,
                     help="strains resident per rank for the C5 line (the 1/8 shard of 100,000)")
     return ap.parse_args()
@@ -269,8 +251,6 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
     # tuning switches of this workspace only (A/B measurements)
     if a.input_chunks is not None:
         ws.set_option(native.OPT_INPUT_CHUNKS, a.input_chunks)
-    if a.small_stages is not None:
-        ws.set_option(native.OPT_SMALL_STAGES, a.small_stages)
     if a.grid_cap is not None:
         ws.set_option(native.OPT_GRID_CAP, a.grid_cap)
     # the output layer's Adam update queued and launched beside the next step's hidden layers
@@ -278,20 +258,8 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
     ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, a.defer_adam if a.defer_adam is not None else 1)
     # gradient-bucket events only where an exchange waits on them (GM2_OPT_GRAD_BUCKETS)
     ws.set_option(native.OPT_GRAD_BUCKETS, 1 if world > 1 else a.grad_buckets)
-    if a.side_priority is not None:
-        ws.set_option(native.OPT_SIDE_PRIORITY, a.side_priority)
-    if a.side_cus is not None:
-        ws.set_option(native.OPT_SIDE_CUS, a.side_cus)
-    if a.small_tile is not None:
-        ws.set_option(native.OPT_SMALL_TILE, a.small_tile)
     if a.recon_tile is not None:
         ws.set_option(native.OPT_RECON_TILE, a.recon_tile)
-    if a.bn_fuse is not None:
-        ws.set_option(native.OPT_BN_FUSE, a.bn_fuse)
-    if a.dw9_last is not None:
-        ws.set_option(native.OPT_DW9_LAST, a.dw9_last)
-    if a.tail_split is not None:
-        ws.set_option(native.OPT_TAIL_SPLIT, a.tail_split)
     # zero-copy rows (gm2_batch.resident): the resident matrix's bf16 rows + target bits, built once
     # before timing, read in place by each step's input-layer GEMMs and loss epilogue (no gather)
     res = mat.operands(prec) if not a.no_zero_copy else None
@@ -312,11 +280,7 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         native.grad_norm(ws, model.params, grads, scal[i], loss[i])
         native.adam_step(ws, model.params, grads, opt.exp_avg, opt.exp_avg_sq, scal[i])
 
-    # the steps on a stream of their own (--main-stream): the CU-masked side stream of
-    # GM2_OPT_SIDE_CUS is a blocking stream, which serialises with the NULL stream only
     torch.cuda.synchronize()
-    sctx = torch.cuda.stream(torch.cuda.Stream(device=dev)) if a.main_stream else contextlib.nullcontext()
-    sctx.__enter__()
     for i in range(a.warmup):
         step(i)
     ws.join()  # (a queued output-layer update runs before the timed region, the timed steps' inside it)
@@ -333,7 +297,6 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         host_s += time.perf_counter() - h0
     ws.join()
     torch.cuda.synchronize()
-    sctx.__exit__(None, None, None)
     if a.host_timing:  # (stderr: the host's enqueue time per step, the GPU running asynchronously)
         print(f"host enqueue {1e3 * host_s / max(1, nsteps - a.warmup):.3f} ms/step", file=sys.stderr)
     if dist is not None:
@@ -355,10 +318,7 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         raise RuntimeError(f"non-finite loss / gradient norm at step(s) {np.flatnonzero(bad).tolist()}")
     info = {"prefetch": prefetch, "input_chunks": ws.get_option(native.OPT_INPUT_CHUNKS),
             "defer_adam": ws.get_option(native.OPT_DEFER_OUTPUT_ADAM),
-            "side_priority": ws.get_option(native.OPT_SIDE_PRIORITY),
-            "dw9_last": ws.get_option(native.OPT_DW9_LAST), "tail_split": ws.get_option(native.OPT_TAIL_SPLIT),
             "grad_buckets": ws.get_option(native.OPT_GRAD_BUCKETS),
-            "side_cus": ws.get_option(native.OPT_SIDE_CUS),
             "zero_copy": res is not None,
             "x": x if (rank == 0 and world == 1) else None, "mat": mat}
     del model, opt, ws, grads, sync
@@ -426,9 +386,7 @@ def main():
                                      f"{info['input_chunks']} launch(es)")
                    if world > 1 else "none (one GPU)",
                    "input_prefetch": info["prefetch"], "deferred_output_adam": info["defer_adam"],
-                   "side_priority": info["side_priority"], "dw9_last": info["dw9_last"],
-                   "tail_split": info["tail_split"], "grad_bucket_events": info["grad_buckets"],
-                   "zero_copy_rows": info["zero_copy"], "side_cus": info["side_cus"]},
+                   "grad_bucket_events": info["grad_buckets"], "zero_copy_rows": info["zero_copy"]},
         "train_tflops": round(value * train_flops_per_vector(G, H, L) / 1e12, 2),
         "nonfinite_steps": 0,
         # dominant kernel: decoder output layer GEMM [B,H]x[H,G] + fused BCE/abundance/dlogits epilogue

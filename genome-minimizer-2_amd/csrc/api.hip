@@ -85,6 +85,18 @@ Dims make_dims(const gm2_dims* d, int gpad = kTile) {
 // ---------------------------------------------------------------------------------------------
 // workspace layout (bytes). Everything 256-B aligned. Element size es = 4 (F32) or 2 (BF16).
 // ---------------------------------------------------------------------------------------------
+// The gated sampling decode's control block (uint32 words, workspace region s3ctl):
+//   [0, 16)    cumulative uint64[8] (k_decode_stats; zero from gm2_workspace_init), read by
+//              gm2_workspace_stat: split tiles, exact tiles, band elements, band flips, band
+//              overflow, decodes with split tiles, decodes without
+//   [16, 48)   split-kernel tiles of this call (sharded), [48, 80) exact-kernel tiles
+//   80         band elements found by this call, 81 bits its recompute flipped
+//   [96, ...)  block maxima of the row norms: activations (roundup(n, 256) / 256), then weights
+// Words [16, 96 + blocks) are zeroed at the start of every gated decode.
+struct DecodeCtl {
+  static constexpr int kCum = 0, kTilesSplit = 16, kTilesExact = 48, kCount = 80, kFlips = 81, kBlk = 96;
+};
+
 struct Layout {
   Dims d;
   int prec;
@@ -99,16 +111,12 @@ struct Layout {
   int64_t nahdr, nasq;         // norm-ahead header int[4] and per-tile sums of squares (NormAhead)
   int64_t X1, XB1;             // second input slot: the next batch's rows, staged under this step's tail
   int64_t syncb;               // SyncBN all-reduce vector: 2H + 2 doubles
-  // bf16x3 sampling decode (f32 workspaces; GM2_OPT_SAMPLE_SPLIT): the split activations
+  // gated sampling decode (f32 workspaces; GM2_OPT_SAMPLE_SPLIT): the split activations
   // [roundup(Bm, 256)][2H] and output weights [roundup(G, 256)][2H] (bf16, (hi | lo) per 32 columns),
-  // the two row-norm maxima
-  int64_t s3a, s3w, s3max;
+  // their row norms (s3rn, s3cn), the control block (DecodeCtl) and the band list
+  int64_t s3a, s3w, s3rn, s3cn, s3ctl, s3band;
   int64_t adamscal;            // scalar block of a queued output-layer Adam update
   int64_t ridx;                // zero-copy rows: int32 [roundup(Bm, 256)] resident-matrix row per batch row
-  // split-tail scratch of the two one-pass weight-gradient GEMMs (GM2_OPT_TAIL_SPLIT): tile parts
-  // (fp32) and arrival counters (zero from gm2_workspace_init; each launch leaves them zero)
-  int64_t tailp9, tailc9, tailp0, tailc0;
-  int tails;
 };
 
 #ifdef GM2_DEBUG
@@ -185,16 +193,12 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   const bool split3 = prec == GM2_F32;
   o.s3a = take(split3 ? round_up(Bm, 2 * kTile) * 2 * H * 2 : 0);
   o.s3w = take(split3 ? round_up(d.G, 2 * kTile) * 2 * H * 2 : 0);
-  o.s3max = take((2 * kSplitShards + 2) * 4);  // squared-norm maxima shards, gated-decode counters
+  o.s3rn = take(split3 ? round_up(Bm, 2 * kTile) * 4 : 0);
+  o.s3cn = take(split3 ? round_up(d.G, 2 * kTile) * 4 : 0);
+  o.s3ctl = take(split3 ? (DecodeCtl::kBlk + round_up(Bm, 2 * kTile) / 256 + round_up(d.G, 2 * kTile) / 256) * 4 : 0);
+  o.s3band = take(split3 ? (int64_t)kBandCap * 8 : 0);
   o.adamscal = take(GM2_NUM_SCALARS * 4);
   o.ridx = take(round_up(Bm, 2 * kTile) * 4);
-  // (only where those GEMMs can have more 256x256 tiles than a chip has CUs)
-  const bool tails = prec == GM2_BF16 && (H / 256) * (d.Gp / 256) > 256;
-  o.tails = tails ? 1 : 0;
-  o.tailp9 = take(tails ? kTailPartBytes : 0);
-  o.tailc9 = take(tails ? kTailCntBytes : 0);
-  o.tailp0 = take(tails ? kTailPartBytes : 0);
-  o.tailc0 = take(tails ? kTailCntBytes : 0);
   o.total = cur;
   return o;
 }
@@ -237,8 +241,6 @@ struct Ctx {
   }
   T* t(int64_t off) const { return (T*)(ws + off); }
   float* f(int64_t off) const { return (float*)(ws + off); }
-  float* tail_part(int64_t off) const { return lo.tails ? (float*)(ws + off) : nullptr; }
-  int* tail_cnt(int64_t off) const { return lo.tails ? (int*)(ws + off) : nullptr; }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -288,7 +290,6 @@ struct WsState {
   Options opt;
   int dev = -1;
   hipStream_t side = nullptr;
-  hipStream_t side9 = nullptr;  // GM2_OPT_SIDE_CUS > 0: the CU-masked stream of the output-layer weight gradient
   std::vector<hipEvent_t> ev;  // fork/join ring
   size_t next = 0;
   hipEvent_t bucket[GM2_GRAD_BUCKETS] = {};
@@ -300,12 +301,10 @@ struct WsState {
   void* coll_user = nullptr;
   hipEvent_t adam9_done = nullptr;  // a deferred output-layer Adam update (GM2_OPT_DEFER_OUTPUT_ADAM)
   bool adam9_pending = false;       // launched on the side stream, not yet joined
-  int side_prio = 0;                // priority the side stream was created with
-  int side_cus = 0;                 // CU-mask size the side stream was created with (0 = all CUs)
   int cus = 0;                      // compute units of dev
-  int64_t split_decodes = 0;        // sampling decodes that ran the bf16x3 output layer (GM2_STAT_*)
-  int64_t exact_decodes = 0;        // ... and the exact-fp32 one (host-decided: probs requests etc.)
-  const unsigned* gate_counts = nullptr;  // device counters of the gated decodes [split, exact]
+  int64_t exact_decodes = 0;        // decodes the host sent to the exact-fp32 kernel alone (probs requests,
+                                    // GM2_OPT_SAMPLE_SPLIT = 0, preconditions): GM2_STAT_EXACT_DECODES
+  const unsigned long long* decode_cum = nullptr;  // the gated decodes' cumulative device counters (DecodeCtl)
   // the queued (not yet launched) output-layer update: launched by kick() beside the next training
   // call's hidden layers, or by join() on the joining stream
   struct QueuedAdam {
@@ -326,8 +325,6 @@ struct WsState {
   }
   void destroy() {
     if (side) (void)hipStreamDestroy(side);
-    if (side9) (void)hipStreamDestroy(side9);
-    side9 = nullptr;
     for (auto e : ev) (void)hipEventDestroy(e);
     for (auto e : bucket)
       if (e) (void)hipEventDestroy(e);
@@ -336,45 +333,17 @@ struct WsState {
     side = nullptr;
     ev.clear();
   }
-  // the side stream when GM2_OPT_SIDE_STREAM is on (created on first use, at GM2_OPT_SIDE_PRIORITY;
-  // re-created after draining when that option changed), else nullptr
+  // the side stream when GM2_OPT_SIDE_STREAM is on (created on first use), else nullptr
   hipStream_t side_stream() {
     if (!opt.side_stream) return nullptr;
-    if ((side || side9) && (side_prio != opt.side_priority || side_cus != opt.side_cus)) {
-      if (side) HIP_OK(hipStreamSynchronize(side));
-      if (side9) HIP_OK(hipStreamSynchronize(side9));
-      if (side) HIP_OK(hipStreamDestroy(side));
-      if (side9) HIP_OK(hipStreamDestroy(side9));
-      side = side9 = nullptr;
-    }
     if (!side) {
-      int least = 0, greatest = 0;
-      HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      const int prio = opt.side_priority > 0 ? least : opt.side_priority < 0 ? greatest : 0;
-      HIP_OK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, std::min(std::max(prio, greatest), least)));
-      if (opt.side_cus > 0 && opt.side_cus < cus) {
-        // the lowest n bits: the driver deals mask bits round-robin over the XCDs (and their shader
-        // engines), so every XCD keeps the same share of CUs for the caller's stream. (A CU-masked
-        // stream is a blocking stream: it serialises with the NULL stream, so the caller's work must
-        // run on a stream of its own -- bench.py --main-stream.)
-        std::vector<uint32_t> mask((cus + 31) / 32, 0u);
-        for (int i = 0; i < opt.side_cus; ++i) mask[i / 32] |= 1u << (i % 32);
-        HIP_OK(hipExtStreamCreateWithCUMask(&side9, (uint32_t)mask.size(), mask.data()));
-      }
-      side_prio = opt.side_priority;
-      side_cus = opt.side_cus;
+      HIP_OK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
       if (ev.empty()) {
         ev.resize(64);
         for (auto& e : ev) HIP_OK(hipEventCreateWithFlags(&e, order_event_flags()));
       }
     }
     return side;
-  }
-  // the stream of the output-layer weight gradient: the CU-masked one when GM2_OPT_SIDE_CUS is set,
-  // else the side stream
-  hipStream_t dw9_stream() {
-    hipStream_t s = side_stream();
-    return side9 ? side9 : s;
   }
   void launch_queued(hipStream_t s, int max_grid = 0) {
     QueuedAdam& q = qadam;
@@ -453,14 +422,11 @@ void ws_release(void* ws) {
   auto it = ws_map().find(ws);
   if (it == ws_map().end()) return;
   WsState& st = *it->second;
-  // a deferred output-layer update must not be lost (queued) nor outlive the workspace memory it
-  // reads its scalars from (running): launch a queued one and wait for it before the state goes
-  if (st.qadam.queued) {
-    const hipStream_t s = st.side ? st.side : nullptr;
-    st.launch_queued(s);
-    HIP_OK(hipStreamSynchronize(s));
-    st.adam9_pending = false;
-  }
+  // A still-QUEUED output-layer update is dropped, not launched: release can run at garbage-collection
+  // time, after the parameter / moment buffers it would write were freed (callers join with
+  // gm2_workspace_join before releasing, as gm2.h says; the Python host does). A RUNNING one is
+  // waited for: it reads its scalar block from the workspace memory about to be freed.
+  st.qadam.queued = false;
   if (st.adam9_pending) {  // (launched on the side stream)
     if (st.side) HIP_OK(hipStreamSynchronize(st.side));
     else HIP_OK(hipEventSynchronize(st.adam9_done));
@@ -559,21 +525,14 @@ const int kBlk[6][4] = {{E0W, E0B, E1G, E1BT}, {E3W, E3B, E4G, E4BT}, {E6W, E6B,
 // Pre-BatchNorm Linear: Y = in . W^T + bias (fp32 [Bp][H]) and, when `stats`, the per-128-row
 // chunk (mean, M2) partials of Y -> part. One launch when the GEMM plan is a single pass of 128-row
 // tiles (statistics in the store epilogue); otherwise split-K slabs + k_bn_fwd_partial.
-// fuse (GM2_OPT_BN_FUSE): the A operand is relu(BatchNorm(fuse->aY)) formed on load, `in` receives it
-// (the StoreEpi's a* fields; bn_fuse_ok checked the plan)
 template <typename T>
 void linear_pre_bn(const Ctx<T>& c, const T* in, int64_t ldin, int Bp, const T* W, int64_t ldw, int B, int H, int K,
-                   const float* bias, float* Y, float* part, bool stats, const int32_t* prow = nullptr,
-                   const StoreEpi* fuse = nullptr) {
+                   const float* bias, float* Y, float* part, bool stats, const int32_t* prow = nullptr) {
   GemmArgs<T> g{in, ldin, W, ldw, B, H, K, Bp, H, 0};
-  StoreEpi bn = fuse ? *fuse : StoreEpi{};
+  StoreEpi bn;
   bn.mode = stats ? 1 : 0;
   bn.part = (float2*)part;
   bn.ldp = H;
-  if (fuse) {
-    if (!launch_gemm_bn<T>(g, Y, H, bias, bn, c.s)) throw Gm2Error("BatchNorm-fused GEMM: plan changed");
-    return;
-  }
   if (!prow && launch_gemm_bn<T>(g, Y, H, bias, bn, c.s)) return;
   const int S = gemm_to_slabs<T>(c, in, ldin, Bp, W, ldw, H, B, H, K, H, 1, 1, prow);
   launch_bn_fwd_partial(c.f(c.slab_off), S, (int64_t)Bp * H, H, bias, B, H, Y, part, c.s);
@@ -681,13 +640,6 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
   int64_t ldin = c.ridx ? c.ld_xres : d.Gp;
   int Kin = (int)d.Gp;
   const int64_t shadow_in[6] = {l.sE0, l.sE1, l.sE2, l.sD0, l.sD1, l.sD2};
-  // GM2_OPT_BN_FUSE: BatchNorm blocks 0, 1, 3, 4 reach their consumer (the next hidden GEMM) as
-  // statistics only (k_bn_fwd_finalize); that GEMM forms relu(BN(Y)) while loading its A operand
-  // and also stores the bf16 A the backward reads. Blocks 2 and 5 feed the heads / the loss GEMM
-  // and keep their apply pass.
-  const bool fuse_on = train && !sync && sizeof(T) == 2 && opts().bn_fuse;
-  StoreEpi fz;
-  bool pend = false;
   for (int i = 0; i < 6; ++i) {
     if (i == 3) {
       const int S = gemm_to_slabs<T>(c, c.t(l.A[2]), H, Bp, c.t(l.sHD), H, (int)d.L2r, B, 2 * L, H, 2 * L);
@@ -698,8 +650,7 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
       Kin = (int)d.Lp;
     }
     linear_pre_bn<T>(c, in, ldin, Bp, c.t(shadow_in[i]), i == 3 ? d.Lr : Kin, B, H, Kin, prm + d.off[kBlk[i][1]],
-                     c.f(l.Y[i]), c.f(l.bnpart), train != 0, i == 0 ? c.ridx : nullptr, pend ? &fz : nullptr);
-    pend = false;
+                     c.f(l.Y[i]), c.f(l.bnpart), train != 0, i == 0 ? c.ridx : nullptr);
     // a queued output-layer Adam update of the previous step starts here, beside the hidden layers
     // (HBM-bound next to latency-bound small GEMMs; the gather and the input-layer GEMM before this
     // point leave it nothing: one is HBM-bound too, the other holds every CU's registers)
@@ -708,26 +659,9 @@ void forward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* bn, i
       launch_bn_sync_pack(c.f(l.bnpart), B, H, 0, syncb, c.s);
       c.st->allreduce(syncb, 2 * H + 2, c.s);
     }
-    if (fuse_on && (i == 0 || i == 1 || i == 3 || i == 4) &&
-        bn_fuse_ok<T>(GemmArgs<T>{c.t(l.A[i]), H, c.t(shadow_in[i + 1]), H, B, H, H, Bp, H, 0})) {
-      launch_bn_fwd_finalize(c.f(l.bnpart), B, H, prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]],
-                             bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H, c.f(l.save[i]), c.s);
-      fz = StoreEpi{};
-      fz.aY = c.f(l.Y[i]);
-      fz.ldaY = H;
-      fz.aSave = c.f(l.save[i]);
-      fz.aGamma = prm + d.off[kBlk[i][2]];
-      fz.aBeta = prm + d.off[kBlk[i][3]];
-      fz.aH = H;
-      fz.aRows = B;
-      if constexpr (sizeof(T) == 2) fz.aOut = c.t(l.A[i]);
-      fz.ldaOut = H;
-      pend = true;
-    } else {
-      launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train, prm + d.off[kBlk[i][2]],
-                             prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
-                             c.f(l.save[i]), c.t(l.A[i]), c.s, sync ? syncb : nullptr);
-    }
+    launch_bn_fwd_apply<T>(c.f(l.Y[i]), H, c.f(l.bnpart), B, Bp, H, train, prm + d.off[kBlk[i][2]],
+                           prm + d.off[kBlk[i][3]], bn + (int64_t)i * 2 * H, bn + (int64_t)i * 2 * H + H,
+                           c.f(l.save[i]), c.t(l.A[i]), c.s, sync ? syncb : nullptr);
     in = c.t(l.A[i]);
     ldin = H;
     Kin = H;
@@ -853,34 +787,23 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     const char* e = std::getenv("GM2_TAIL_AFTER_DW9");
     return e && e[0] == '1';
   }();
-  // GM2_OPT_SIDE_CUS > 0: the (one-pass) output-layer weight gradient runs on a CU-masked stream
-  // of its own, so the hidden chain keeps the other CUs, and the hidden layers' weight gradients on
-  // the side stream do not queue behind it (split-K plans stay on the side stream: its slabs)
-  hipStream_t s9 = sr ? w.s : c.s;
-  auto output_weight_grad = [&] {
+  const hipStream_t s9 = sr ? w.s : c.s;
+  {
     const GemmArgs<T>& g9 = bg.g9;
     const bool direct9 = plan_gemm<T>(g9).splits == 1;
-    if (sr && direct9) s9 = st.dw9_stream();
-    if (sr) st.order(c.s, s9);
+    fork();
     if (!tail_after) tail_on(s9);
     if (direct9) {
       // (A5^T here on the side stream; on the main stream before the fork measured ~35 us/step
       // slower, profiles/r02_a5t_placement_ab.txt)
       launch_transpose<T>(c.t(l.A[5]), H, Bp, H, c.t(l.AT5), Bp, s9);
-      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, s9, bg.direct ? nasq : nullptr, c.tail_part(l.tailp9),
-                           c.tail_cnt(l.tailc9));
+      launch_gemm_trans<T>(g9, gr + d.off[D9W], H, s9, bg.direct ? nasq : nullptr);
     } else {
       gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
     }
     if (tail_after) tail_on(s9);  // (the output bias gradient: bucket 0 as well)
     if (st.opt.grad_buckets) HIP_OK(hipEventRecord(st.bucket[0], s9));
-  };
-  // GM2_OPT_DW9_LAST: forked beside the input-layer dWe0 GEMM instead, so the hidden-layer chain
-  // runs without the 126-us tiles of dW9 holding every CU, and the two big weight-gradient GEMMs'
-  // tile rounds interleave (their last rounds fill each other's idle CUs)
-  const bool dw9_last = st.opt.dw9_last != 0 && sr;
-  if (!dw9_last) output_weight_grad();
-  tail_on(c.s);  // (dW9 forked last: on the caller's stream)
+  }
   // dA_j = dY . W (K-major dY, MN-major W) into the slab area; when the plan allows, the GEMM's
   // epilogue also takes BatchNorm j's backward partials (sum do, sum (y-mean) do)
   bool have_part = false;
@@ -933,7 +856,6 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       // is; dWe0 starts without waiting for it (the join follows the dWe0 launch: the side stream's
       // last small GEMM / column sums run beside dWe0's first tiles instead of before them)
       if (st.opt.grad_buckets) HIP_OK(hipEventRecord(st.bucket[1], w.s));
-      if (dw9_last) output_weight_grad();
       if (input_chunked(bg, H)) {  // four row-quarter launches, bucket 2 + q final after launch q
         for (int q = 0; q < 4; ++q) {
           GemmArgs<T> gq = bg.g0;
@@ -946,8 +868,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
           st.bucket_ev[2 + q] = 2 + q;
         }
       } else {
-        if (!bg.direct || !launch_gemm_sq<T>(bg.g0, gr + d.off[E0W], G, nasq + bg.n9, c.s, false,
-                                             c.tail_part(l.tailp0), c.tail_cnt(l.tailc0)))
+        if (!bg.direct || !launch_gemm_sq<T>(bg.g0, gr + d.off[E0W], G, nasq + bg.n9, c.s, false))
           gemm_to<T>(c, c.t(l.dYT0), Bp, H, bg.g0.Q, bg.g0.ldq, Gp, H, G, Bp, gr + d.off[E0W], nullptr, 0, G, 1, 0,
                      bg.g0.qrow);
         // one launch: buckets 2..5 become final together, one event marks all four
@@ -955,7 +876,6 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
         for (int q = 0; q < 4; ++q) st.bucket_ev[2 + q] = 2;
       }
       if (sr) st.order(w.s, c.s);  // join: the caller's stream sees every weight gradient
-      if (sr && s9 != w.s) st.order(s9, c.s);
       if (nx) {  // the next batch's rows -> the other input slot, on the side stream after dWe0 (beside
                  // it, it only slows the GEMM down by its own length): under the data-parallel exchange
                  // of the input-layer gradient, or beside the clip / Adam passes on one GPU
@@ -996,46 +916,72 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   }
 }
 
-// The sampling decode's output layer as ONE bf16 GEMM over K' = 2H (extras.py:196-201, decode +
-// threshold): activations and output weights split into bf16 (hi | lo) per 32 columns
-// (launch_split3), and the main loop (mainloop_pp, S3) sums hi.hi + hi.lo + lo.hi -- each fp32
-// product a.w up to 3.02 x 2^-16 |a| |w| (the dropped lo.lo term and the two splits' residuals),
-// i.e. per logit at most
-//     e = 4.62e-5 sum_k |a_k| |w_k| <= 4.62e-5 max_r ||a_r||_2 max_g ||w_g||_2
-// (Cauchy-Schwarz; the two maxima come from the split kernels) on top of the fp32 accumulation the
-// exact path has as well. When that bound is at most kSplitBound the mask is the exact-fp32 mask
-// wherever |logit - threshold| > e, i.e. everywhere outside |logit| <= kSplitBound + 9e-8, inside
-// the 1e-3 band the parity tests exempt (fp32 arithmetic itself decides those differently by
-// summation order); otherwise -- weights or activations large enough to need it -- the exact-fp32
-// kernel runs. The choice is made on the device: both output-layer kernels are launched behind the
-// split kernels and each reads the two maxima (MaskGate) and runs only on its verdict (the other's
-// grid exits at once), so no call waits on the host: a host read of the maxima stalled every
-// chunk behind the previous chunk's mask copy on the DMA engine and drained the queue (sampling
-// 3.0 M genomes/s end to end; gm2_workspace_stat reads the per-path device counters).
-// False: not taken (the caller runs the exact path alone).
-
+// The sampling decode's output layer, gated per tile (extras.py:196-201, decode + threshold).
+//  * bf16x3 split: activations and output weights split into bf16 (hi | lo) per 32 columns
+//    (launch_split3), and the main loop (mainloop_pp, S3) sums hi.hi + hi.lo + lo.hi -- each fp32
+//    product a.w up to 3.02 x 2^-16 |a| |w| (the dropped lo.lo term and the two splits' residuals),
+//    i.e. per logit at most e = 4.62e-5 ||a_r||_2 ||w_g||_2 (Cauchy-Schwarz) on top of the fp32
+//    accumulation the exact path has as well.
+//  * Per 256 x 256 tile (genome rows x genes) the gate takes the split form when 4.62e-5 x the
+//    block's largest ||a_r|| x the block's largest ||w_g|| is at most kSplitBound (2.5e-4); every
+//    other tile runs the exact-fp32 kernel. One large activation row or weight row thus sends only
+//    its own tiles to fp32. Both kernels are launched over their full grids behind the split kernels
+//    and each tile's workgroup runs only on its verdict (the rest exit at once): no call waits on the
+//    host. (A host read of the maxima stalled every chunk behind the previous chunk's mask copy and
+//    drained the queue: 3.0 M genomes/s end to end. The first device form gated whole chunks on the
+//    global maxima, so one large row or weight sent every tile to fp32.)
+//  * Certified band (SURVEY.md 7 "Hard parts" (ii)): both epilogues list the elements whose logit
+//    lies within coef * ||a_r|| ||w_g|| of the threshold (MaskBand) -- where the reference's own fp32
+//    arithmetic, or the split, could land on either side -- and k_band_fix recomputes each listed
+//    logit in fp64 from the same fp32 activations and weights and sets its mask bit from that. The
+//    counts (tiles per path, band elements, bits the recompute flipped, list overflow) accumulate in
+//    the workspace (DecodeCtl) for gm2_workspace_stat.
+// False: not taken (the caller runs the exact path alone, without band recompute).
 bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, int64_t ldm, uint8_t* bits,
                    int64_t ldb) {
   const Dims& d = c.d;
   const Layout& l = c.lo;
   const int H = (int)d.H, G = (int)d.G;
-  if (!l.s3a || (bits && ldb * 8 < G)) return false;
   const int Bq = (int)round_up(n, 2 * kTile), Gq = (int)round_up(G, 2 * kTile);
-  // [a2 shards | w2 shards | split count, exact count]
-  unsigned* smax = (unsigned*)(c.ws + l.s3max);
-  unsigned* cnt = smax + 2 * kSplitShards;
+  // Preconditions of the split kernels and the two gated output-layer kernels, checked before
+  // anything is launched; when one fails the caller runs the exact path alone. The output weights
+  // start at off[D9W] floats into the parameter buffer, which is 2L mod 128 floats: an odd latent
+  // width leaves them only 4-B aligned (launch_split3 reads 16-B pieces). The exact kernel's packed
+  // stores need ldb * 8 >= its padded gene extent, the split kernel's the 256-padded one up to ldb.
+  if (!l.s3a || H % 32) return false;
+  if ((((uintptr_t)(prm + d.off[D9W])) | ((uintptr_t)c.f(l.A[5]))) & 15) return false;
+  if (bits && ((ldb & 15) || (((uintptr_t)bits) & 15) || ldb * 8 < d.Gp)) return false;
+  if (mask && !bits && (ldm < G)) return false;
+  unsigned* ctl = (unsigned*)(c.ws + l.s3ctl);
+  unsigned* ablk = ctl + DecodeCtl::kBlk;
+  unsigned* wblk = ablk + Bq / 256;
   bf16_t* a3 = (bf16_t*)(c.ws + l.s3a);
   bf16_t* w3 = (bf16_t*)(c.ws + l.s3w);
-  HIP_OK(hipMemsetAsync(smax, 0, 2 * kSplitShards * 4, c.s));
-  launch_split3(c.f(l.A[5]), H, n, Bq, H, a3, 2 * H, smax, c.s);
-  launch_split3(prm + d.off[D9W], H, G, Gq, H, w3, 2 * H, smax + kSplitShards, c.s);
-  if (c.st) c.st->gate_counts = cnt;
+  float* rn = c.f(l.s3rn);
+  float* cn = c.f(l.s3cn);
+  uint2* list = (uint2*)(c.ws + l.s3band);
+  const float* w9 = prm + d.off[D9W];
+  HIP_OK(hipMemsetAsync(ctl + DecodeCtl::kTilesSplit, 0, (DecodeCtl::kBlk - DecodeCtl::kTilesSplit + Bq / 256 + Gq / 256) * 4,
+                        c.s));
+  launch_split3(c.f(l.A[5]), H, n, Bq, H, a3, 2 * H, rn, ablk, c.s);
+  launch_split3(w9, H, G, Gq, H, w3, 2 * H, cn, wblk, c.s);
+  if (c.st) c.st->decode_cum = (const unsigned long long*)(ctl + DecodeCtl::kCum);
+  // band half-widths per unit ||a_r|| ||w_g|| (MaskBand): split tiles also carry the split's own error
+  // and the fp32 accumulation of its 3H products, exact tiles the fp32 accumulation of H products;
+  // both, the reference's own fp32 accumulation of H products
+  const double gH = band_gamma((double)H), g3H = band_gamma(3.0 * H);
+  const MaskBand bs{rn, cn, (float)(kSplitUnit * 1.01 + g3H + gH), ctl + DecodeCtl::kCount, list, kBandCap};
+  const MaskBand be{rn, cn, (float)(2.0 * gH), ctl + DecodeCtl::kCount, list, kBandCap};
   GemmArgs<bf16_t> g{a3, 2 * H, w3, 2 * H, n, G, 2 * H, Bq, Gq, 0};
   launch_gemm_mask<bf16_t>(g, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
-                           true, MaskGate{smax, 1, cnt});
+                           true, MaskGate{ablk, wblk, 1, ctl + DecodeCtl::kTilesSplit}, bs);
   GemmArgs<float> ge{c.f(l.A[5]), H, c.f(l.sD3), H, n, G, H, (int)round_up(n, kTile), (int)d.Gp, 0};
   launch_gemm_mask<float>(ge, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
-                          false, MaskGate{smax, 2, cnt + 1});
+                          false, MaskGate{ablk, wblk, 2, ctl + DecodeCtl::kTilesExact}, be);
+  launch_band_fix(list, ctl + DecodeCtl::kCount, kBandCap, c.f(l.A[5]), H, w9, H, prm + d.off[D9B], H, bits, ldb, mask,
+                  ldm, ctl + DecodeCtl::kFlips, c.s);
+  launch_decode_stats(ctl + DecodeCtl::kTilesSplit, ctl + DecodeCtl::kTilesExact, ctl + DecodeCtl::kCount,
+                      ctl + DecodeCtl::kFlips, kBandCap, (unsigned long long*)(ctl + DecodeCtl::kCum), c.s);
   return true;
 }
 
@@ -1601,13 +1547,26 @@ int gm2_workspace_stat(void* ws, int key, int64_t* value) {
     WsState& st = ws_state(ws);
     switch (key) {
       case GM2_STAT_SPLIT_DECODES:
-      case GM2_STAT_EXACT_DECODES: {
-        unsigned dc[2] = {0u, 0u};  // (the gated decodes' device counters: waits for the device)
-        if (st.gate_counts) {
+      case GM2_STAT_EXACT_DECODES:
+      case GM2_STAT_SPLIT_TILES:
+      case GM2_STAT_EXACT_TILES:
+      case GM2_STAT_BAND_ELEMENTS:
+      case GM2_STAT_BAND_FLIPS:
+      case GM2_STAT_BAND_OVERFLOW: {
+        unsigned long long cum[8] = {};  // (the gated decodes' device counters: waits for the device)
+        if (st.decode_cum) {
           HIP_OK(hipDeviceSynchronize());
-          HIP_OK(hipMemcpy(dc, st.gate_counts, 8, hipMemcpyDeviceToHost));
+          HIP_OK(hipMemcpy(cum, st.decode_cum, sizeof cum, hipMemcpyDeviceToHost));
         }
-        *value = key == GM2_STAT_SPLIT_DECODES ? st.split_decodes + dc[0] : st.exact_decodes + dc[1];
+        switch (key) {
+          case GM2_STAT_SPLIT_DECODES: *value = (int64_t)cum[5]; break;
+          case GM2_STAT_EXACT_DECODES: *value = st.exact_decodes + (int64_t)cum[6]; break;
+          case GM2_STAT_SPLIT_TILES: *value = (int64_t)cum[0]; break;
+          case GM2_STAT_EXACT_TILES: *value = (int64_t)cum[1]; break;
+          case GM2_STAT_BAND_ELEMENTS: *value = (int64_t)cum[2]; break;
+          case GM2_STAT_BAND_FLIPS: *value = (int64_t)cum[3]; break;
+          default: *value = (int64_t)cum[4]; break;
+        }
         break;
       }
       default: throw Gm2Error("unknown statistic %d", key);
@@ -1652,8 +1611,8 @@ int gm2_debug_check_layout(const gm2_dims* d, int precision, int64_t* n_regions,
     const int64_t named[] = {o.sE0, o.sE1, o.sE2, o.sHD, o.sD0, o.sD1, o.sD2, o.sD3, o.X, o.XB, o.HD, o.Z, o.dL,
                              o.slabs, o.side_slabs, o.DA, o.dH, o.AT5, o.dYT0, o.bnpart, o.colpart, o.losspart,
                              o.klpart, o.gradpart, o.colbwd, o.nahdr, o.nasq, o.clip, o.scal0, o.X1, o.XB1, o.syncb,
-                             o.s3a, o.s3w, o.s3max,
-                             o.adamscal, o.ridx, o.tailp9, o.tailc9, o.tailp0, o.tailc0};
+                             o.s3a, o.s3w, o.s3rn, o.s3cn, o.s3ctl, o.s3band,
+                             o.adamscal, o.ridx};
     auto known = [&](int64_t off) {
       for (const auto& x : r)
         if (x.first == off) return true;

@@ -68,13 +68,6 @@ using SmallDeep = Cfg<128, 128, 2, 2, 4>;
 // The same tile with 8 waves (2x4, 64x32 each): two waves per SIMD, so one's LDS reads and waits
 // hide behind the other's MFMAs (GM2_OPT_SMALL_WAVES = 8)
 using SmallDeep8 = Cfg<128, 128, 2, 4, 4>;
-// Five stages (the whole 160 KB LDS): four K-steps in flight (GM2_OPT_SMALL_STAGES = 5)
-using SmallDeep5 = Cfg<128, 128, 2, 2, 5>;
-using SmallDeep85 = Cfg<128, 128, 2, 4, 5>;
-// Half-width tiles (GM2_OPT_SMALL_TILE = 64; bf16, both operands K-major: the forward's hidden
-// layers): 128x64, 4 waves (64x32 each), 3-stage ring of 24 KB -- 72 KB, two workgroups per CU, so
-// twice the tiles (and requests in flight) per CU at 1.5x the operand bytes per FLOP
-using SmallHalf = Cfg<128, 64, 2, 2, 3, 2>;
 
 struct TileXY {
   int m0, n0, split, t;
@@ -286,120 +279,6 @@ __device__ __forceinline__ void mainloop(const T* __restrict__ P, int64_t ldp, c
     }
     wait_stages<C>(min(NS - 2, nk - 2 - kt));
     __syncthreads();
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Main loop with the A operand formed on load (IDX 3, GM2_OPT_BN_FUSE; bf16, both operands
-// K-major): A = relu(Y * alpha + beta') rounded to bf16 for rows < aRows, 0 beyond -- the values
-// k_bn_fwd_apply writes, bit for bit -- with Y the previous layer's pre-BatchNorm output (fp32
-// [rows][ldaY]) and (alpha, beta') per K column from its saved (mean, invstd), gamma and beta, in
-// an LDS table past the staging ring. Y goes to registers two K-steps ahead (plain loads), is
-// transformed and written into the A half of its LDS stage at the swizzled chunk positions the
-// fragment reads expect; B (the weight) stays on the LDS-DMA ring. Workgroups of column block cb
-// also store the A chunks of the K-steps t = cb (mod column blocks): the bf16 activation the
-// backward's weight gradients read, each chunk written once in all. The MFMA sequence is the
-// generic main loop's, so the tile's sums are those of the unfused launch.
-// ---------------------------------------------------------------------------------------------
-template <class C>
-__device__ __forceinline__ void mainloop_bnA(const GemmArgs<bf16_t>& g, const StoreEpi& bn, int m0, int n0, int kbeg,
-                                             int nk, char* smem, f32x4 (&acc)[C::FM][C::FN]) {
-  constexpr int CPT = C::BM * 8 / C::NT;  // A chunks (8 k) per thread per K-step
-  constexpr int LPB = C::BN * 8 / C::NT;  // B LDS-DMA loads per thread per K-step
-  constexpr int NS = C::NS;
-  static_assert(NS >= 3 && CPT >= 1 && LPB >= 1 && 2 * CPT + LPB <= 63, "bnA main loop shape");
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / C::WGN, wn = wid % C::WGN;
-#pragma unroll
-  for (int a = 0; a < C::FM; ++a)
-#pragma unroll
-    for (int b = 0; b < C::FN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (nk <= 0) return;
-  float2* ctab = (float2*)(smem + C::LDS);  // [nk * 64]: (alpha, beta') of this split's K columns
-  for (int i = tid; i < nk * 64; i += C::NT) {
-    const int col = kbeg + i;
-    const float mean = bn.aSave[col], invstd = bn.aSave[bn.aH + col];
-    const float alpha = invstd * bn.aGamma[col];
-    ctab[i] = make_float2(alpha, fmaf(-mean, alpha, bn.aBeta[col]));
-  }
-  const int tn = g.Np / C::BN, cb = n0 / C::BN, t0 = kbeg / 64;
-  auto loadA = [&](int t, float4 (&r)[CPT][2]) {
-#pragma unroll
-    for (int ch = 0; ch < CPT; ++ch) {
-      const int id = ch * C::NT + tid, row = id >> 3, c = id & 7;
-      const float* src = bn.aY + (int64_t)min(m0 + row, bn.aRows - 1) * bn.ldaY + kbeg + t * 64 + c * 8;
-      r[ch][0] = *(const float4*)src;
-      r[ch][1] = *(const float4*)(src + 4);
-    }
-  };
-  auto putA = [&](int t, const float4 (&r)[CPT][2]) {
-    char* sa = smem + (t % NS) * C::STAGE;
-    const bool share = (t0 + t) % tn == cb;
-#pragma unroll
-    for (int ch = 0; ch < CPT; ++ch) {
-      const int id = ch * C::NT + tid, row = id >> 3, c = id & 7;
-      const bool ok = m0 + row < bn.aRows;
-      const float v[8] = {r[ch][0].x, r[ch][0].y, r[ch][0].z, r[ch][0].w, r[ch][1].x, r[ch][1].y, r[ch][1].z, r[ch][1].w};
-      const float2* k2 = ctab + t * 64 + c * 8;
-      uint32_t pk[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float2 ka = k2[2 * e], kb = k2[2 * e + 1];
-        const float a0 = ok ? fmaxf(fmaf(v[2 * e], ka.x, ka.y), 0.f) : 0.f;
-        const float a1 = ok ? fmaxf(fmaf(v[2 * e + 1], kb.x, kb.y), 0.f) : 0.f;
-        pk[e] = f2bf2(a0, a1);
-      }
-      const uint4 w = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-      *(uint4*)(sa + frag_off(row, c)) = w;
-      if (share) *(uint4*)(bn.aOut + (int64_t)(m0 + row) * bn.ldaOut + kbeg + t * 64 + c * 8) = w;
-    }
-  };
-  auto stageB = [&](int t) {
-    stage_kmajor<C, bf16_t, C::BN>(g.Q, g.ldq, n0, kbeg + t * 64, smem + (t % NS) * C::STAGE + C::BM * 128, wid, lane);
-  };
-  float4 ra[CPT][2], rb[CPT][2];
-#pragma unroll
-  for (int st = 0; st < NS - 1; ++st)
-    if (st < nk) stageB(st);
-  loadA(0, ra);
-  if (nk > 1) loadA(1, rb);
-  __syncthreads();  // (the coefficient table)
-  putA(0, ra);
-  if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * CPT) : "memory");  // B(0), older than A(0)
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // one K-step: next loads, MFMAs on stage t, step t + 1's A into its stage, barrier. `cur` holds
-  // A(t) (consumed) and receives A(t + 2); `nxt` holds A(t + 1)
-  auto step = [&](int t, float4 (&cur)[CPT][2], float4 (&nxt)[CPT][2]) {
-    const bool mb = t + NS - 1 < nk, ma = t + 2 < nk;
-    if (mb) stageB(t + NS - 1);
-    if (ma) loadA(t + 2, cur);
-    const char* sA = smem + (t % NS) * C::STAGE;
-    const char* sB = sA + C::BM * 128;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 b[C::FN];
-#pragma unroll
-      for (int ni = 0; ni < C::FN; ++ni) b[ni] = frag_bf16<true, C::BN>(sB, wn * C::WTN + ni * 16, s, lane);
-#pragma unroll
-      for (int mi = 0; mi < C::FM; ++mi) {
-        const bf16x8 a = frag_bf16<true, C::BM>(sA, wm * C::WTM + mi * 16, s, lane);
-#pragma unroll
-        for (int ni = 0; ni < C::FN; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[ni], acc[mi][ni], 0, 0, 0);
-      }
-    }
-    if (t + 1 < nk) putA(t + 1, nxt);
-    // everything older than this step's own issues has landed (B(t + 1) before A(t + 1))
-    if (mb && ma) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPB + 2 * CPT) : "memory");
-    else if (mb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPB) : "memory");
-    else if (ma) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * CPT) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  };
-  for (int t = 0; t < nk; t += 2) {
-    step(t, ra, rb);
-    if (t + 1 < nk) step(t + 1, rb, ra);
   }
 }
 
@@ -713,64 +592,7 @@ __device__ __forceinline__ double sq4(float a, float b, float c, float d) {
 template <class C, typename T, bool AK, bool BK, bool PP, int IDX>
 __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g, float* __restrict__ C0,
                                            float* __restrict__ C1, int msplit, int64_t ldc, int64_t slab,
-                                           const float* __restrict__ bias, const StoreEpi& bn, char* smem,
-                                           int tj = -1, int part = 0);
-
-// Split tail (StoreEpi::tail_S > 1): part `part` of tail tile tj has its K-part's accumulators in
-// acc. Every part stores them (lane-linear, 16-B per lane, coalesced) into its slot and counts
-// itself in; the last to arrive sums the slots in part order -- its own from registers -- into
-// acc, resets the tile's counter for the next launch and returns true (it runs the epilogue); the
-// others return false. No workgroup waits on another. The parts may run on different XCDs (L2s
-// not coherent with each other): the slots move through system-coherent (sc1) buffer stores /
-// loads, the stores drained before the count -- no cache-wide writeback or invalidate, which would
-// cost every other workgroup on the XCD its cached operands.
-constexpr int kSc1 = 16;  // buffer instruction cache policy: sc1
-
-template <class C>
-__device__ __forceinline__ bool tail_join(f32x4 (&acc)[C::FM][C::FN], const StoreEpi& bn, int tj, int part,
-                                          char* smem) {
-  constexpr int NF = C::FM * C::FN;
-  const int S = bn.tail_S;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(bn.tail_part, 0, 0x7fffffff, 0x00020000);
-  // byte offset of fragment f of part q's slot for this thread
-  auto off = [&](int q, int f) { return ((tj * S + q) * NF + f) * C::NT * 16 + (int)threadIdx.x * 16; };
-#pragma unroll
-  for (int mi = 0; mi < C::FM; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < C::FN; ++ni)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[mi][ni]), rs, off(part, mi * C::FN + ni),
-                                             0, kSc1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* flag = (int*)smem;  // (the staging LDS is free after the main loop)
-  if (threadIdx.x == 0)
-    *flag = __hip_atomic_fetch_add(bn.tail_cnt + tj, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const int arrived = *flag;
-  if (arrived != S - 1) return false;
-  auto ld = [&](int q, int f) {
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off(q, f), 0, kSc1));
-  };
-  if (S == 2) {  // one other part: a + b == b + a, so either order is part order
-    const int other = part ^ 1;
-#pragma unroll
-    for (int mi = 0; mi < C::FM; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < C::FN; ++ni) acc[mi][ni] = acc[mi][ni] + ld(other, mi * C::FN + ni);
-  } else {
-#pragma unroll
-    for (int mi = 0; mi < C::FM; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < C::FN; ++ni) {
-        f32x4 sum = part == 0 ? acc[mi][ni] : ld(0, mi * C::FN + ni);
-        for (int q = 1; q < S; ++q) sum = sum + (q == part ? acc[mi][ni] : ld(q, mi * C::FN + ni));
-        acc[mi][ni] = sum;
-      }
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(bn.tail_cnt + tj, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  return true;
-}
+                                           const float* __restrict__ bias, const StoreEpi& bn, char* smem);
 
 // IDX (zero-copy rows, PP only): 1 = P's rows through g.prow, 2 = Q's k-rows through g.qrow; the
 // tile's slice of the index array sits in an LDS table after the staging ring
@@ -781,22 +603,6 @@ __global__ __launch_bounds__(C::NT, C::MINW) void k_gemm_store(GemmArgs<T> g, fl
   extern __shared__ __attribute__((aligned(16))) char smem[];
   GM2_STAMP(0);
   const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
-  if constexpr (std::is_same_v<C, Big>) {
-    if (bn.tail_S > 1) {  // split tail: one item per workgroup, whole tiles first (see StoreEpi)
-      // XCD-aware order within each dispatch round of tail_cus workgroups, rounds in launch order,
-      // so the tail parts are the last round
-      const int base = (blockIdx.x / bn.tail_cus) * bn.tail_cus;
-      const int w = base + xcd_wg(blockIdx.x - base, min(bn.tail_cus, (int)gridDim.x - base));
-      if (w < bn.tail_R) {
-        store_tile<C, T, AK, BK, PP, IDX>(tile_at<C>(w, tm, tn, 0), g, C0, C1, msplit, ldc, slab, bias, bn, smem);
-      } else {
-        const int tj = (w - bn.tail_R) / bn.tail_S;
-        store_tile<C, T, AK, BK, PP, IDX>(tile_at<C>(bn.tail_R + tj, tm, tn, 0), g, C0, C1, msplit, ldc, slab, bias,
-                                          bn, smem, tj, w - bn.tail_R - tj * bn.tail_S);
-      }
-      return;
-    }
-  }
   if (bn.ntiles == 0) {  // one tile per workgroup
     store_tile<C, T, AK, BK, PP, IDX>(tile_of<C>(tm, tn), g, C0, C1, msplit, ldc, slab, bias, bn, smem);
     return;
@@ -814,15 +620,9 @@ __global__ __launch_bounds__(C::NT, C::MINW) void k_gemm_store(GemmArgs<T> g, fl
 template <class C, typename T, bool AK, bool BK, bool PP, int IDX>
 __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g, float* __restrict__ C0,
                                            float* __restrict__ C1, int msplit, int64_t ldc, int64_t slab,
-                                           const float* __restrict__ bias, const StoreEpi& bn, char* smem,
-                                           int tj, int part) {
-  int kbeg = tl.split * g.k_per_split;
-  int kend = min(g.K, kbeg + g.k_per_split);
-  if (tj >= 0) {  // split-tail part: K-tiles [part * per, (part + 1) * per) of the one pass
-    const int per = (g.K / E<T>::KT + bn.tail_S - 1) / bn.tail_S;
-    kbeg = part * per * E<T>::KT;
-    kend = min(g.K, kbeg + per * E<T>::KT);
-  }
+                                           const float* __restrict__ bias, const StoreEpi& bn, char* smem) {
+  const int kbeg = tl.split * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = (kend - kbeg) / E<T>::KT;
   GM2_DBG(tl.m0 + C::BM <= g.Mp && tl.n0 + C::BN <= g.Np && kbeg >= 0 && kend <= g.K, kDbgTile);
   f32x4 acc[C::FM][C::FN];
@@ -842,15 +642,10 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
       __syncthreads();
     }
     mainloop_pp<AK, BK, IDX>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc, sidx);
-  } else if constexpr (IDX == 3) {
-    static_assert(sizeof(T) == 2 && AK && BK, "BatchNorm-fused A operand: bf16, K-major");
-    mainloop_bnA<C>(g, bn, tl.m0, tl.n0, kbeg, nk, smem, acc);
   } else {
     static_assert(IDX == 0, "zero-copy rows: ping-pong main loop only");
     mainloop<C, T, AK, BK>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, kbeg, nk, smem, acc);
   }
-  GM2_STAMP(5);
-  if (tj >= 0 && !tail_join<C>(acc, bn, tj, part, smem)) return;
   GM2_STAMP(2);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   float* Cz = C0 + (int64_t)tl.split * slab;
@@ -1399,18 +1194,39 @@ struct MaskOut {
   int* counts; const uint32_t* xbits; int64_t ldxb;
   float thr;
   MaskGate gate;
+  MaskBand band;
 };
+
+// The certified band (MaskBand): the tile's row norms and column norms go to LDS past the staging
+// ring before the main loop (whose barriers order them before the epilogue); an element is in the
+// band when |l - T| <= ||a_r|| * (coef * ||w_g||). The epilogues only flag a lane (a few VALU per
+// element); a wave with a flagged lane re-walks its fragments and appends the flagged (row, gene)
+// pairs (rare: a handful per tile).
+template <class C>
+__device__ __forceinline__ void band_stage(const MaskBand& b, const TileXY& tl, char* smem) {
+  float* brn = (float*)(smem + C::LDS);
+  for (int i = threadIdx.x; i < C::BM + C::BN; i += C::NT)
+    brn[i] = i < C::BM ? b.rn[tl.m0 + i] : b.cn[tl.n0 + i - C::BM];
+}
+
+__device__ __forceinline__ void band_push(const MaskBand& b, int r, int gcol) {
+  const unsigned slot = atomicAdd(b.count, 1u);
+  if (slot < b.cap) b.list[slot] = make_uint2((unsigned)r, (unsigned)gcol);
+}
 
 // PP: the 256x256 bf16 ping-pong main loop in its S3 form (the bf16x3 sampling decode: hi.hi +
 // hi.lo + lo.hi over operands split by launch_split3, K' = 2H, decode_split3)
 template <class C, typename T, bool PP = false, bool BITS = false>
 __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float* __restrict__ bias, MaskOut o) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (o.gate.run) {  // (uniform: every workgroup of the launch takes the same branch)
-    if (split_bound_ok(o.gate.maxima) != (o.gate.run == 1)) return;
-    if (o.gate.count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(o.gate.count, 1u);
-  }
   const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
+  if (o.gate.run) {  // per tile: the verdict of the 256 x 256 block this tile lies in (uniform per workgroup)
+    if (split_tile_ok(o.gate, tl.m0, tl.n0) != (o.gate.run == 1)) return;
+    if (threadIdx.x == 0) atomicAdd(o.gate.tiles + blockIdx.x % kSplitShards, 1u);
+  }
+  const bool bchk = o.band.rn != nullptr;
+  if (bchk) band_stage<C>(o.band, tl, smem);
+  const float* brn = (const float*)(smem + C::LDS);  // [BM] row norms, then [BN] column norms
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP) {
     static_assert(std::is_same_v<C, Big> && sizeof(T) == 2, "ping-pong: 256x256 bf16");
@@ -1426,27 +1242,50 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
       // column l&15, so one ballot per (mi, ni, j) yields 16 gene bits for each of 4 rows; lane r < 4
       // gathers row r's 64 bits over the wave's 4 column fragments and writes them to a [BM][32 B]
       // bit image (one ds_write_b64 per (mi, j), where the u8 image took one byte store per logit)
-      float bnv[C::FN];
+      float bnv[C::FN], ce[C::FN];
 #pragma unroll
       for (int ni = 0; ni < C::FN; ++ni) {
         const int n = tl.n0 + wn * C::WTN + ni * 16 + (lane & 15);
-        bnv[ni] = n < g.N ? bias[n] : -INFINITY;  // (pad genes: never set)
+        bnv[ni] = n < g.N ? bias[n] : -INFINITY;  // (pad genes: never set, never in the band)
+        ce[ni] = bchk ? o.band.coef * brn[C::BM + wn * C::WTN + ni * 16 + (lane & 15)] : 0.f;
       }
       const int sh = 16 * (lane & 3);
+      bool anyb = false;
 #pragma unroll
-      for (int mi = 0; mi < C::FM; ++mi)
+      for (int mi = 0; mi < C::FM; ++mi) {
+        const float4 ra4 = bchk ? *(const float4*)(brn + wm * C::WTM + mi * 16 + 4 * (lane >> 4))
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float ra[4] = {ra4.x, ra4.y, ra4.z, ra4.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           uint64_t rb = 0;
 #pragma unroll
           for (int ni = 0; ni < C::FN; ++ni) {
-            const uint64_t bal = __ballot(acc[mi][ni][j] + bnv[ni] > kMaskLogitThreshold);
+            const float l = acc[mi][ni][j] + bnv[ni];
+            const uint64_t bal = __ballot(l > kMaskLogitThreshold);
             rb |= ((bal >> sh) & 0xFFFFull) << (16 * ni);
+            anyb |= fabsf(l - kMaskLogitThreshold) <= ra[j] * ce[ni];
           }
           if (lane < 4)
             *(uint64_t*)(smem + (wm * C::WTM + mi * 16 + 4 * lane + j) * (C::BN / 8) + wn * (C::WTN / 8)) = rb;
           __builtin_amdgcn_sched_barrier(0);  // (one row quad at a time: the ballots' SGPR pairs stay few)
         }
+      }
+      if (__ballot(anyb)) {  // (rare) append this wave's band elements (unrolled: acc stays in registers)
+#pragma unroll
+        for (int mi = 0; mi < C::FM; ++mi)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = tl.m0 + wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
+            const float raj = brn[r - tl.m0];
+#pragma unroll
+            for (int ni = 0; ni < C::FN; ++ni) {
+              const float l = acc[mi][ni][j] + bnv[ni];
+              if (fabsf(l - kMaskLogitThreshold) <= raj * ce[ni] && r < g.M)
+                band_push(o.band, r, tl.n0 + wn * C::WTN + ni * 16 + (lane & 15));
+            }
+          }
+      }
       __syncthreads();
       constexpr int BPR = C::BN / 8;
       const int rows = min(C::BM, g.M - tl.m0);
@@ -1461,24 +1300,50 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
   constexpr int PI = C::BN + 16;  // u8 image pitch
   uint8_t* img = (uint8_t*)smem;  // [BM][PI] (mainloop staging is free after its last barrier)
   const bool half = o.thr == 0.5f;
+  bool anyb = false;
+  float bnv[C::FN], ce[C::FN];
 #pragma unroll
   for (int ni = 0; ni < C::FN; ++ni) {
     const int nl = wn * C::WTN + ni * 16 + (lane & 15);
     const int n = tl.n0 + nl;
-    const float bn = n < g.N ? bias[n] : 0.f;
+    bnv[ni] = n < g.N ? bias[n] : 0.f;
+    ce[ni] = (bchk && n < g.N) ? o.band.coef * brn[C::BM + nl] : -1.f;  // (pad genes: never in the band)
+  }
 #pragma unroll
-    for (int mi = 0; mi < C::FM; ++mi)
+  for (int mi = 0; mi < C::FM; ++mi) {
+    const float4 ra4 = bchk ? *(const float4*)(brn + wm * C::WTM + mi * 16 + 4 * (lane >> 4))
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float ra[4] = {ra4.x, ra4.y, ra4.z, ra4.w};
+#pragma unroll
+    for (int ni = 0; ni < C::FN; ++ni) {
+      const int nl = wn * C::WTN + ni * 16 + (lane & 15);
+      const int n = tl.n0 + nl;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int ml = wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
         const int m = tl.m0 + ml;
-        const float l = acc[mi][ni][j] + bn;
+        const float l = acc[mi][ni][j] + bnv[ni];
         float p = 0.f;
         if (o.probs || !half) p = 1.0f / (1.0f + expf(-l));
         const bool pred = n < g.N && (half ? l > kMaskLogitThreshold : p > o.thr);
         img[ml * PI + nl] = pred ? 1 : 0;
         if (o.probs && m < g.M && n < g.N) o.probs[(int64_t)m * o.ldpr + n] = p;
+        anyb |= fabsf(l - kMaskLogitThreshold) <= ra[j] * ce[ni];
       }
+    }
+  }
+  if (bchk && __ballot(anyb)) {  // (rare) append this wave's band elements (unrolled: acc stays in registers)
+#pragma unroll
+    for (int mi = 0; mi < C::FM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < C::FN; ++ni)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ml = wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
+          const float l = acc[mi][ni][j] + bnv[ni];
+          if (fabsf(l - kMaskLogitThreshold) <= brn[ml] * ce[ni] && tl.m0 + ml < g.M)
+            band_push(o.band, tl.m0 + ml, tl.n0 + wn * C::WTN + ni * 16 + (lane & 15));
+        }
   }
   __syncthreads();
   const int rows = min(C::BM, g.M - tl.m0);
@@ -1650,18 +1515,7 @@ static bool pp_enabled() { return opts().gemm_pp != 0; }
 // call f(Cfg{}) with the 128x128 fp32-store tile configuration the options select
 template <class F>
 static auto small_cfg(F&& f) {
-  const bool w8 = opts().small_waves == 8;
-  if (opts().small_stages == 5) return w8 ? f(SmallDeep85{}) : f(SmallDeep5{});
-  return w8 ? f(SmallDeep8{}) : f(SmallDeep{});
-}
-
-// the half-width tiles where they apply (both operands K-major, bf16), else small_cfg
-template <typename T, class F>
-static auto small_cfg_for(const GemmArgs<T>& g, F&& f) {
-  if constexpr (sizeof(T) == 2) {
-    if (opts().small_tile == 64 && g.pk && g.qk && g.Np % 64 == 0) return f(SmallHalf{});
-  }
-  return small_cfg(f);
+  return opts().small_waves == 8 ? f(SmallDeep8{}) : f(SmallDeep{});
 }
 
 // GM2_OPT_GRID_CAP bits: 1 = the output-layer weight-gradient GEMM (side stream, beside the
@@ -1703,19 +1557,15 @@ template <class C, typename T, bool AK, bool BK, bool PP, int IDX = 0>
 static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
                            const float* bias, const StoreEpi& bn, hipStream_t s) {
   // (zero-copy rows: the index table after the staging ring -- a tile's rows, or a split's k-rows)
-  // (IDX 3: the (alpha, beta') table of the split's K columns, 8 bytes each)
-  constexpr int table_max = IDX == 1 ? C::BM * 4 : IDX == 2 ? kMaxIdxRows * 4 : IDX == 3 ? 160 * 1024 - C::LDS : 0;
+  constexpr int table_max = IDX == 1 ? C::BM * 4 : IDX == 2 ? kMaxIdxRows * 4 : 0;
   static_assert(C::LDS + table_max <= 160 * 1024, "LDS budget");
-  const int lds = C::LDS + (IDX == 1 ? C::BM * 4 : IDX == 2 ? a.k_per_split * 4 : IDX == 3 ? a.k_per_split * 8 : 0);
+  const int lds = C::LDS + (IDX == 1 ? C::BM * 4 : IDX == 2 ? a.k_per_split * 4 : 0);
   if (lds > 160 * 1024) throw Gm2Error("gemm: %d bytes of LDS", lds);
   if (IDX == 2 && a.k_per_split > kMaxIdxRows) throw Gm2Error("zero-copy rows: %d k-rows per split", a.k_per_split);
   ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP, IDX>, C::LDS + table_max);
   int grid = tiles;
   StoreEpi ep = bn;
-  if (bn.tail_S > 1) {  // split tail: one workgroup per item (plan_tail)
-    grid = bn.tail_R + bn.tail_rem * bn.tail_S;
-    ep.ntiles = 0;
-  } else if (bn.ntiles) {  // capped grid: the same number of rounds on fewer CUs
+  if (bn.ntiles) {  // capped grid: the same number of rounds on fewer CUs
     const int cus = device_cus(), rounds = (tiles + cus - 1) / cus;
     grid = (tiles + rounds - 1) / rounds;
     ep.ntiles = grid < tiles ? tiles : 0;
@@ -1754,7 +1604,6 @@ static int store_impl(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
   a.k_per_split = (int)(round_up(nkt, splits) / splits) * kt;
   splits = (int)((g.K + a.k_per_split - 1) / a.k_per_split);
   const int tiles = (g.Mp / C::BM) * (g.Np / C::BN) * splits;
-  if (C::BN == 64 && !(g.pk && g.qk)) throw Gm2Error("gemm: 128x64 tiles need K-major operands");
   TimedLaunch tl(kKcGemmStore, s);
   if (g.pk && g.qk) store_launch<C, T, true, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
   else if (g.pk && !g.qk) store_launch<C, T, true, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
@@ -1776,7 +1625,7 @@ int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
     }
   }
   check_gemm(g, 128);
-  return small_cfg_for(g, [&](auto cfg) { return store_impl<decltype(cfg), T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s); });
+  return small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s); });
 }
 
 template <typename T>
@@ -1784,28 +1633,8 @@ int gemm_tiles(const GemmArgs<T>& g) {
   return use_big(g) ? (g.Mp / Big::BM) * (g.Np / Big::BN) : (g.Mp / SmallDeep::BM) * (g.Np / SmallDeep::BN);
 }
 
-// Split-tail plan of a one-pass 256-tile launch over `tiles` tiles (StoreEpi::tail_*): R whole
-// rounds of c = min(CUs, kTailItems) tiles, then the rem left-over tiles in S parts each (S <= CUs / rem, <= 4, >= 8 K-tiles per part); false when the last round is full or the
-// parts would be too small
-static bool plan_tail(int tiles, int K, float* part, int* cnt, StoreEpi& ep) {
-  if (!part || !cnt) return false;
-  const int cus = std::min(device_cus(), kTailItems), nk = K / 64;
-  const int R = tiles / cus, rem = tiles - R * cus;
-  if (R == 0 || rem == 0) return false;
-  const int S = std::min({cus / rem, 4, nk / 8});
-  if (S < 2) return false;
-  ep.tail_R = R * cus;
-  ep.tail_cus = cus;
-  ep.tail_rem = rem;
-  ep.tail_S = S;
-  ep.tail_part = part;
-  ep.tail_cnt = cnt;
-  return true;
-}
-
 template <typename T>
-bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s, bool force_big,
-                    float* tail_part, int* tail_cnt) {
+bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s, bool force_big) {
   // force_big: a one-pass 256x256-tile launch even where the plan would pick 128 tiles (a row
   // slice of a big-tile GEMM, same per-element results as the whole)
   const bool big = force_big ? (sizeof(T) == 2 && g.Mp % 256 == 0 && g.Np % 256 == 0) : use_big(g);
@@ -1817,8 +1646,6 @@ bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hip
   if constexpr (sizeof(T) == 2) {
     if (big) {
       check_gemm(g, 256);
-      if (!force_big && (opts().tail_split & 2) && pp_enabled())
-        plan_tail((g.Mp / 256) * (g.Np / 256), g.K, tail_part, tail_cnt, ep);
       store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
       return true;
     }
@@ -1829,8 +1656,7 @@ bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hip
 }
 
 template <typename T>
-bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, double* sq, float* tail_part,
-                       int* tail_cnt) {
+bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, double* sq) {
   if (plan_gemm(g).splits != 1) return false;
   StoreEpi ep;
   ep.trans = 1;
@@ -1839,8 +1665,6 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
   if constexpr (sizeof(T) == 2) {
     if (use_big(g)) {
       check_gemm(g, 256);
-      if ((opts().tail_split & 1) && pp_enabled())
-        plan_tail((g.Mp / 256) * (g.Np / 256), g.K, tail_part, tail_cnt, ep);
       store_impl<Big, T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s);
       return true;
     }
@@ -1854,17 +1678,6 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
 // plan is one pass of 128-row tiles (the statistics chunk), else the caller runs the separate pass
 
 
-// whether linear_pre_bn can take its A operand as BatchNorm(Y) on load (GM2_OPT_BN_FUSE): bf16, the
-// one-pass 128-tile plan with the statistics epilogue, both operands K-major, and the coefficient
-// table beside the staging ring
-template <typename T>
-bool bn_fuse_ok(const GemmArgs<T>& g) {
-  if (sizeof(T) != 2 || !opts().bn_fuse || !opts().bn_epilogue || !g.pk || !g.qk) return false;
-  const GemmPlan p = plan_gemm(g);
-  if (p.tile != 128 || p.splits != 1 || g.N % 4) return false;
-  return small_cfg([&](auto cfg) { return decltype(cfg)::LDS + g.K * 8 <= 160 * 1024; });
-}
-
 template <typename T>
 bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const StoreEpi& bn, hipStream_t s) {
   static_assert(Small::BM == kBnRowChunk, "statistics chunk = row tile");
@@ -1872,23 +1685,7 @@ bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bi
   const GemmPlan p = plan_gemm(g);
   if (p.tile != 128 || p.splits != 1 || (bn.mode && (g.N % 4 || bn.ldy % 4))) return false;
   check_gemm(g, 128);
-  if (bn.aY) {  // the A operand formed from the previous layer's Y (bn_fuse_ok checked the shape)
-    if constexpr (sizeof(T) == 2) {
-      small_cfg([&](auto cfg) {
-        using Cf = decltype(cfg);
-        GemmArgs<T> a = g;
-        a.k_per_split = g.K;
-        TimedLaunch tl(kKcGemmStore, s);
-        store_launch_k<Cf, T, true, true, false, 3>(a, (g.Mp / Cf::BM) * (g.Np / Cf::BN), C, nullptr, 0, ldc, 0, bias,
-                                                    bn, s);
-        GM2_CHECK_LAUNCH();
-        return 0;
-      });
-      return true;
-    }
-    throw Gm2Error("BatchNorm-fused A operand: bf16 only");
-  }
-  small_cfg_for(g, [&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s); });
+  small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s); });
   return true;
 }
 
@@ -1984,24 +1781,29 @@ bool gemm_idx_ok(const GemmArgs<T>& g) {
 template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs, int64_t ldpr,
                       hipStream_t s, uint8_t* bits, int64_t ldb, int* counts, const uint32_t* xbits, int64_t ldxb,
-                      float thr, bool big, MaskGate gate) {
+                      float thr, bool big, MaskGate gate, MaskBand band) {
   check_gemm(g, big ? 256 : 128);
   // (the 256-column tiles may reach past the row pitch: their bits stores stop at ldb, past G)
   if (bits && ((ldb & 15) || (((uintptr_t)bits) & 15) || ldb * 8 < (big ? g.N : g.Np)))
     throw Gm2Error("mask bits: row pitch %lld must be a multiple of 16 bytes covering the padded genes", (long long)ldb);
   if (counts && (!xbits || ldxb * 32 < g.Np)) throw Gm2Error("mask counts: target bits required");
-  MaskOut o{mask, ldm, bits, ldb, probs, ldpr, counts, xbits, ldxb, thr, gate};
+  MaskOut o{mask, ldm, bits, ldb, probs, ldpr, counts, xbits, ldxb, thr, gate, band};
+  if (band.rn && (!band.cn || !band.count || !band.list || thr != 0.5f))
+    throw Gm2Error("mask band: norms, counter and list required (threshold 0.5 only)");
+  const int band_lds = band.rn ? (big ? 512 : 256) * 4 : 0;  // (row + column norms past the staging ring)
   TimedLaunch tl(kKcMask, s);
   if constexpr (sizeof(T) == 2) {
     if (big) {
       if (g.Mp % 256 || g.Np % 256 || g.K % 64) throw Gm2Error("mask (256x256): padded extents");
-      constexpr int lds = std::max<int>(Big::LDS, 256 * (256 + 16));
+      static_assert(Big::LDS >= 256 * (256 + 16), "u8 image inside the staging ring");
+      constexpr int lds_max = Big::LDS + 512 * 4;
+      const int lds = Big::LDS + band_lds;
       const dim3 grid((g.Mp / 256) * (g.Np / 256));
       if (bits && !mask && !probs && !counts && thr == 0.5f) {  // packed bits only: ballot epilogue
-        ensure_lds_attr((const void*)k_gemm_mask<Big, T, true, true>, lds);
+        ensure_lds_attr((const void*)k_gemm_mask<Big, T, true, true>, lds_max);
         hipLaunchKernelGGL((k_gemm_mask<Big, T, true, true>), grid, dim3(Big::NT), lds, s, g, bias, o);
       } else {
-        ensure_lds_attr((const void*)k_gemm_mask<Big, T, true>, lds);
+        ensure_lds_attr((const void*)k_gemm_mask<Big, T, true>, lds_max);
         hipLaunchKernelGGL((k_gemm_mask<Big, T, true>), grid, dim3(Big::NT), lds, s, g, bias, o);
       }
       GM2_CHECK_LAUNCH();
@@ -2009,17 +1811,18 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
     }
   }
   if (big) throw Gm2Error("mask (256x256): bf16 only");
-  hipLaunchKernelGGL((k_gemm_mask<Small, T>), dim3((g.Mp / 128) * (g.Np / 128)), dim3(Small::NT), Small::LDS, s, g,
-                     bias, o);
+  static_assert(Small::LDS >= 128 * (128 + 16), "u8 image inside the staging ring");
+  if (band_lds) ensure_lds_attr((const void*)k_gemm_mask<Small, T>, Small::LDS + 256 * 4);
+  hipLaunchKernelGGL((k_gemm_mask<Small, T>), dim3((g.Mp / 128) * (g.Np / 128)), dim3(Small::NT), Small::LDS + band_lds,
+                     s, g, bias, o);
   GM2_CHECK_LAUNCH();
 }
 
 #define GM2_INST(T)                                                                                              \
-  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t, double*, float*, int*);       \
-  template bool launch_gemm_sq<T>(const GemmArgs<T>&, float*, int64_t, double*, hipStream_t, bool, float*, int*);              \
+  template bool launch_gemm_trans<T>(const GemmArgs<T>&, float*, int64_t, hipStream_t, double*);                    \
+  template bool launch_gemm_sq<T>(const GemmArgs<T>&, float*, int64_t, double*, hipStream_t, bool);                \
   template int gemm_tiles<T>(const GemmArgs<T>&);                        \
   template bool launch_gemm_bn<T>(const GemmArgs<T>&, float*, int64_t, const float*, const StoreEpi&, hipStream_t);   \
-  template bool bn_fuse_ok<T>(const GemmArgs<T>&);                                                              \
   template int launch_gemm_store<T>(const GemmArgs<T>&, int, float*, float*, int, int64_t, int64_t, const float*, \
                                     hipStream_t);                                                                \
   template int gemm_recon_grid_blocks<T>(const GemmArgs<T>&);                                                   \
@@ -2034,10 +1837,10 @@ GM2_INST(bf16_t)
 #undef GM2_INST
 template void launch_gemm_mask<float>(const GemmArgs<float>&, const float*, uint8_t*, int64_t, float*, int64_t,
                                       hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float, bool,
-                                      MaskGate);
+                                      MaskGate, MaskBand);
 template void launch_gemm_mask<bf16_t>(const GemmArgs<bf16_t>&, const float*, uint8_t*, int64_t, float*, int64_t,
                                        hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float, bool,
-                                       MaskGate);
+                                       MaskGate, MaskBand);
 
 #ifdef GM2_DEBUG
 GM2_DBG_TAKE_FN(dbg_take_gemm)

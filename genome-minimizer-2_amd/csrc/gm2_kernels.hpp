@@ -74,7 +74,7 @@ struct GemmArgs {
   int64_t idx_lim = 0;
 };
 
-// ---- tuning options (gm2.h GM2_OPT_*): results are bit-identical under every value but tail_split ----
+// ---- tuning options (gm2.h GM2_OPT_*): results are bit-identical under every value ----
 // Each workspace carries its own copy (gm2_workspace_set_option); gm2_set_option edits the process
 // defaults that new workspaces and workspace-less calls (gm2_gemm) start from. The launchers read
 // the options of the call in progress through opts(), which an OptionScope sets per C-ABI call.
@@ -85,20 +85,13 @@ struct Options {
   int small_split = 1;   // GM2_OPT_SMALL_SPLIT  split-K of the chip-filling short-K 128-tile GEMMs
   int bn_epilogue = 1;   // GM2_OPT_BN_EPILOGUE  BatchNorm statistics in the GEMM store epilogue
   int small_waves = 8;   // GM2_OPT_SMALL_WAVES  waves of the 128x128 fp32-store tiles (4 or 8)
-  int small_stages = 4;  // GM2_OPT_SMALL_STAGES LDS ring depth of those tiles (4 or 5)
   int grid_cap = 2;      // GM2_OPT_GRID_CAP     capped grids: 1 dW9, 2 dWe0, 4 recon
   int input_chunks = 1;  // GM2_OPT_INPUT_CHUNKS launches of the input-layer weight gradient (1 or 4)
   int sync_bn = 0;       // GM2_OPT_SYNC_BN      train-mode BatchNorm over every rank's rows (collective)
   int defer_adam = 0;    // GM2_OPT_DEFER_OUTPUT_ADAM  output-layer Adam update beside the next step's hidden
                          //   layers on this many workgroups per CU (0 = not deferred)
-  int side_priority = 0; // GM2_OPT_SIDE_PRIORITY  side stream priority: -1 high, 0 normal, 1 low
-  int dw9_last = 0;      // GM2_OPT_DW9_LAST  output-layer weight gradient forked beside dWe0, not first
-  int tail_split = 0;    // GM2_OPT_TAIL_SPLIT  split tails of the one-pass weight-gradient GEMMs: 1 dW9, 2 dWe0
   int grad_buckets = 1;  // GM2_OPT_GRAD_BUCKETS  record the gradient-bucket events (gm2_wait_grad_bucket)
-  int side_cus = 0;      // GM2_OPT_SIDE_CUS  CU mask of the side stream: this many CUs (0 = all)
-  int small_tile = 128;  // GM2_OPT_SMALL_TILE  N width of the forward's hidden-layer tiles (128 or 64)
   int sample_split = 1;  // GM2_OPT_SAMPLE_SPLIT  bf16x3 output layer of the sampling decode (bound permitting)
-  int bn_fuse = 0;       // GM2_OPT_BN_FUSE  forward hidden GEMMs form their A operand as BatchNorm+ReLU of Y on load
 };
 // validated edit of one option (throws on an unknown key or a bad value)
 void option_set(Options& o, int key, int value);
@@ -150,46 +143,18 @@ struct StoreEpi {
   // (grid = ceil(tiles / rounds) for the same number of rounds: the idle CUs of the last round
   // become free CUs for the other stream's work for the whole launch)
   int ntiles = 0;
-  // split tail (tail_S > 1; one K pass, 256x256 tiles): one workgroup per item -- the first tail_R
-  // tiles whole (whole dispatch rounds of tail_cus workgroups), then the last tail_rem tiles in
-  // tail_S K-parts each. The parts meet through tail_part (each part's fp32 accumulators,
-  // [tile][part][BM * BN]) and tail_cnt[tile] (arrival counters, zero between launches: the last
-  // part to arrive resets its tile's); the last to arrive sums the parts in part order and runs
-  // the epilogue.
-  int tail_R = 0, tail_cus = 0, tail_rem = 0, tail_S = 1;
-  float* tail_part = nullptr;
-  int* tail_cnt = nullptr;
-  // A operand formed on load (GM2_OPT_BN_FUSE, launch_gemm_bn): A = relu(BatchNorm(aY)) in bf16 from
-  // the previous layer's pre-BN output aY [rows][ldaY] fp32 and its saved (mean, invstd) aSave
-  // [2][aH], gamma, beta; rows >= aRows are 0. The bf16 A is also stored to aOut [rows][ldaOut]
-  const float* aY = nullptr;
-  int64_t ldaY = 0;
-  const float *aSave = nullptr, *aGamma = nullptr, *aBeta = nullptr;
-  int aH = 0, aRows = 0;
-  bf16_t* aOut = nullptr;
-  int64_t ldaOut = 0;
 };
-// split-tail scratch of one GEMM: at most kTailItems tile parts of 256 x 256 fp32 + counters
-constexpr int kTailItems = 256;
-constexpr int64_t kTailPartBytes = (int64_t)kTailItems * 256 * 256 * 4;
-constexpr int64_t kTailCntBytes = kTailItems * 4;
 // GEMM + BatchNorm statistics of its output in one launch when the plan allows (one K pass of
 // 128-row tiles); returns false (nothing launched) otherwise
 template <typename T>
 bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bias, const StoreEpi& bn, hipStream_t s);
-template <typename T>
-bool bn_fuse_ok(const GemmArgs<T>& g);
 // C^T = (P . Q^T)^T into C [N][ldc] in one launch when the plan is one K pass; false otherwise
-// (tail_part / tail_cnt: split-tail scratch, kTailPartBytes / kTailCntBytes, used when the option
-// GM2_OPT_TAIL_SPLIT selects this GEMM and the tile count leaves a short last round)
 template <typename T>
-bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, double* sq = nullptr,
-                       float* tail_part = nullptr, int* tail_cnt = nullptr);
+bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t s, double* sq = nullptr);
 // C = P . Q^T in one K pass with the per-tile sum of squares of C into sq (see StoreEpi::sq);
 // false (nothing launched) when the plan splits K
 template <typename T>
-bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s, bool force_big = false,
-                    float* tail_part = nullptr, int* tail_cnt = nullptr);
+bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hipStream_t s, bool force_big = false);
 // tiles of a one-pass launch of g (the sq entries it writes)
 template <typename T>
 int gemm_tiles(const GemmArgs<T>& g);
@@ -220,33 +185,53 @@ constexpr int kMaxIdxRows = 8192;
 template <typename T>
 bool gemm_idx_ok(const GemmArgs<T>& g);
 // The bf16x3 sampling decode's error bound (api.hip decode_split3): per logit at most
-// kSplitUnit * sqrt(max_r ||a_r||^2) * sqrt(max_g ||w_g||^2) * 1.01; the split output layer runs
-// only while that is <= kSplitBound
+// kSplitUnit * ||a_r||_2 * ||w_g||_2 * 1.01 (Cauchy-Schwarz over the split's per-product error). The
+// gate is per 256 x 256 tile: a tile runs split when kSplitUnit * max_r ||a_r|| * max_g ||w_g|| * 1.01
+// over its 256 genome rows and 256 genes (the split kernels' block maxima) is <= kSplitBound, else
+// the exact-fp32 kernel computes it.
 constexpr double kSplitBound = 2.5e-4;
 constexpr double kSplitUnit = 4.62e-5;  // 3.02 x 2^-16, rounded up
-// each squared-norm maximum is kept in kSplitShards words (one atomic max per split workgroup into
-// shard blockIdx % kSplitShards); the maximum is the max over the shards
-constexpr int kSplitShards = 32;
-// Device-side choice between the split and the exact output layer (both launched, one runs): the
-// kernel reads the two squared-norm maxima (float bits, kSplitShards shards each: activations then
-// weights) and runs when its `run` matches the bound's verdict (1: split taken, 2: exact taken),
-// counting itself in *count (once per launch)
+constexpr int kSplitShards = 32;        // tile counters, sharded by blockIdx % kSplitShards
+// Device-side choice between the split and the exact output layer, per tile (both kernels launched
+// over their full grids; a tile's workgroup runs only when the gate's verdict for its 256 x 256
+// block is its `run`: 1 split, 2 exact), counting the tiles it ran into tiles[blockIdx % 32]
 struct MaskGate {
-  const unsigned* maxima = nullptr;
+  const unsigned* ablk = nullptr;  // per 256-genome-row block: max ||a_r|| (fp32 bits)
+  const unsigned* wblk = nullptr;  // per 256-gene block: max ||w_g|| (fp32 bits)
   int run = 0;
-  unsigned* count = nullptr;
+  unsigned* tiles = nullptr;
 };
-__device__ __forceinline__ bool split_bound_ok(const unsigned* maxima) {
-  unsigned am = 0u, wm = 0u;  // (non-negative floats order as unsigned)
-#pragma unroll
-  for (int i = 0; i < kSplitShards; ++i) {
-    am = max(am, maxima[i]);
-    wm = max(wm, maxima[kSplitShards + i]);
-  }
-  const double a2 = (double)__uint_as_float(am), w2 = (double)__uint_as_float(wm);
-  const double bound = kSplitUnit * sqrt(a2) * sqrt(w2) * 1.01;
-  return bound <= kSplitBound;  // (NaN / inf: false, the exact path)
+__device__ __forceinline__ bool split_tile_ok(const MaskGate& g, int m0, int n0) {
+  const double a = (double)__uint_as_float(g.ablk[m0 >> 8]), w = (double)__uint_as_float(g.wblk[n0 >> 8]);
+  return kSplitUnit * a * w * 1.01 <= kSplitBound;  // (NaN / inf: false, the exact path)
 }
+// The certified band of the sampling decode (SURVEY.md 7 "Hard parts" (ii)): logits with
+// |l - T| <= coef * ||a_r|| * ||w_g|| (T = the mask threshold) may sit on either side of T in the
+// reference's own fp32 arithmetic; the mask epilogues append those (row, gene) pairs to `list`
+// (count = entries found, capacity cap: the rest only counted), and k_band_fix recomputes each one's
+// logit in fp64 from the same fp32 activations / weights and sets its mask bit from that.
+//   coef (split tiles) = kSplitUnit * 1.01 + gamma_3H + gamma_H: the split's own error, its fp32
+//     accumulation of 3H products and the reference's fp32 accumulation of H products
+//   coef (exact tiles) = 2 gamma_H (gamma_n = n u / (1 - n u), u = 2^-24)
+struct MaskBand {
+  const float* rn = nullptr;  // ||a_r|| per genome row (nullptr: no band check)
+  const float* cn = nullptr;  // ||w_g|| per gene
+  float coef = 0.f;
+  unsigned* count = nullptr;
+  uint2* list = nullptr;      // (row, gene)
+  unsigned cap = 0;
+};
+inline double band_gamma(double n) { return n * 0x1p-24 / (1.0 - n * 0x1p-24); }
+constexpr unsigned kBandCap = 1u << 22;  // band list entries per decode call (32 MB)
+// k_band_fix over list[0 .. min(count, cap)): fp64 logit of (A[row], W[gene]) + bias, mask bit =
+// (float)logit > T (the correctly rounded fp32 logit against the reference's threshold); packed
+// bits (bits != nullptr) or u8 mask. ctl: the decode's per-call counters (api.hip DecodeCtl)
+void launch_band_fix(const uint2* list, const unsigned* count, unsigned cap, const float* A, int64_t lda,
+                     const float* W, int64_t ldw, const float* bias, int H, uint8_t* bits, int64_t ldb, uint8_t* mask,
+                     int64_t ldm, unsigned* flips, hipStream_t s);
+// one workgroup: the decode call's per-call counters -> the workspace's cumulative ones (DecodeCtl)
+void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* count,
+                         const unsigned* flips, unsigned cap, unsigned long long* cum, hipStream_t s);
 
 // output layer + threshold (sampling / metrics): u8 mask, packed bits, probs, per-row (TP, FP, FN).
 // big (bf16 only): the bf16x3 split decode -- 256x256 ping-pong tiles over operands in
@@ -255,7 +240,7 @@ template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs,
                       int64_t ldpr, hipStream_t s, uint8_t* bits = nullptr, int64_t ldb = 0, int* counts = nullptr,
                       const uint32_t* xbits = nullptr, int64_t ldxb = 0, float thr = 0.5f, bool big = false,
-                      MaskGate gate = {});
+                      MaskGate gate = {}, MaskBand band = {});
 
 // ---- kernels.hip ----
 constexpr int kBnRowChunk = 128;  // rows per BatchNorm partial-statistics chunk
@@ -280,19 +265,16 @@ void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float
                            const float* gamma, const float* beta, int B, int H, float* part, float* dsum,
                            hipStream_t s);
 // bf16x3 split of fp32 rows (the sampling decode's output layer): out [rows_pad][2K], each 64-column
-// K-tile c = (hi | lo) of columns [32c, 32c + 32) (K % 32 == 0); rows >= rows zero; atomic maxima
-// of the row sums of squares (fp32 bits) into smax[0 .. kSplitShards)
-void launch_split3(const float* X, int64_t ldx, int rows, int rows_pad, int K, bf16_t* out, int64_t ldo, unsigned* smax,
-                   hipStream_t s);
+// K-tile c = (hi | lo) of columns [32c, 32c + 32) (K % 32 == 0); rows >= rows zero; rn[r] = the row's
+// 2-norm (rounded up; 0 for pad rows), blk[r / 256] = max of rn over each 256-row block (fp32 bits,
+// atomic max: zero it first). rows_pad % 256 == 0.
+void launch_split3(const float* X, int64_t ldx, int rows, int rows_pad, int K, bf16_t* out, int64_t ldo, float* rn,
+                   unsigned* blk, hipStream_t s);
 // dst[c][r] = src[r][c] for an R x Cn block (multiples of 64)
 template <typename T>
 void launch_transpose(const T* src, int64_t lds_, int R, int Cn, T* dst, int64_t ldd, hipStream_t s);
 // BatchNorm finalize (chunk merge per column) + elementwise apply in one launch per layer
 // (sync != nullptr: SyncBN, the global batch's all-reduced sums from launch_bn_sync_pack)
-// train-mode BatchNorm statistics of the chunk partials -> save (mean, invstd) and the running
-// statistics, without the apply pass (its consumer forms A on load: GM2_OPT_BN_FUSE)
-void launch_bn_fwd_finalize(const float* part, int B, int H, const float* gamma, const float* beta, float* rmean,
-                            float* rvar, float* save, hipStream_t s);
 template <typename T>
 void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
                          const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,

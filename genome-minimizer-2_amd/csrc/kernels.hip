@@ -847,17 +847,6 @@ __device__ __forceinline__ float2 bn_fwd_coef(const float2* __restrict__ part, i
   return make_float2(alpha, fmaf(-meanf, alpha, beta[col]));
 }
 
-// train-mode statistics of column blockIdx.x * 256 + threadIdx.x from the chunk partials: save and
-// running statistics exactly as k_bn_fwd_apply's row-block-0 threads write them (its consumer, a
-// GEMM with the BatchNorm-fused A operand, reads save / gamma / beta)
-__global__ __launch_bounds__(256) void k_bn_fwd_finalize(const float2* __restrict__ part, int B, int H,
-                                                         const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, float* rmean, float* rvar,
-                                                         float* save) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col < H) (void)bn_fwd_coef(part, B, H, 1, gamma, beta, rmean, rvar, save, col, true, nullptr);
-}
-
 // A = relu(y*alpha + beta') for rows < B, 0 for rows in [B, Bp). Grid: (ceil(H/256), Bp/64).
 template <typename T>
 __global__ __launch_bounds__(256) void k_bn_fwd_apply(const float* __restrict__ Y, int64_t ld,
@@ -1061,51 +1050,124 @@ __global__ __launch_bounds__(256) void k_bn_sync_running(const double* __restric
 // activations and output weights both take this layout, and the GEMM's main loop (mainloop_pp, S3)
 // multiplies each K-tile's halves as hi.hi + hi.lo + lo.hi -- the fp32 product up to 3.02 x 2^-16
 // |x| |w| per term -- from 2K columns of operand bytes instead of the 3K of a (hi|hi|lo).(hi|lo|hi)
-// concatenation. Rows in [rows, rows_pad) are zero. The largest row sum of squares (fp32 bits:
-// non-negative floats order as unsigned) goes to smax[0 .. kSplitShards) by atomic maxima, one per
-// workgroup into shard blockIdx % kSplitShards (the error bound, ||a||_2 ||w||_2, reads the max of
-// the shards): with one atomic per row into a single word the launches ran at the word's atomic rate
-// (65,536 rows: 750 us for 0.34 GB). One wave per row at a time (grid-stride), 8 columns per lane
-// per pass.
+// concatenation. Rows in [rows, rows_pad) are zero. Per row r it also writes rn[r] = ||x_r||_2 (0 for
+// pad rows) -- the per-element error bounds of the decode's band check (MaskOut::rn / cn) -- and the
+// block maximum of those norms over each 256-row block b into blk[b] (fp32 bits, non-negative floats
+// order as unsigned) by one atomic max per workgroup: the per-tile gate (MaskGate) of the split output
+// layer. Each workgroup takes 16 consecutive rows (one wave 4), so it touches one block word only.
+// (The first form kept ONE global maximum with one atomic per row into a single word: the launches ran
+// at that word's atomic rate, 65,536 rows in 750 us.)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_split3(const float* __restrict__ X, int64_t ldx, int rows, int rows_pad, int K,
-                                              bf16_t* __restrict__ out, int64_t ldo, unsigned* __restrict__ smax) {
+__global__ __launch_bounds__(256) void k_split3(const float* __restrict__ X, int64_t ldx, int rows, int K,
+                                              bf16_t* __restrict__ out, int64_t ldo, float* __restrict__ rn,
+                                              unsigned* __restrict__ blk) {
   __shared__ float wmax[4];
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float mx = 0.f;
-  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < rows_pad; r += gridDim.x * 4) {
-  float ss = 0.f;
-  for (int k0 = lane * 8; k0 < K; k0 += 512) {
-    float x[8];
-    if (r < rows) {
-      const float4 a = *(const float4*)(X + (int64_t)r * ldx + k0), b = *(const float4*)(X + (int64_t)r * ldx + k0 + 4);
-      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
-    } else {
+#pragma unroll 1
+  for (int q = 0; q < 4; ++q) {
+    const int r = blockIdx.x * 16 + wv * 4 + q;
+    float ss = 0.f;
+    for (int k0 = lane * 8; k0 < K; k0 += 512) {
+      float x[8];
+      if (r < rows) {
+        const float4 a = *(const float4*)(X + (int64_t)r * ldx + k0), b = *(const float4*)(X + (int64_t)r * ldx + k0 + 4);
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+      } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = 0.f;
-    }
-    uint32_t hw[4], lw[4];
+        for (int e = 0; e < 8; ++e) x[e] = 0.f;
+      }
+      uint32_t hw[4], lw[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float h0 = bf2f(f2bf(x[2 * e])), h1 = bf2f(f2bf(x[2 * e + 1]));
-      hw[e] = f2bf2(x[2 * e], x[2 * e + 1]);
-      lw[e] = f2bf2(x[2 * e] - h0, x[2 * e + 1] - h1);
-      ss = fmaf(x[2 * e], x[2 * e], ss);
-      ss = fmaf(x[2 * e + 1], x[2 * e + 1], ss);
+      for (int e = 0; e < 4; ++e) {
+        const float h0 = bf2f(f2bf(x[2 * e])), h1 = bf2f(f2bf(x[2 * e + 1]));
+        hw[e] = f2bf2(x[2 * e], x[2 * e + 1]);
+        lw[e] = f2bf2(x[2 * e] - h0, x[2 * e + 1] - h1);
+        ss = fmaf(x[2 * e], x[2 * e], ss);
+        ss = fmaf(x[2 * e + 1], x[2 * e + 1], ss);
+      }
+      const uint4 hv = make_uint4(hw[0], hw[1], hw[2], hw[3]), lv = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+      bf16_t* o = out + (int64_t)r * ldo + 2 * (k0 & ~31) + (k0 & 31);
+      *(uint4*)(o) = hv;
+      *(uint4*)(o + 32) = lv;
     }
-    const uint4 hv = make_uint4(hw[0], hw[1], hw[2], hw[3]), lv = make_uint4(lw[0], lw[1], lw[2], lw[3]);
-    bf16_t* o = out + (int64_t)r * ldo + 2 * (k0 & ~31) + (k0 & 31);
-    *(uint4*)(o) = hv;
-    *(uint4*)(o + 32) = lv;
+    // (the bound uses the norm rounded up: sqrt of a sum of squares carried in fp32 is within a few
+    // ulps of the true norm; x 1.0001 covers that with room)
+    const float nrm = r < rows ? sqrtf(wave_sum(ss)) * 1.0001f : 0.f;
+    if (lane == 0) rn[r] = nrm;
+    mx = fmaxf(mx, nrm);
   }
-  ss = wave_sum(ss);
-  if (r < rows) mx = fmaxf(mx, ss);
-  }
-  if (lane == 0) wmax[threadIdx.x >> 6] = mx;
+  if (lane == 0) wmax[wv] = mx;
   __syncthreads();
   if (threadIdx.x == 0) {
     const float m = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
-    atomicMax(smax + (blockIdx.x % kSplitShards), __float_as_uint(m));
+    atomicMax(blk + blockIdx.x / 16, __float_as_uint(m));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Certified-band recompute of the sampling decode (MaskBand; SURVEY.md 7 "Hard parts" (ii)): one
+// wave per listed (row, gene): logit = sum_k A[row][k] W[gene][k] in fp64 (each lane a strided
+// slice of k in order, then a fixed-order wave reduction: deterministic) + bias[gene]; the mask bit
+// becomes (float)logit > T, the correctly rounded fp32 logit against the reference's threshold.
+// Packed bits are set / cleared with 32-bit atomics (several waves may share a word), u8 masks by
+// byte stores. flips counts the bits the recompute changed.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_band_fix(const uint2* __restrict__ list, const unsigned* __restrict__ count,
+                                                unsigned cap, const float* __restrict__ A, int64_t lda,
+                                                const float* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
+                                                int H, uint8_t* bits, int64_t ldb, uint8_t* mask, int64_t ldm,
+                                                unsigned* flips) {
+  const unsigned n = min(*count, cap);
+  const int lane = threadIdx.x & 63;
+  for (unsigned e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4) {
+    const uint2 rg = list[e];
+    const float* a = A + (int64_t)rg.x * lda;
+    const float* w = W + (int64_t)rg.y * ldw;
+    double acc = 0.0;
+    for (int k = lane; k < H; k += 64) acc = fma((double)a[k], (double)w[k], acc);
+    acc = wave_sum_d(acc) + (double)bias[rg.y];
+    const bool pred = (float)acc > kMaskLogitThreshold;
+    if (lane == 0) {
+      bool was;
+      if (bits) {
+        unsigned* word = (unsigned*)(bits + (int64_t)rg.x * ldb) + (rg.y >> 5);
+        const unsigned bit = 1u << (rg.y & 31);
+        const unsigned old = pred ? atomicOr(word, bit) : atomicAnd(word, ~bit);
+        was = (old & bit) != 0;
+      } else {
+        uint8_t* p = mask + (int64_t)rg.x * ldm + rg.y;
+        was = *p != 0;
+        *p = pred ? 1 : 0;
+      }
+      if (was != pred) atomicAdd(flips, 1u);
+    }
+  }
+}
+
+// the decode call's counters -> the workspace's cumulative ones: cum[0] split tiles, [1] exact
+// tiles, [2] band elements found, [3] bits the recompute flipped, [4] band elements beyond the
+// list's capacity (left as the kernels decided them), [5] decodes with split tiles, [6] without
+__global__ __launch_bounds__(64) void k_decode_stats(const unsigned* __restrict__ tiles_split,
+                                                     const unsigned* __restrict__ tiles_exact,
+                                                     const unsigned* __restrict__ count,
+                                                     const unsigned* __restrict__ flips, unsigned cap,
+                                                     unsigned long long* cum) {
+  const int t = threadIdx.x;
+  unsigned long long a = t < kSplitShards ? tiles_split[t] : 0ull, b = t < kSplitShards ? tiles_exact[t] : 0ull;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  if (t == 0) {
+    const unsigned c = *count;
+    cum[0] += a;
+    cum[1] += b;
+    cum[2] += c;
+    cum[3] += *flips;
+    cum[4] += c > cap ? c - cap : 0u;
+    cum[a ? 5 : 6] += 1;
   }
 }
 
@@ -1250,14 +1312,6 @@ void launch_colsum(const float* part, int rows, int64_t ld, int64_t n, float* ou
   GM2_CHECK_LAUNCH();
 }
 
-void launch_bn_fwd_finalize(const float* part, int B, int H, const float* gamma, const float* beta, float* rmean,
-                            float* rvar, float* save, hipStream_t s) {
-  if (B <= 0) throw Gm2Error("bn_fwd_finalize: B > 0");
-  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((H + 255) / 256), dim3(256), 0, s, (const float2*)part, B, H, gamma, beta,
-                     rmean, rvar, save);
-  GM2_CHECK_LAUNCH();
-}
-
 template <typename T>
 void launch_bn_fwd_apply(const float* Y, int64_t ld, const float* part, int B, int Bp, int H, int train,
                          const float* gamma, const float* beta, float* rmean, float* rvar, float* save, T* A,
@@ -1289,13 +1343,29 @@ void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const floa
   GM2_CHECK_LAUNCH();
 }
 
-void launch_split3(const float* X, int64_t ldx, int rows, int rows_pad, int K, bf16_t* out, int64_t ldo, unsigned* smax,
-                   hipStream_t s) {
-  if (K % 32 || ldx % 4 || ldo % 8 || ldo < 2 * K || rows > rows_pad || rows_pad % 4 || (((uintptr_t)X) & 15) ||
+void launch_split3(const float* X, int64_t ldx, int rows, int rows_pad, int K, bf16_t* out, int64_t ldo, float* rn,
+                   unsigned* blk, hipStream_t s) {
+  if (K % 32 || ldx % 4 || ldo % 8 || ldo < 2 * K || rows > rows_pad || rows_pad % 256 || (((uintptr_t)X) & 15) ||
       (((uintptr_t)out) & 15))
     throw Gm2Error("split3: K %d, ld %lld / %lld, rows %d / %d", K, (long long)ldx, (long long)ldo, rows, rows_pad);
-  const int grid = std::min(rows_pad / 4, 2048);  // (grid-stride over the rows: 2,048 atomics at most)
-  hipLaunchKernelGGL(k_split3, dim3(grid), dim3(256), 0, s, X, ldx, rows, rows_pad, K, out, ldo, smax);
+  hipLaunchKernelGGL(k_split3, dim3(rows_pad / 16), dim3(256), 0, s, X, ldx, rows, K, out, ldo, rn, blk);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_band_fix(const uint2* list, const unsigned* count, unsigned cap, const float* A, int64_t lda,
+                     const float* W, int64_t ldw, const float* bias, int H, uint8_t* bits, int64_t ldb, uint8_t* mask,
+                     int64_t ldm, unsigned* flips, hipStream_t s) {
+  if ((!bits && !mask) || (bits && (ldb & 3)))
+    throw Gm2Error("band fix: an output (packed bits with 4-B aligned rows, or a u8 mask) is required");
+  // (a fixed grid: the count lives on the device; each wave takes entries e, e + 4 * grid, ...)
+  hipLaunchKernelGGL(k_band_fix, dim3(1024), dim3(256), 0, s, list, count, cap, A, lda, W, ldw, bias, H, bits, ldb,
+                     mask, ldm, flips);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* count,
+                         const unsigned* flips, unsigned cap, unsigned long long* cum, hipStream_t s) {
+  hipLaunchKernelGGL(k_decode_stats, dim3(1), dim3(64), 0, s, tiles_split, tiles_exact, count, flips, cap, cum);
   GM2_CHECK_LAUNCH();
 }
 

@@ -46,10 +46,6 @@ void option_set(Options& o, int key, int value) {
       if (value != 4 && value != 8) throw Gm2Error("small waves %d: 4 or 8", value);
       o.small_waves = value;
       break;
-    case GM2_OPT_SMALL_STAGES:
-      if (value != 4 && value != 5) throw Gm2Error("small stages %d: 4 or 5", value);
-      o.small_stages = value;
-      break;
     case GM2_OPT_GRID_CAP:
       if (value < 0 || value > 7) throw Gm2Error("grid cap bits %d: 0..7", value);
       o.grid_cap = value;
@@ -63,26 +59,8 @@ void option_set(Options& o, int key, int value) {
       if (value < 0 || value > 16) throw Gm2Error("deferred output-layer update: %d workgroups per CU (0..16)", value);
       o.defer_adam = value;
       break;
-    case GM2_OPT_SIDE_PRIORITY:
-      if (value < -1 || value > 1) throw Gm2Error("side priority %d: -1, 0 or 1", value);
-      o.side_priority = value;
-      break;
-    case GM2_OPT_DW9_LAST: o.dw9_last = value ? 1 : 0; break;
-    case GM2_OPT_TAIL_SPLIT:
-      if (value < 0 || value > 3) throw Gm2Error("tail split bits %d: 0..3", value);
-      o.tail_split = value;
-      break;
     case GM2_OPT_GRAD_BUCKETS: o.grad_buckets = value ? 1 : 0; break;
-    case GM2_OPT_SIDE_CUS:
-      if (value < 0 || value > 4096) throw Gm2Error("side CUs %d: 0..4096", value);
-      o.side_cus = value;
-      break;
-    case GM2_OPT_SMALL_TILE:
-      if (value != 64 && value != 128) throw Gm2Error("small tile %d: 64 or 128", value);
-      o.small_tile = value;
-      break;
     case GM2_OPT_SAMPLE_SPLIT: o.sample_split = value ? 1 : 0; break;
-    case GM2_OPT_BN_FUSE: o.bn_fuse = value ? 1 : 0; break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -95,19 +73,12 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_SMALL_SPLIT: return o.small_split;
     case GM2_OPT_BN_EPILOGUE: return o.bn_epilogue;
     case GM2_OPT_SMALL_WAVES: return o.small_waves;
-    case GM2_OPT_SMALL_STAGES: return o.small_stages;
     case GM2_OPT_GRID_CAP: return o.grid_cap;
     case GM2_OPT_INPUT_CHUNKS: return o.input_chunks;
     case GM2_OPT_SYNC_BN: return o.sync_bn;
     case GM2_OPT_DEFER_OUTPUT_ADAM: return o.defer_adam;
-    case GM2_OPT_SIDE_PRIORITY: return o.side_priority;
-    case GM2_OPT_DW9_LAST: return o.dw9_last;
-    case GM2_OPT_TAIL_SPLIT: return o.tail_split;
     case GM2_OPT_GRAD_BUCKETS: return o.grad_buckets;
-    case GM2_OPT_SIDE_CUS: return o.side_cus;
-    case GM2_OPT_SMALL_TILE: return o.small_tile;
     case GM2_OPT_SAMPLE_SPLIT: return o.sample_split;
-    case GM2_OPT_BN_FUSE: return o.bn_fuse;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

@@ -20,13 +20,21 @@ def load_model(input_dim, hidden_dim, latent_dim, path_to_model, precision=nativ
 
 
 def sample_from_model(model, latent_dim, num_samples, device, binary_dtype=np.float64, return_probs=True,
-                      chunk=65536):
+                      chunk=65536, stats=None):
     """z ~ N(0, I) drawn with torch.randn(num_samples, latent_dim, device=device) exactly as the
-    reference, decoded in exact fp32 with eval-mode BatchNorm, thresholded at sigmoid > 0.5.
-    Returns (binary [N,G] as `binary_dtype` (reference: float64), probs fp32 [N,G] or None, z)."""
+    reference, decoded with eval-mode BatchNorm (hidden layers in fp32; with probs requested, the
+    reference's default, the output layer in exact fp32 too, else gated per tile between bf16x3 and
+    fp32 with the certified band recomputed in fp64: gm2.h GM2_OPT_SAMPLE_SPLIT), thresholded at
+    sigmoid > 0.5. Returns (binary [N,G] as `binary_dtype` (reference: float64), probs fp32 [N,G] or
+    None, z). `stats` (a dict, optional) receives this call's decode counters (VAE.decode_stats:
+    tiles per path, band elements recomputed in fp64, bits flipped)."""
     with torch.no_grad():
         z = torch.randn(num_samples, latent_dim, device=device)
+    before = model.decode_stats() if stats is not None else None
     mask, probs = model.decode_mask(z, want_probs=return_probs, chunk=chunk)
+    if stats is not None:
+        after = model.decode_stats()
+        stats.update({k: after[k] - before[k] for k in after})
     binary = mask.cpu().numpy()
     if binary_dtype is not None and binary_dtype != np.uint8:
         binary = binary.astype(binary_dtype)

@@ -171,6 +171,16 @@ class VAE:
         return self
 
     # ------------------------------------------------------------------ native workspaces
+    def _carry_decode_stats(self, ws):
+        """(a larger fp32 workspace replaced the previous one: its counters start at zero, so the
+        previous workspace's totals are kept on the host and added back by decode_stats)"""
+        if getattr(self, "_stats_ws", None) is not ws:
+            old = getattr(self, "_stats_ws", None)
+            if old is not None:
+                base = getattr(self, "_stats_base", {})
+                self._stats_base = {k: base.get(k, 0) + old.stat(v) for k, v in native.DECODE_STATS.items()}
+            self._stats_ws = ws
+
     def workspace(self, prec, batch_max):
         """Workspace for (precision, capacity); reused while large enough."""
         key = prec
@@ -255,6 +265,7 @@ class VAE:
         for s in range(0, N, chunk):
             n = min(chunk, N - s)
             ws = self.workspace(native.GM2_F32, min(chunk, N))
+            self._carry_decode_stats(ws)
             native.decode_mask(ws, self.params, self.bn, z[s:s + n], n, mask[s:], G,
                                None if probs is None else probs[s:], G)
         return mask, probs
@@ -270,9 +281,20 @@ class VAE:
         for s in range(0, N, chunk):
             n = min(chunk, N - s)
             ws = self.workspace(native.GM2_F32, min(chunk, N))
+            self._carry_decode_stats(ws)
             native.decode_bits(ws, self.params, self.bn, z[s:s + n], n, pm.bits[s:], pm.ld,
                                None if probs is None else probs[s:], G)
         return pm, probs
+
+    def decode_stats(self):
+        """The sampling decodes' counters on this model's fp32 (sampling) workspace, cumulative
+        (gm2.h GM2_STAT_*): decodes and output-layer tiles per path (bf16x3 split / exact fp32),
+        logits of the certified band recomputed in fp64, the mask bits that recompute flipped, and
+        band elements beyond a call's list capacity. Zeros before the first decode. Waits for the
+        device."""
+        ws = self._workspaces.get(native.GM2_F32)
+        base = getattr(self, "_stats_base", {})
+        return {k: base.get(k, 0) + (ws.stat(v) if ws is not None else 0) for k, v in native.DECODE_STATS.items()}
 
     def encode(self, x):
         """(mean, logvar) of the eval-mode encoder (model.py:95-98) for a 0/1 matrix x [B, G]

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GM2_ABI_VERSION 4
+#define GM2_ABI_VERSION 5
 #define GM2_NUM_PARAMS 30 /* tensors in model.parameters() */
 #define GM2_NUM_SCALARS 16
 
@@ -175,9 +175,11 @@ int gm2_adam_step(const gm2_dims* d, int precision, float* params, const float* 
 int gm2_eval_forward(const gm2_dims* d, int precision, const gm2_batch* batch, const float* params,
                      const float* bn_running, const float* scalars, double* loss, void* ws, void* stream);
 
-/* Sampling decode (extras.py:192-203, main.py:351-370): z fp32 [n][L] -> eval-mode decoder in exact
- * fp32 -> mask u8 [n][ld_mask] = (sigmoid(logit) > 0.5), optionally probs fp32 [n][ld_probs]
- * (NULL to skip). n <= batch_max. */
+/* Sampling decode (extras.py:192-203, main.py:351-370): z fp32 [n][L] -> eval-mode decoder (hidden
+ * layers in exact fp32; the output layer gated per tile between bf16x3 and exact fp32 with an fp64
+ * recompute of the certified band, GM2_OPT_SAMPLE_SPLIT) -> mask u8 [n][ld_mask] =
+ * (sigmoid(logit) > 0.5), optionally probs fp32 [n][ld_probs] (NULL to skip; a probs request runs
+ * the whole output layer in exact fp32). n <= batch_max. */
 int gm2_decode_mask(const gm2_dims* d, const float* params, const float* bn_running, const float* z,
                     int64_t n, uint8_t* mask, int64_t ld_mask, float* probs, int64_t ld_probs, void* ws,
                     void* stream);
@@ -254,8 +256,7 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  * own stream; gm2_timing_end synchronises those events and returns their summed duration and the
  * launch count. Classes: GM2_KC_RECON_LOSS (decoder output layer GEMM + fused BCE / dlogits
  * epilogue), GM2_KC_GEMM_STORE (every other GEMM), GM2_KC_MASK (sampling output layer GEMM). */
-/* Tuning switches (no effect on results' semantics; every value is parity-tested; bit-identical
- * results under every value but GM2_OPT_TAIL_SPLIT's). Each workspace
+/* Tuning switches (no effect on results' semantics; every value is parity-tested). Each workspace
  * has its own set: gm2_workspace_set_option / gm2_workspace_get_option edit / read it and act on
  * the calls that use that workspace. gm2_set_option / gm2_get_option edit / read the PROCESS
  * DEFAULTS: the set a workspace receives at gm2_workspace_init, and the one gm2_gemm (no
@@ -273,7 +274,6 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       0 = always a separate statistics pass.
  *   GM2_OPT_SMALL_WAVES waves per workgroup (4 or 8) of the 128x128 fp32-store GEMM tiles (the
  *                       hidden-layer GEMMs).
- *   GM2_OPT_SMALL_STAGES LDS ring depth (4 or 5) of those 128x128 tiles: K-steps in flight.
  *   GM2_OPT_GRID_CAP    bit 1 = the output-layer, bit 2 = the input-layer weight-gradient GEMM,
  *                       bit 4 = the output-layer loss GEMM runs on a capped grid (workgroups loop over tiles; same rounds, fewer CUs)
  *                       so the work beside it keeps CUs (default 2); 0 = one workgroup per tile.
@@ -302,49 +302,19 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       moments are not updated: read them only after gm2_workspace_join (every
  *                       other libgm2 call on the workspace joins first, which launches a queued
  *                       update on its stream), and keep the buffers passed to gm2_adam_step alive.
- *   GM2_OPT_SIDE_PRIORITY priority of the workspace's side stream (weight-gradient GEMMs, a
- *                       deferred output-layer update): 0 = normal (default), 1 = low (the caller's
- *                       critical-path kernels take CUs first), -1 = high. Takes effect at the next
- *                       side-stream use (the stream is re-created after draining).
- *   GM2_OPT_DW9_LAST    1 = the output-layer weight-gradient GEMM (gradient bucket 0) is forked
- *                       beside the input-layer one at the end of the backward instead of first
- *                       (the hidden-layer chain then runs without it); bucket 0 becomes final late,
- *                       so a data-parallel exchange overlaps less of it. Default 0.
- *   GM2_OPT_TAIL_SPLIT  bit 1 = the output-layer, bit 2 = the input-layer weight-gradient GEMM
- *                       splits the tiles of its short last round (one K pass, 256x256 tiles, more
- *                       tiles than CUs, e.g. 860 on 256 CUs = 3 rounds + 92) into 2..4 K-parts on
- *                       otherwise idle CUs; the last part to finish sums the parts (in part order:
- *                       deterministic) and stores the tile. The ONE option that changes bits: a
- *                       split tile's fp32 sums are formed in two parts (same values up to fp32
- *                       rounding). Default 0.
  *   GM2_OPT_GRAD_BUCKETS (workspace option) 1 = gm2_train_fwd_bwd records the gradient-bucket
  *                       events gm2_wait_grad_bucket waits on (default); 0 = it records none (each
  *                       is a system-scope release on the stream: ~7 us of idle GPU apiece), and
  *                       gm2_wait_grad_bucket fails. For a single process that exchanges nothing.
- *   GM2_OPT_SIDE_CUS    (workspace option) n > 0 = the side stream is created with a CU mask of n
- *                       of the device's CUs (hipExtStreamCreateWithCUMask; the mask's bits are
- *                       interleaved over the XCDs by the driver), so its weight-gradient GEMMs and
- *                       deferred update leave the other CUs to the caller's critical-path chain;
- *                       0 = every CU (default). Replaces GM2_OPT_SIDE_PRIORITY while set. Takes
- *                       effect at the next side-stream use (re-created after draining).
- *                       Results are bit-identical.
- *   GM2_OPT_SMALL_TILE  N width of the 128-row tiles of the bf16 GEMMs whose operands are both
- *                       K-major (the forward's hidden layers): 128 (default) or 64 (two 72-KB
- *                       workgroups per CU). Results are bit-identical.
- *   GM2_OPT_SAMPLE_SPLIT 1 = gm2_decode_mask / gm2_decode_bits without probs run the output layer as
- *                       one bf16 GEMM over 2H (the fp32 activations and weights split into bf16
- *                       hi + lo, summing hi.hi + hi.lo + lo.hi per K-tile) when the error bound
- *                       4.62e-5 max||a||_2 max||w||_2 is at most 2.5e-4; the masks then equal the
- *                       exact-fp32 masks outside |logit| <= 2.5e-4 (inside the 1e-3 band fp32
- *                       summation order decides anyway), else the call runs the exact path
- *                       (default). 0 = always the exact-fp32 output layer. probs requests always
- *                       run exact.
- *   GM2_OPT_BN_FUSE     1 = a bf16 training forward forms the A operand of the hidden-layer GEMMs that
- *                       follow BatchNorm blocks 1, 2, 4, 5 as relu(BatchNorm(Y)) on load (Y the
- *                       previous layer's fp32 pre-BN output) instead of a separate apply pass; the
- *                       bf16 activations the backward reads are stored by the same GEMMs. Results
- *                       bit-identical to 0. Not with SyncBN (its statistics pass through the
- *                       collective first). */
+ *   GM2_OPT_SAMPLE_SPLIT 1 (default) = gm2_decode_mask / gm2_decode_bits without probs run the output
+ *                       layer gated per 256 x 256 tile: as one bf16 GEMM over 2H (the fp32
+ *                       activations and weights split into bf16 hi + lo, summing hi.hi + hi.lo +
+ *                       lo.hi per K-tile) where 4.62e-5 x the tile's largest ||a_r||_2 x its largest
+ *                       ||w_g||_2 is at most 2.5e-4, in exact fp32 elsewhere; logits in the certified
+ *                       band around the threshold are then recomputed in fp64 (GM2_STAT_BAND_*), so
+ *                       a mask bit differs from the correctly rounded logit's only within the
+ *                       reference's own fp32 rounding band. 0 = always the exact-fp32 output layer
+ *                       without band recompute (as do probs requests). */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -353,18 +323,11 @@ enum {
   GM2_OPT_BN_EPILOGUE = 5,
   GM2_OPT_SMALL_WAVES = 6,
   GM2_OPT_INPUT_CHUNKS = 7,
-  GM2_OPT_SMALL_STAGES = 8,
   GM2_OPT_GRID_CAP = 9,
   GM2_OPT_SYNC_BN = 10,
   GM2_OPT_DEFER_OUTPUT_ADAM = 11,
-  GM2_OPT_SIDE_PRIORITY = 12,
-  GM2_OPT_DW9_LAST = 13,
-  GM2_OPT_TAIL_SPLIT = 14,
   GM2_OPT_GRAD_BUCKETS = 15,
-  GM2_OPT_SIDE_CUS = 16,
-  GM2_OPT_SMALL_TILE = 17,
-  GM2_OPT_SAMPLE_SPLIT = 18,
-  GM2_OPT_BN_FUSE = 19
+  GM2_OPT_SAMPLE_SPLIT = 18
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);
@@ -373,9 +336,26 @@ int gm2_workspace_get_option(void* ws, int key, int* value);
 /* Make `stream` wait for work the workspace left running on its side stream (a deferred output-
  * layer Adam update, GM2_OPT_DEFER_OUTPUT_ADAM); no-op when nothing is pending. */
 int gm2_workspace_join(void* ws, void* stream);
-/* Counters of a workspace's host-side state: GM2_STAT_SPLIT_DECODES = sampling decodes whose output
- * layer ran bf16x3 (GM2_OPT_SAMPLE_SPLIT), GM2_STAT_EXACT_DECODES = those that ran exact fp32. */
-enum { GM2_STAT_SPLIT_DECODES = 1, GM2_STAT_EXACT_DECODES = 2 };
+/* Counters of a workspace's sampling decodes (gm2_decode_mask / gm2_decode_bits), cumulative since
+ * gm2_workspace_init; reading one waits for the device.
+ *   GM2_STAT_SPLIT_DECODES  decodes whose output layer ran at least one tile as bf16x3 (GM2_OPT_SAMPLE_SPLIT)
+ *   GM2_STAT_EXACT_DECODES  decodes with no bf16x3 tile (the gate's verdict, a probs request,
+ *                           GM2_OPT_SAMPLE_SPLIT off, or the split path's preconditions)
+ *   GM2_STAT_SPLIT_TILES / GM2_STAT_EXACT_TILES  output-layer tiles (256 x 256 split, 128 x 128 exact)
+ *                           each kernel of the gated decode ran
+ *   GM2_STAT_BAND_ELEMENTS  logits the gated decode found in the certified band |logit - T| <=
+ *                           coef * ||a_r||_2 ||w_g||_2 and recomputed in fp64
+ *   GM2_STAT_BAND_FLIPS     mask bits that recompute changed
+ *   GM2_STAT_BAND_OVERFLOW  band elements beyond a call's list capacity (4,194,304), left as computed */
+enum {
+  GM2_STAT_SPLIT_DECODES = 1,
+  GM2_STAT_EXACT_DECODES = 2,
+  GM2_STAT_SPLIT_TILES = 3,
+  GM2_STAT_EXACT_TILES = 4,
+  GM2_STAT_BAND_ELEMENTS = 5,
+  GM2_STAT_BAND_FLIPS = 6,
+  GM2_STAT_BAND_OVERFLOW = 7
+};
 int gm2_workspace_stat(void* ws, int key, int64_t* value);
 
 /* The all-reduce SyncBN needs (GM2_OPT_SYNC_BN), supplied by the caller: SUM `count` doubles at the

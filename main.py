@@ -206,7 +206,13 @@ def run_sampling(args):
     else:
         z = focused_z(model, config.latent_dim, args.num_samples, args.noise_level, device)
     lo, hi = rank_slice(args.num_samples, rank, world)
+    st0 = model.decode_stats()
     packed, _ = model.decode_bits(z[lo:hi])   # masks stay on the GPU, 8 genes per byte
+    st = {k: v - st0[k] for k, v in model.decode_stats().items()}
+    # (this rank's decode: output-layer tiles per path and the certified band)
+    print(f"- Decode (rank {rank}): {st['split_tiles']} bf16x3 / {st['exact_tiles']} fp32 output tiles; "
+          f"{st['band_elements']} band logits recomputed in fp64, {st['band_flips']} bits changed"
+          + (f", {st['band_overflow']} past the list" if st["band_overflow"] else ""))
     if dist is not None:
         # the ranks' packed slices -> the full set (rank 0 writes the reference's files)
         from gm2.masks import PackedMasks

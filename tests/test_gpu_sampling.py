@@ -7,6 +7,10 @@
     genes sample, its output-space nearest neighbour, z* + sigma * N(0, I) decoded;
   * sample -> train one epoch -> sample on the same model: the second sampling decodes with the
     trained weights (the fp32 decode shadows are re-derived after the bf16 optimizer steps).
+  * the gated decode (GM2_OPT_SAMPLE_SPLIT, api.hip decode_split3) on a REFERENCE-produced fixture
+    where it runs a mix of bf16x3 and exact-fp32 tiles (tests/golden/make_golden_sampling_split.py),
+    with the certified-band fp64 recompute, and the exact path on the same fixture; every test that
+    decodes asserts which path ran from the workspace counters (gm2.h GM2_STAT_*).
 Bar: masks bit-exact to the oracle's fp32 decode outside the fp64 rounding band of each logit
 (|logit64| <= 1e-3: counted, reported, not asserted), probabilities rel 2e-5.
 """
@@ -119,7 +123,17 @@ def test_c3_million_genomes_properties_and_stratified_oracle():
     m.eval()
     torch.manual_seed(0)
     z = torch.randn(N, L)
+    st0 = m.decode_stats()
     pm, _ = m.decode_bits(z.cuda(), chunk=chunk)
+    st = _delta(st0, m.decode_stats())
+    chunks = (N + chunk - 1) // chunk
+    blocks = sum((min(chunk, N - s) + 255) // 256 for s in range(0, N, chunk)) * ((G + 255) // 256)
+    print(f"decode path: {st}")
+    # the default path: every chunk's output layer gated per tile; at these weights every tile's bound
+    # admits the bf16x3 split (so the speed the bench reports is the split kernel's)
+    assert st["split_decodes"] == chunks and st["exact_decodes"] == 0, st
+    assert st["split_tiles"] == blocks and st["exact_tiles"] == 0, st
+    assert st["band_overflow"] == 0 and st["band_elements"] > 0, st
     assert pm.n == N and pm.ld == native.packed_row_bytes(G) == 6880
     sizes = pm.row_sizes()
     rng = np.random.Generator(np.random.PCG64(7))
@@ -146,8 +160,12 @@ def test_c3_million_genomes_properties_and_stratified_oracle():
 
 
 def _stats(m):
-    ws = m.workspace(native.GM2_F32, 1)
-    return ws.stat(native.STAT_SPLIT_DECODES), ws.stat(native.STAT_EXACT_DECODES)
+    st = m.decode_stats()
+    return st["split_decodes"], st["exact_decodes"]
+
+
+def _delta(before, after):
+    return {k: after[k] - before[k] for k in after}
 
 
 @pytest.mark.parametrize("G,H,L,N", [(2900, 512, 32, 5000), (1000, 128, 16, 777)])
@@ -199,9 +217,106 @@ def test_split3_decode_falls_back_when_the_bound_is_too_large():
     res = []
     for split in (1, 0):
         m.workspace(native.GM2_F32, N).set_option(native.OPT_SAMPLE_SPLIT, split)
-        before = _stats(m)
+        before = m.decode_stats()
         mask, _ = m.decode_mask(z)
-        after = _stats(m)
-        assert after[0] == before[0] and after[1] == before[1] + 1
-        res.append(mask.cpu())
-    assert torch.equal(res[0], res[1])
+        d = _delta(before, m.decode_stats())
+        assert d["split_decodes"] == 0 and d["exact_decodes"] == 1 and d["split_tiles"] == 0, d
+        if split:  # every tile of the gated decode ran exact fp32 (300 x 700: 3 x 6 tiles of 128)
+            assert d["exact_tiles"] == 3 * 6, d
+        res.append((mask.cpu().numpy().astype(bool), d))
+    # the same fp32 kernel; the gated call also recomputed its certified band in fp64, which may
+    # change only bits of band elements (and never more bits than it reports flipped)
+    diff = int((res[0][0] != res[1][0]).sum())
+    assert diff <= res[0][1]["band_flips"], (diff, res[0][1])
+    assert _masks_ok(res[0][0], P, S, z) == 0 and _masks_ok(res[1][0], P, S, z) == 0
+
+
+def _split_fixture():
+    from golden_io import load
+    g = load("sampling_split")
+    G, H, L, N = [int(v) for v in g["dims"]]
+    P, S = oracle_state(G, H, L, 0)
+    for k in g.files:
+        if k.startswith("sd/"):
+            name = k[3:]
+            (P if name in P else S)[name] = torch.tensor(g[k].astype(np.float32) if g[k].dtype == np.float16 else g[k])
+    z = torch.tensor(g["z16"].astype(np.float32))
+    ref = np.unpackbits(g["mask_bits"], axis=1, count=G, bitorder="little").astype(bool)
+    near = np.zeros(N * G, dtype=np.float64) + np.inf  # fp64 logit where |logit| <= 2e-3, else inf
+    near[g["near_idx"]] = g["near_logit64"]
+    return g, (G, H, L, N), P, S, z, ref, near.reshape(N, G)
+
+
+def test_split_fixture_gated_decode_matches_reference():
+    """The gated sampling decode (default GM2_OPT_SAMPLE_SPLIT = 1) on a reference-produced fixture
+    (tests/golden/make_golden_sampling_split.py: G 3,000, hidden 512, latent 32, 1,024 genomes; one
+    genome block and one gene block scaled past the split bound): the tiles the fixture's fp64
+    verdict admits run bf16x3, the rest exact fp32 (counted per path), logits in the certified band
+    are recomputed in fp64. Bars, for the packed and the u8 output alike:
+      * bit-exact to the reference's own masks outside |logit64| <= 1e-3;
+      * every mask bit equals the correctly rounded fp64 logit's (float(logit64) > T) wherever
+        |logit64| > 2e-5 -- the band recompute leaves only the hidden layers' fp32 noise;
+      * counters: 2 x the fixture's split tiles, 2 x 4 x its exact 256-blocks (128-tiles), band
+        elements found and recomputed, none past the list."""
+    g, (G, H, L, N), P, S, z, ref, l64 = _split_fixture()
+    m = to_model(P, S, G, H, L, native.GM2_F32)
+    m.eval()
+    verdict = g["split_verdict"].astype(bool)
+    st0 = m.decode_stats()
+    pm, _ = m.decode_bits(z)
+    mask, _ = m.decode_mask(z)
+    d = _delta(st0, m.decode_stats())
+    print(f"decode path: {d}; fixture verdict {int(verdict.sum())} split / {int((~verdict).sum())} exact blocks")
+    assert d["split_decodes"] == 2 and d["exact_decodes"] == 0, d
+    assert d["split_tiles"] == 2 * int(verdict.sum()), d
+    assert d["exact_tiles"] == 2 * 4 * int((~verdict).sum()), d
+    assert d["band_elements"] > 0 and d["band_overflow"] == 0, d
+    bits = np.unpackbits(pm.bits.cpu().numpy(), axis=1, bitorder="little")
+    assert not bits[:, G:].any()
+    for got in (bits[:, :G].astype(bool), mask.cpu().numpy().astype(bool)):
+        band = np.abs(l64) <= 1e-3
+        bad = (got != ref) & ~band
+        print(f"{int(((got != ref) & band).sum())} reference mismatches inside the 1e-3 band, {int(bad.sum())} outside")
+        assert int(bad.sum()) == 0
+        # the fp64 decision: (float)logit64 > T
+        dec64 = l64.astype(np.float32) > np.float32(8.940696716308594e-08)
+        known = np.isfinite(l64) & (np.abs(l64) > 2e-5)
+        assert int(((got != dec64) & known).sum()) == 0, int(((got != dec64) & known).sum())
+
+
+def test_split_fixture_exact_path_matches_reference():
+    """GM2_OPT_SAMPLE_SPLIT = 0 on the same reference fixture: the whole output layer in exact fp32
+    (no tile gate, no band recompute; counted as an exact decode), bit-exact to the reference's masks
+    outside |logit64| <= 1e-3."""
+    g, (G, H, L, N), P, S, z, ref, l64 = _split_fixture()
+    m = to_model(P, S, G, H, L, native.GM2_F32)
+    m.eval()
+    m.workspace(native.GM2_F32, N).set_option(native.OPT_SAMPLE_SPLIT, 0)
+    st0 = m.decode_stats()
+    mask, _ = m.decode_mask(z)
+    d = _delta(st0, m.decode_stats())
+    assert d["exact_decodes"] == 1 and d["split_decodes"] == 0 and d["split_tiles"] == 0 and d["band_elements"] == 0, d
+    got = mask.cpu().numpy().astype(bool)
+    band = np.abs(l64) <= 1e-3
+    print(f"{int(((got != ref) & band).sum())} mismatches inside the 1e-3 band")
+    assert int(((got != ref) & ~band).sum()) == 0
+
+
+def test_odd_latent_width_decodes_on_the_exact_path():
+    """latent_dim = 1 (odd: the output weights start 4-B aligned in the parameter buffer,
+    which the split kernels cannot read) -- the gated decode's preconditions fail before anything is
+    launched and the call runs the exact path (counted as such) instead of failing."""
+    G, H, L, N = 500, 128, 1, 700
+    P, S = perturb_bn(*oracle_state(G, H, L, 95), seed=96)
+    P["decoder.9.bias"] = torch.linspace(-1.0, 1.0, G)
+    m = to_model(P, S, G, H, L, native.GM2_F32)
+    m.eval()
+    z = torch.randn(N, L, generator=torch.Generator().manual_seed(97))
+    st0 = m.decode_stats()
+    pm, _ = m.decode_bits(z)
+    mask, _ = m.decode_mask(z)
+    d = _delta(st0, m.decode_stats())
+    assert d["exact_decodes"] == 2 and d["split_decodes"] == 0, d
+    np.testing.assert_array_equal(np.unpackbits(pm.bits.cpu().numpy(), axis=1, count=G, bitorder="little"),
+                                  mask.cpu().numpy())
+    assert _masks_ok(mask.cpu().numpy(), P, S, z) == 0

@@ -33,12 +33,13 @@ def test_header_constants_match_binding():
     bucket count, option keys, the gm2_batch field order (ABI 2 adds `next`); option setters accept
     and reject values without a GPU, and the bucket bounds tile the gradient buffer in order. ABI 3:
     options and bucket events are per workspace; a workspace libgm2 never initialised is refused.
-    ABI 4: gm2_batch gains the resident-operand fields; gm2_resident_layout sizes them."""
+    ABI 4: gm2_batch gains the resident-operand fields; gm2_resident_layout sizes them. ABI 5: seven
+    tuning options pruned (their keys now refused), the sampling decode's GM2_STAT_* counters."""
     import ctypes
     from gm2 import native
     txt = open(os.path.join(ROOT, "include", "gm2.h")).read()
     assert int(re.search(r"#define GM2_ABI_VERSION (\d+)", txt).group(1)) == native.lib().gm2_abi_version() \
-        == native.ABI_VERSION == 4
+        == native.ABI_VERSION == 5
     bogus = ctypes.c_void_p(0x1000)
     v = ctypes.c_int()
     assert native.lib().gm2_workspace_set_option(bogus, native.OPT_GRID_CAP, 1) != 0
@@ -50,6 +51,10 @@ def test_header_constants_match_binding():
     opts = dict((k, int(v)) for k, v in re.findall(r"GM2_OPT_([A-Z_]+) = (\d+)", txt))
     for k, v in opts.items():
         assert getattr(native, "OPT_" + k) == v, k
+    stats = dict((k, int(v)) for k, v in re.findall(r"GM2_STAT_([A-Z_]+) = (\d+)", txt))
+    assert len(stats) == 7 and set(native.DECODE_STATS.values()) == set(stats.values())
+    for k, v in stats.items():
+        assert getattr(native, "STAT_" + k) == v, k
     assert [f[0] for f in native.Batch._fields_] == ["data", "ld_data", "rows", "n", "eps", "next", "resident",
                                                      "ld_resident", "resident_bits", "ld_resident_bits",
                                                      "resident_rows", "resident_prec"]
@@ -71,14 +76,12 @@ def test_header_constants_match_binding():
     native.set_option(native.OPT_INPUT_CHUNKS, 1)
     with pytest.raises(RuntimeError, match="1 or 4"):
         native.set_option(native.OPT_INPUT_CHUNKS, 2)
-    with pytest.raises(RuntimeError, match="4 or 5"):
-        native.set_option(native.OPT_SMALL_STAGES, 3)
-    old = native.get_option(native.OPT_TAIL_SPLIT)
-    native.set_option(native.OPT_TAIL_SPLIT, 3)
-    assert native.get_option(native.OPT_TAIL_SPLIT) == 3
-    native.set_option(native.OPT_TAIL_SPLIT, old)
-    with pytest.raises(RuntimeError, match="tail split"):
-        native.set_option(native.OPT_TAIL_SPLIT, 4)
+    with pytest.raises(RuntimeError, match="4 or 8"):
+        native.set_option(native.OPT_SMALL_WAVES, 5)
+    # the options pruned in ABI 5 (measured slower or neutral; evidence kept in profiles/) are gone
+    for key in (8, 12, 13, 14, 16, 17, 19):
+        with pytest.raises(RuntimeError, match="unknown option"):
+            native.set_option(key, 0)
     G, H, L = 55039, 1024, 64
     b = native.grad_bucket_bounds(native.dims(G, H, L, 4096))
     cover = sorted(b)

@@ -92,12 +92,9 @@ static void dims_and_layouts() {
   for (int64_t G : {1, 8, 9, 127, 128, 55039}) CHECK(gm2_packed_row_bytes(G) >= (G + 7) / 8, "packed row bytes");
 }
 
-static const int kKeys[] = {GM2_OPT_GEMM_PP,       GM2_OPT_SIDE_STREAM,  GM2_OPT_RECON_TILE,  GM2_OPT_SMALL_SPLIT,
-                            GM2_OPT_BN_EPILOGUE,   GM2_OPT_SMALL_WAVES,  GM2_OPT_INPUT_CHUNKS, GM2_OPT_SMALL_STAGES,
-                            GM2_OPT_GRID_CAP,      GM2_OPT_SYNC_BN,      GM2_OPT_DEFER_OUTPUT_ADAM,
-                            GM2_OPT_SIDE_PRIORITY, GM2_OPT_DW9_LAST,     GM2_OPT_TAIL_SPLIT,  GM2_OPT_GRAD_BUCKETS,
-                            GM2_OPT_SIDE_CUS,      GM2_OPT_SMALL_TILE,   GM2_OPT_SAMPLE_SPLIT,
-                            GM2_OPT_BN_FUSE};
+static const int kKeys[] = {GM2_OPT_GEMM_PP,      GM2_OPT_SIDE_STREAM,  GM2_OPT_RECON_TILE,        GM2_OPT_SMALL_SPLIT,
+                            GM2_OPT_BN_EPILOGUE,  GM2_OPT_SMALL_WAVES,  GM2_OPT_INPUT_CHUNKS,      GM2_OPT_GRID_CAP,
+                            GM2_OPT_SYNC_BN,      GM2_OPT_DEFER_OUTPUT_ADAM, GM2_OPT_GRAD_BUCKETS, GM2_OPT_SAMPLE_SPLIT};
 
 static void options() {
   std::vector<int> saved;

@@ -1,7 +1,6 @@
 // Launch time of the one-pass weight-gradient GEMM (launch_gemm_sq: fp32 store + per-tile sums of
 // squares) alone on the chip, per grid mode (diagnostic probe, not part of libgm2):
-//   mode 0 one workgroup per tile, 1 capped grid (GM2_OPT_GRID_CAP bit 2), 2 split tail
-//   (GM2_OPT_TAIL_SPLIT bit 2). Random bf16 operands. With -DGM2_STAMPS it also prints the phase
+//   mode 0 one workgroup per tile, 1 capped grid (GM2_OPT_GRID_CAP bit 2). Random bf16 operands. With -DGM2_STAMPS it also prints the phase
 //   distribution per workgroup (entry, main loop done, stores done).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 [-DGM2_STAMPS] -I../../include
 //        -I../../genome-minimizer-2_amd/csrc time_sq.hip -o time_sq
@@ -35,24 +34,19 @@ int main(int argc, char** argv) {
   const int reps = argc > 7 ? atoi(argv[7]) : 20;
   const int Mp = (M + 255) / 256 * 256, Np = (N + 255) / 256 * 256;
   bf16_t *P, *Q;
-  float *C, *part;
+  float* C;
   double* sq;
-  int* cnt;
   hipMalloc(&P, (size_t)Mp * K * 2);
   hipMalloc(&Q, (size_t)Np * K * 2);
   hipMalloc(&C, (size_t)M * N * 4);
   hipMalloc(&sq, (size_t)(Mp / 256) * (Np / 256) * 8);
-  hipMalloc(&part, kTailPartBytes);
-  hipMalloc(&cnt, kTailCntBytes);
-  hipMemset(cnt, 0, kTailCntBytes);
   fill(P, (size_t)Mp * K, 1);
   fill(Q, (size_t)Np * K, 2);
   GemmArgs<bf16_t> g{P, pk ? K : Mp, Q, qk ? K : Np, M, N, K, Mp, Np, 0, pk, qk};
   Options o = default_options();
   o.grid_cap = mode == 1 ? 2 : 0;
-  o.tail_split = mode == 2 ? 2 : 0;
   OptionScope scope(o);
-  auto run = [&] { launch_gemm_sq<bf16_t>(g, C, N, sq, nullptr, false, part, cnt); };
+  auto run = [&] { launch_gemm_sq<bf16_t>(g, C, N, sq, nullptr, false); };
   for (int r = 0; r < 3; ++r) run();
   hipDeviceSynchronize();
   hipEvent_t e0, e1;
@@ -91,22 +85,6 @@ int main(int argc, char** argv) {
   pr("start", start);
   pr("to-loop", loop);
   pr("end", end);
-  if (mode == 2) {  // the split tail's parts: launch order puts them after the whole tiles
-    const int whole = (Mp / 256) * (Np / 256) / 256 * 256;
-    std::vector<double> ps, pl, pj, pe;
-    for (int b = whole; b < blocks; ++b) {
-      const unsigned long long* s = &st[b * 8];
-      if (!s[0] || s[0] < t0) continue;
-      ps.push_back((s[0] - t0) * 0.01);
-      pl.push_back((s[5] - s[1]) * 0.01);
-      if (s[2] > s[5]) pj.push_back((s[2] - s[5]) * 0.01);
-      if (s[3] > s[0]) pe.push_back((s[3] - t0) * 0.01);
-    }
-    pr("part start", ps);
-    pr("part loop", pl);
-    pr("part join", pj);
-    pr("part end", pe);
-  }
 #endif
   return 0;
 }
