@@ -1499,6 +1499,18 @@ int gm2_reparameterize(int64_t n, const float* mu, const float* logvar, const fl
   });
 }
 
+int gm2_exchange_pack(const float* x, int64_t n, uint16_t* out, int64_t n_pad, void* stream) {
+  return guarded([&] { launch_exchange_pack(x, n, (bf16_t*)out, n_pad, (hipStream_t)stream); });
+}
+
+int gm2_exchange_ranksum(const uint16_t* parts, int world, int64_t chunk, uint16_t* out, void* stream) {
+  return guarded([&] { launch_exchange_ranksum((const bf16_t*)parts, world, chunk, (bf16_t*)out, (hipStream_t)stream); });
+}
+
+int gm2_exchange_unpack(const uint16_t* in, int64_t n, float* x, void* stream) {
+  return guarded([&] { launch_exchange_unpack((const bf16_t*)in, n, x, (hipStream_t)stream); });
+}
+
 int gm2_grad_bucket_bounds(const gm2_dims* d, int64_t* lo_hi) {
   return guarded([&] { bucket_bounds(make_dims(d), lo_hi); });
 }

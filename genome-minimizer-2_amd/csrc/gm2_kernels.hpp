@@ -316,6 +316,12 @@ void launch_slab_sum(const float* slabs, int S, int64_t slab, int M, int N, floa
 void launch_fwd_tail(const float* lpart, int nl, const float* kpart, int nk, double* loss, const float* cpart, int rows,
                      int64_t ld, int64_t n, float* cout, int* hdr, int hv0, int hv1, hipStream_t s);
 
+// bf16 gradient exchange (gm2.h gm2_exchange_*): fp32 -> bf16 (RNE, zero pad to n_pad); the rank-order
+// fp32 sum of `world` bf16 chunks rounded to bf16 (chunk % 8 == 0); bf16 -> fp32
+void launch_exchange_pack(const float* x, int64_t n, bf16_t* out, int64_t n_pad, hipStream_t s);
+void launch_exchange_ranksum(const bf16_t* parts, int world, int64_t chunk, bf16_t* out, hipStream_t s);
+void launch_exchange_unpack(const bf16_t* in, int64_t n, float* x, hipStream_t s);
+
 // ---- masks.hip: consumers of the packed sampled masks ----
 void launch_count_groups(const uint8_t* bits, int64_t n, int64_t ldb, const int32_t* goff, int64_t ngroups,
                          const int32_t* pos, int32_t* counts, hipStream_t s);

@@ -1106,6 +1106,91 @@ __global__ __launch_bounds__(256) void k_split3(const float* __restrict__ X, int
 }
 
 // ---------------------------------------------------------------------------------------------
+// bf16 gradient exchange (gm2/ddp.py bf16_exchange_sum, gm2.h gm2_exchange_*): pack rounds the fp32
+// gradient to bf16 (RNE, zero pad up to n_pad), ranksum forms out[i] = bf16(((p_0[i] + p_1[i]) + ...)
+// + p_{world-1}[i]) in fp32 in rank order from the world's received bf16 chunks, unpack widens the
+// gathered bf16 vector back into the fp32 gradient. 8 elements per thread (16-B bf16 / 32-B fp32).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_exchange_pack(const float* __restrict__ x, int64_t n, bf16_t* __restrict__ out,
+                                                     int64_t n_pad) {
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < n_pad; i += (int64_t)gridDim.x * 256 * 8) {
+    uint32_t w[4];
+    if (i + 8 <= n && (((uintptr_t)(x + i)) & 15) == 0) {
+      const float4 a = *(const float4*)(x + i), b = *(const float4*)(x + i + 4);
+      w[0] = f2bf2(a.x, a.y); w[1] = f2bf2(a.z, a.w); w[2] = f2bf2(b.x, b.y); w[3] = f2bf2(b.z, b.w);
+    } else {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = i + e < n ? x[i + e] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = f2bf2(v[2 * e], v[2 * e + 1]);
+    }
+    if (i + 8 <= n_pad) {
+      *(uint4*)(out + i) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (i + e < n_pad) out[i + e] = (bf16_t)(w[e >> 1] >> (16 * (e & 1)));
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_exchange_ranksum(const bf16_t* __restrict__ parts, int world, int64_t chunk,
+                                                        bf16_t* __restrict__ out) {
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < chunk; i += (int64_t)gridDim.x * 256 * 8) {
+    float acc[8];
+    const bool vec = i + 8 <= chunk;
+    for (int r = 0; r < world; ++r) {
+      const bf16_t* p = parts + (int64_t)r * chunk + i;
+      float v[8];
+      if (vec) {
+        const uint4 q = *(const uint4*)p;
+        const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] = __uint_as_float(u[e] << 16);
+          v[2 * e + 1] = __uint_as_float(u[e] & 0xFFFF0000u);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = i + e < chunk ? bf2f(p[e]) : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = r == 0 ? v[e] : acc[e] + v[e];
+    }
+    if (vec) {
+      *(uint4*)(out + i) = make_uint4(f2bf2(acc[0], acc[1]), f2bf2(acc[2], acc[3]), f2bf2(acc[4], acc[5]),
+                                      f2bf2(acc[6], acc[7]));
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (i + e < chunk) out[i + e] = f2bf(acc[e]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_exchange_unpack(const bf16_t* __restrict__ in, int64_t n, float* __restrict__ x) {
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < n; i += (int64_t)gridDim.x * 256 * 8) {
+    if (i + 8 <= n && (((uintptr_t)(x + i)) & 15) == 0) {
+      const uint4 q = *(const uint4*)(in + i);
+      const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] = __uint_as_float(u[e] << 16);
+        v[2 * e + 1] = __uint_as_float(u[e] & 0xFFFF0000u);
+      }
+      *(float4*)(x + i) = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)(x + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (i + e < n) x[i + e] = bf2f(in[i + e]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Certified-band recompute of the sampling decode (MaskBand; SURVEY.md 7 "Hard parts" (ii)): one
 // wave per listed (row, gene): logit = sum_k A[row][k] W[gene][k] in fp64 (each lane a strided
 // slice of k in order, then a fixed-order wave reduction: deterministic) + bias[gene]; the mask bit
@@ -1349,6 +1434,33 @@ void launch_split3(const float* X, int64_t ldx, int rows, int rows_pad, int K, b
       (((uintptr_t)out) & 15))
     throw Gm2Error("split3: K %d, ld %lld / %lld, rows %d / %d", K, (long long)ldx, (long long)ldo, rows, rows_pad);
   hipLaunchKernelGGL(k_split3, dim3(rows_pad / 16), dim3(256), 0, s, X, ldx, rows, K, out, ldo, rn, blk);
+  GM2_CHECK_LAUNCH();
+}
+
+static unsigned elementwise_grid(int64_t n) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 2047) / 2048, 8192));
+}
+
+void launch_exchange_pack(const float* x, int64_t n, bf16_t* out, int64_t n_pad, hipStream_t s) {
+  if (n < 0 || n_pad < n || (((uintptr_t)out) & 15)) throw Gm2Error("exchange pack: n %lld, n_pad %lld", (long long)n, (long long)n_pad);
+  if (n_pad == 0) return;
+  hipLaunchKernelGGL(k_exchange_pack, dim3(elementwise_grid(n_pad)), dim3(256), 0, s, x, n, out, n_pad);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_exchange_ranksum(const bf16_t* parts, int world, int64_t chunk, bf16_t* out, hipStream_t s) {
+  if (world < 1 || chunk < 0 || chunk % 8 || (((uintptr_t)parts | (uintptr_t)out) & 15))
+    throw Gm2Error("exchange ranksum: world %d, chunk %lld (a multiple of 8, 16-B aligned buffers)", world,
+                   (long long)chunk);
+  if (chunk == 0) return;
+  hipLaunchKernelGGL(k_exchange_ranksum, dim3(elementwise_grid(chunk)), dim3(256), 0, s, parts, world, chunk, out);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_exchange_unpack(const bf16_t* in, int64_t n, float* x, hipStream_t s) {
+  if (n < 0 || (((uintptr_t)in) & 15)) throw Gm2Error("exchange unpack: n %lld", (long long)n);
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_exchange_unpack, dim3(elementwise_grid(n)), dim3(256), 0, s, in, n, x);
   GM2_CHECK_LAUNCH();
 }
 

@@ -81,20 +81,28 @@ def bf16_exchange_sum(dist, x, scratch=None):
     at most world x 2^-24 of sum_r |x_r|, and the sum is rounded once),
     and every rank gets identical values. Returns the reduced vector (fp32, x's device) in x.
     `scratch`: optional dict reused across calls for the bf16 buffers.
+    On a GPU the casts and the rank-order sum are libgm2's kernels (gm2_exchange_pack / _ranksum /
+    _unpack); host tensors (the CPU gloo tests of the method) take the same arithmetic in torch.
     gloo with device tensors (the one-GPU rehearsal tests) stages the two collectives through host
     memory; RCCL runs them on the device."""
     world = dist.get_world_size()
     n = x.numel()
     c = -(-n // world)
+    if x.is_cuda:
+        c = -(-c // 8) * 8  # (the kernels take 16-B chunks)
     sc = scratch if scratch is not None else {}
     if sc.get("n", 0) < world * c or sc["send"].device != x.device:
         for k in ("send", "recv", "gath"):
             sc[k] = torch.empty(world * c, dtype=torch.bfloat16, device=x.device)
         sc["n"] = world * c
     send, recv, gath = sc["send"][:world * c], sc["recv"][:world * c], sc["gath"][:world * c]
-    send[:n].copy_(x)
-    send[n:].zero_()
-    host = x.is_cuda and dist.get_backend() == "gloo"
+    dev = x.is_cuda
+    if dev:
+        native.exchange_pack(x, send)
+    else:
+        send[:n].copy_(x)
+        send[n:].zero_()
+    host = dev and dist.get_backend() == "gloo"
     if host:
         hs, hr = send.cpu(), torch.empty(world * c, dtype=torch.bfloat16)
         dist.all_to_all_single(hr, hs)
@@ -102,17 +110,27 @@ def bf16_exchange_sum(dist, x, scratch=None):
     else:
         dist.all_to_all_single(recv, send)
     parts = recv.view(world, c)
-    acc = parts[0].float()
-    for r in range(1, world):  # rank order: the same value on every rank, run to run
-        acc.add_(parts[r].float())
-    mine = acc.to(torch.bfloat16)
+    if dev:
+        mine = sc.setdefault("mine", torch.empty(0, dtype=torch.bfloat16, device=x.device))
+        if mine.numel() < c:
+            mine = sc["mine"] = torch.empty(c, dtype=torch.bfloat16, device=x.device)
+        mine = mine[:c]
+        native.exchange_ranksum(recv, world, mine)
+    else:
+        acc = parts[0].float()
+        for r in range(1, world):  # rank order: the same value on every rank, run to run
+            acc.add_(parts[r].float())
+        mine = acc.to(torch.bfloat16)
     if host:
         hg = [torch.empty(c, dtype=torch.bfloat16) for _ in range(world)]
         dist.all_gather(hg, mine.cpu())
         gath.copy_(torch.cat(hg))
     else:
         dist.all_gather_into_tensor(gath, mine)
-    x.copy_(gath[:n])
+    if dev:
+        native.exchange_unpack(gath, x)
+    else:
+        x.copy_(gath[:n])
     return x
 
 

@@ -34,7 +34,8 @@ EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_of
            "gm2_workspace_set_option", "gm2_workspace_get_option", "gm2_workspace_release",
            "gm2_workspace_set_collective", "gm2_workspace_join",
            "gm2_resident_layout", "gm2_resident_build",
-           "gm2_timing_begin", "gm2_timing_end", "gm2_workspace_stat"]
+           "gm2_timing_begin", "gm2_timing_end", "gm2_workspace_stat",
+           "gm2_exchange_pack", "gm2_exchange_ranksum", "gm2_exchange_unpack"]
 ABI_VERSION = 5
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
 OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE, OPT_SMALL_SPLIT, OPT_BN_EPILOGUE, OPT_SMALL_WAVES = 1, 2, 3, 4, 5, 6
@@ -116,6 +117,9 @@ def lib():
         "gm2_resident_layout": (C.c_int, [i64, i64, i32, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                            C.POINTER(C.c_int64), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
         "gm2_resident_build": (C.c_int, [vp, i64, i64, i64, i32, vp, vp, vp]),
+        "gm2_exchange_pack": (C.c_int, [vp, i64, vp, i64, vp]),
+        "gm2_exchange_ranksum": (C.c_int, [vp, i32, i64, vp, vp]),
+        "gm2_exchange_unpack": (C.c_int, [vp, i64, vp, vp]),
         "gm2_timing_begin": (C.c_int, [i32]),
         "gm2_timing_end": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     }
@@ -387,6 +391,21 @@ def wait_grad_bucket(ws: Workspace, bucket: int, stream_obj):
     """Make `stream_obj` (a torch.cuda.Stream) wait until gradient bucket `bucket` of the last
     backward on workspace `ws` is final (device-side wait)."""
     check(lib().gm2_wait_grad_bucket(ws.ptr, int(bucket), C.c_void_p(stream_obj.cuda_stream)), "gm2_wait_grad_bucket")
+
+
+def exchange_pack(x, out):
+    """out[:n] = bf16(x) (RNE), out[n:] = 0 (gm2_exchange_pack; x fp32, out bf16, both on the device)."""
+    check(lib().gm2_exchange_pack(ptr(x), x.numel(), ptr(out), out.numel(), stream()), "gm2_exchange_pack")
+
+
+def exchange_ranksum(parts, world, out):
+    """out = bf16(fp32 sum of the `world` chunks of `parts` in rank order) (gm2_exchange_ranksum)."""
+    check(lib().gm2_exchange_ranksum(ptr(parts), int(world), out.numel(), ptr(out), stream()), "gm2_exchange_ranksum")
+
+
+def exchange_unpack(src, x):
+    """x = fp32(src[:x.numel()]) (gm2_exchange_unpack)."""
+    check(lib().gm2_exchange_unpack(ptr(src), x.numel(), ptr(x), stream()), "gm2_exchange_unpack")
 
 
 def set_option(key: int, value: int):

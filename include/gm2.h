@@ -159,6 +159,19 @@ int gm2_train_fwd_bwd(const gm2_dims* d, int precision, const gm2_batch* batch, 
 int gm2_grad_bucket_bounds(const gm2_dims* d, int64_t* lo_hi);
 int gm2_wait_grad_bucket(void* ws, int bucket, void* stream);
 
+/* The bf16 exchange of the big weight-gradient buckets (gm2/ddp.py bf16_exchange_sum; the reference
+ * is single-device): every rank rounds its bucket to bf16 once (pack), sends chunk j to
+ * rank j (all-to-all, the caller's collective), rank j sums the world's chunks in fp32 IN RANK ORDER
+ * and rounds the sum to bf16 once (ranksum), an all-gather hands every rank every chunk, and unpack
+ * widens it back into the fp32 gradient. Device pointers, stream-ordered, no allocation.
+ *   gm2_exchange_pack     out[i] = bf16_rne(x[i]) for i < n, 0 for n <= i < n_pad (out 16-B aligned)
+ *   gm2_exchange_ranksum  out[i] = bf16_rne((((float)parts[0][i] + parts[1][i]) + ...) + parts[world-1][i]),
+ *                         parts = world chunks of `chunk` elements back to back (chunk % 8 == 0)
+ *   gm2_exchange_unpack   x[i] = (float)in[i], i < n */
+int gm2_exchange_pack(const float* x, int64_t n, uint16_t* out, int64_t n_pad, void* stream);
+int gm2_exchange_ranksum(const uint16_t* parts, int world, int64_t chunk, uint16_t* out, void* stream);
+int gm2_exchange_unpack(const uint16_t* in, int64_t n, float* x, void* stream);
+
 /* L1 term + clip_grad_norm_ statistics (trainer.py:119; loss_components.py:167-184): computes
  * ||g + lambda*sign(theta)||_2 (loss slot [4]), sum|theta| (slot [3]) and the clip coefficient
  * min(1, max_norm/(norm+1e-6)) kept in the workspace for gm2_adam_step. */

@@ -454,3 +454,57 @@ def test_three_rank_batch_smaller_than_two_per_rank(tmp_path):
         np.testing.assert_array_equal(r[0]["params"], r[k]["params"])
         np.testing.assert_array_equal(r[0]["rec"], r[k]["rec"])
     assert np.isfinite(r[0]["rec"]).all() and np.isfinite(r[0]["params"]).all()
+
+
+def _xchg_worker(rank, world, port, out_dir, n):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from gm2.ddp import bf16_exchange_sum
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = torch.Generator().manual_seed(500 + rank)
+    x = torch.randn(n, generator=g) * torch.exp(2.0 * torch.randn(n, generator=g)) * 1e-3
+    x[::53] = 0.0
+    dev = bf16_exchange_sum(dist, x.cuda(), {})    # libgm2's pack / rank-order sum / unpack kernels
+    host = bf16_exchange_sum(dist, x.clone(), {})  # the same method in torch (the CPU form)
+    np.save(os.path.join(out_dir, f"d{rank}.npy"), dev.cpu().numpy())
+    np.save(os.path.join(out_dir, f"h{rank}.npy"), host.numpy())
+    dist.destroy_process_group()
+
+
+def test_two_rank_bf16_exchange_kernels_bit_equal_to_torch(tmp_path):
+    """gm2.ddp.bf16_exchange_sum on device tensors runs the cast, the rank-order fp32 sum and the
+    widening as libgm2 kernels (gm2_exchange_pack / _ranksum / _unpack); over 2 ranks (gloo, both on
+    the one GPU) the result equals the torch form of the same method bit for bit, on both ranks."""
+    n = (1 << 17) + 37
+    port = _free_port()
+    mp.spawn(_xchg_worker, args=(2, port, str(tmp_path), n), nprocs=2, join=True)
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(tmp_path / f"d{r}.npy"), np.load(tmp_path / f"h{r}.npy"))
+    np.testing.assert_array_equal(np.load(tmp_path / "d0.npy"), np.load(tmp_path / "d1.npy"))
+
+
+def test_exchange_kernels_against_torch_single_process():
+    """The three exchange entry points directly, world 3 and a ragged length: pack == torch's RNE cast
+    with zero pad, ranksum == ((p0 + p1) + p2) in fp32 then RNE, unpack == the exact widening."""
+    from gm2 import native
+    n, world = 100_003, 3
+    c = -(-n // world)
+    c = -(-c // 8) * 8
+    x = (torch.randn(world * c) * torch.exp(3.0 * torch.randn(world * c))).cuda()
+    x[::17] = 0.0
+    send = torch.empty(world * c, dtype=torch.bfloat16, device="cuda")
+    native.exchange_pack(x[:n], send)
+    ref = torch.zeros(world * c, dtype=torch.bfloat16, device="cuda")
+    ref[:n] = x[:n].to(torch.bfloat16)
+    assert torch.equal(send.view(torch.int16), ref.view(torch.int16))
+    parts = x.to(torch.bfloat16)
+    out = torch.empty(c, dtype=torch.bfloat16, device="cuda")
+    native.exchange_ranksum(parts, world, out)
+    acc = parts[:c].float()
+    for r in range(1, world):
+        acc = acc + parts[r * c:(r + 1) * c].float()
+    assert torch.equal(out.view(torch.int16), acc.to(torch.bfloat16).view(torch.int16))
+    y = torch.empty(n - 5, device="cuda")
+    native.exchange_unpack(parts, y)
+    assert torch.equal(y, parts[:n - 5].float())
