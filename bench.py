@@ -12,8 +12,10 @@ SUM-all-reduced over RCCL every step (weak scaling: value = all ranks' rows / ma
 `torch.distributed.run` process; this parent never touches the GPU) and exits with its code.
 
 Also reported (extra fields, not `value`): sampling throughput of `--mode sample` for the v1 preset
-(C3: 1e6 genomes/s decoded in exact fp32, thresholded into packed masks, essential genes counted on
-the device, masks + counts copied to pinned host memory), the same training step in the other GEMM
+(C3: 1e6 genomes from a v1 checkpoint trained on the synthetic matrix, decoded with the output layer
+gated per tile between bf16x3 and exact fp32 and the certified band recomputed in fp64, thresholded
+into packed masks, essential genes counted on the device, masks + counts copied to pinned host
+memory; the split fraction and band counts are reported), the same training step in the other GEMM
 precision (f32 next to the bf16 headline), the live-timed dominant kernel against the MFMA roofline,
 and the CPU baseline (the oracle = the reference's algorithm on torch-CPU, fp32, all host threads,
 the same v0 step at batch 4096 on the same matrix; plus the C1 batch-64 point), and the C5-shaped
@@ -84,6 +86,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sample", action="store_true")
     ap.add_argument("--sample-genomes", type=int, default=1000000)
+    ap.add_argument("--sample-train-epochs", type=int, default=10,
+                    help="epochs of v1 training (lr 1e-3, batch 4096, the synthetic matrix) before the sample leg "
+                         "decodes from that checkpoint; 0 = the untrained (xavier) model")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-f32-line", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true",
@@ -426,10 +431,36 @@ def main():
         dist.destroy_process_group()
 
 
+def train_v1_checkpoint(a, dev, G, H, L):
+    """The sample leg's checkpoint: a v1 model (hidden 512, latent 32, bf16 GEMMs) trained
+    a.sample_train_epochs epochs at lr 1e-3 (batch 4096, clip 1.0, L1 0.01, the v1 KL / abundance
+    schedules) on the synthetic pan-genome matrix, so the output weights and activations have
+    trained scales (the decode's per-tile gate and certified band see realistic logits). Every rank
+    trains the same model on the same data (deterministic kernels)."""
+    from gm2.data import ResidentMatrix, StrainLoader, synthetic_pangenome
+    from gm2.model import VAE
+    from gm2.trainer import Adam, StepLR, create_v1_trainer
+    from gm2 import native
+    torch.manual_seed(11)
+    m = VAE(G, H, L, device=dev, precision=native.GM2_BF16)
+    opt = Adam(m, lr=1e-3)
+    tr = create_v1_trainer(m, opt, StepLR(opt), a.sample_train_epochs, 1.0, 0.01)
+    mat = ResidentMatrix(synthetic_pangenome(a.strains, G, seed=4242), device=dev)
+    loader = StrainLoader(mat, None, 4096, shuffle=True)
+    for ep in range(a.sample_train_epochs):
+        tr.train_epoch(loader, ep)
+    torch.cuda.synchronize()
+    del mat, loader, tr
+    torch.cuda.empty_cache()
+    return m
+
+
 def sample_bench(a, dev, dist=None, rank=0, world=1):
     """C3: v1 preset (hidden 512, latent 32) `--mode sample` of a.sample_genomes genomes (1e6 by
-    default) in 65,536-genome chunks: z ~ N(0, I) drawn on the device (extras.py:197), exact-fp32
-    decode + threshold into packed masks in HBM (gm2_decode_bits), the essential-gene counts of
+    default) in 65,536-genome chunks from a trained v1 checkpoint (train_v1_checkpoint): z ~ N(0, I)
+    drawn on the device (extras.py:197), the decode (fp32 hidden layers; the output layer gated per
+    tile between bf16x3 and exact fp32, certified band recomputed in fp64) + threshold into packed
+    masks in HBM (gm2_decode_bits), the essential-gene counts of
     every genome on the device (gm2_mask_count_groups, a synthetic 300-gene essential table), and
     the packed masks + counts copied to pinned host memory on a second stream (overlapping the next
     chunk's decode). genomes/s = all of that, end to end; the .npy write to disk is excluded.
@@ -441,7 +472,8 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
     from gm2.model import VAE
     G, H, L = a.genes, 512, 32
     torch.manual_seed(0)
-    m = VAE(G, H, L, device=dev, precision=native.GM2_F32)
+    trained = train_v1_checkpoint(a, dev, G, H, L) if a.sample_train_epochs > 0 else None
+    m = trained or VAE(G, H, L, device=dev, precision=native.GM2_F32)
     m.eval()
     chunk = 65536
     n_all = a.sample_genomes
@@ -482,7 +514,7 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
     if dist is not None:
         dist.barrier()
     native.timing_begin(native.KC_MASK)
-    n_split0 = ws.stat(native.STAT_SPLIT_DECODES)
+    st0 = m.decode_stats()
     t0 = time.perf_counter()
     run(True)
     if dist is not None:
@@ -494,16 +526,21 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     gps = n_all / dt
-    # the output layer ran bf16x3 (GM2_OPT_SAMPLE_SPLIT: one bf16 GEMM over the (hi | lo) split operands,
-    # K' = 2H, three MFMAs per fragment pair: hi.hi + hi.lo + lo.hi; MFMA peak bf16)
-    # on every chunk, or the exact-fp32 kernel (fp32 matrix peak)
     n_dec = (n + chunk - 1) // chunk
-    split = ws.stat(native.STAT_SPLIT_DECODES) - n_split0 == n_dec
+    st = {k: v - st0[k] for k, v in m.decode_stats().items()}
+    # per 256 x 256 tile (genomes x genes) the gate ran the bf16x3 split (K' = 2H, three MFMAs per
+    # fragment pair) or, for the blocks whose bound exceeds 2.5e-4, exact fp32 (128 x 128 tiles, four
+    # per block); split_fraction = the share of blocks that ran split
+    blocks = st["split_tiles"] + st["exact_tiles"] / 4.0
+    split_frac = st["split_tiles"] / blocks if blocks else 0.0
+    split = split_frac > 0.5
     kflops = 2.0 * chunk * H * G * (3 if split else 1)  # executed by one full-chunk launch
-    # every decode launches both output-layer kernels and the device runs the one the error bound
-    # picks (the other's grid exits at once): the executed FLOPs of all n genomes over the time of
-    # every mask-kernel launch
-    ach = 2.0 * n * H * G * (3 if split else 1) / (k_ms * 1e-3) / 1e12
+    # both output-layer kernels are launched per decode and each tile runs in the one its block's
+    # verdict picks: executed FLOPs (3 products per split element, 1 per exact element) and useful
+    # FLOPs (1 per element) over the time of every mask-kernel launch, against the bf16 peak when the
+    # split dominates (the exact kernel runs on the fp32 peak)
+    ach = 2.0 * n * H * G * (3 * split_frac + (1 - split_frac)) / (k_ms * 1e-3) / 1e12
+    useful = 2.0 * n * H * G / (k_ms * 1e-3) / 1e12
     peak = PEAK_BF16_TFLOPS if split else PEAK_F32_TFLOPS
     # the packed masks that reached the host are the decode's: spot-check the last chunk on device
     last = (n - 1) // chunk * chunk
@@ -511,6 +548,10 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
     # (the bf16x3 kernel is k_gemm_mask<Cfg<256, ...>, unsigned short, true>, the exact one <..., float>)
     traffic, traffic_src = pmc_traffic(a, "k_gemm_mask<Cfg<256" if split else "k_gemm_mask<Cfg<128")
     return {"genomes_per_s": round(gps, 1), "preset": "v1", "genomes": n_all, "n_gpus": world, "chunk": chunk,
+            "checkpoint": (f"v1 trained {a.sample_train_epochs} epochs (lr 1e-3, batch 4096, L1 0.01) on the synthetic "
+                           f"{a.strains}x{G} matrix" if trained is not None else "untrained (xavier init)"),
+            "split_fraction": round(split_frac, 4), "split_tiles": st["split_tiles"], "exact_tiles": st["exact_tiles"],
+            "band_elements": st["band_elements"], "band_flips": st["band_flips"], "band_overflow": st["band_overflow"],
             "dtype": "bf16x3 (fp32 split hi/lo, output layer) + f32 (hidden layers)" if split else "f32",
             "mask_format": "packed bits (numpy packbits, little)", "includes": "z draw, decode, threshold, pack, "
             "essential-gene counts, D2H of packed masks + counts to pinned host memory",
@@ -519,6 +560,7 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
             "roofline": {"bound": "mfma", "kernel": "k_gemm_mask<bf16, 256x256 pp> (K' = 2H, 3 products)" if split
                          else "k_gemm_mask<f32>", "achieved": round(ach, 2),
                          "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+                         "useful_tflops": round(useful, 2), "useful_frac": round(useful / peak, 4),
                          "flops_per_launch": kflops,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "launch_ms": round(k_ms / max(n_dec, 1), 4), "launches": k_n, "decodes": n_dec}}

@@ -90,11 +90,13 @@ Dims make_dims(const gm2_dims* d, int gpad = kTile) {
 //              gm2_workspace_stat: split tiles, exact tiles, band elements, band flips, band
 //              overflow, decodes with split tiles, decodes without
 //   [16, 48)   split-kernel tiles of this call (sharded), [48, 80) exact-kernel tiles
-//   80         band elements found by this call, 81 bits its recompute flipped
-//   [96, ...)  block maxima of the row norms: activations (roundup(n, 256) / 256), then weights
-// Words [16, 96 + blocks) are zeroed at the start of every gated decode.
+//   [80, 144)  band elements found by this call per list shard, 144 bits its recompute flipped
+//   [160, ...) block maxima of the row norms: activations (roundup(n, 256) / 256), then weights
+// Words [16, 160 + blocks) are zeroed at the start of every gated decode.
 struct DecodeCtl {
-  static constexpr int kCum = 0, kTilesSplit = 16, kTilesExact = 48, kCount = 80, kFlips = 81, kBlk = 96;
+  static constexpr int kCum = 0, kTilesSplit = 16, kTilesExact = 48, kCounts = 80, kFlips = 80 + kBandShards,
+                       kBlk = 160;
+  static_assert(kFlips < kBlk, "control block");
 };
 
 struct Layout {
@@ -196,7 +198,7 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.s3rn = take(split3 ? round_up(Bm, 2 * kTile) * 4 : 0);
   o.s3cn = take(split3 ? round_up(d.G, 2 * kTile) * 4 : 0);
   o.s3ctl = take(split3 ? (DecodeCtl::kBlk + round_up(Bm, 2 * kTile) / 256 + round_up(d.G, 2 * kTile) / 256) * 4 : 0);
-  o.s3band = take(split3 ? (int64_t)kBandCap * 8 : 0);
+  o.s3band = take(split3 ? (int64_t)kBandShards * kBandShardCap * 8 : 0);
   o.adamscal = take(GM2_NUM_SCALARS * 4);
   o.ridx = take(round_up(Bm, 2 * kTile) * 4);
   o.total = cur;
@@ -778,21 +780,27 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
       *fwd_tail = nullptr;
     }
   };
-  // The forward tail in front of dW9 on the side stream (starved beside dA5's workgroups) holds
-  // dW9's start ~30 us past dA5's end, and that delay is what lets the hidden chain's first kernels
-  // take the CUs before dW9's 860 tiles do: behind dW9 instead, dW9 starts at dA5's end and the
-  // chain's first three kernels stretch to 140 + 131 + 165 us (profiles/r04_fwd_tail_after_dw9.txt,
-  // +340 us per traced step). Env GM2_TAIL_AFTER_DW9=1 for A/Bs.
-  static const bool tail_after = [] {
-    const char* e = std::getenv("GM2_TAIL_AFTER_DW9");
-    return e && e[0] == '1';
+  // The output-layer weight gradient (dW9, gradient bucket 0) is ordered on the side stream behind
+  // an explicit point of the main stream's chain: its `dw9_at`-th kernel counted from dA5 (0 = dA5,
+  // 1 = layer 5's BatchNorm backward apply, 2 = the first hidden dX GEMM, ...; env GM2_DW9_AT for
+  // A/Bs). Launched alongside dA5 it would take the CUs dA5 needs; after dA5 its 860 tiles start as
+  // the hidden chain's first kernels do (the chain's head start is the gap dw9_at leaves). The
+  // forward tail (loss slot sums, output bias gradient, norm-ahead header) runs right in front of
+  // it, on CUs dA5 no longer holds. (Rounds 3-4 had the tail in front of dW9 right after the first
+  // fork: starved beside dA5 for ~360 us, it was what held dW9 back; profiles/r04_fwd_tail_after_dw9.txt.)
+  static const int dw9_at = [] {
+    const char* e = std::getenv("GM2_DW9_AT");
+    return e ? std::max(0, std::atoi(e)) : 0;
   }();
   const hipStream_t s9 = sr ? w.s : c.s;
-  {
+  bool dw9_done = false;
+  auto dw9_launch = [&] {
+    if (dw9_done) return;
+    dw9_done = true;
     const GemmArgs<T>& g9 = bg.g9;
     const bool direct9 = plan_gemm<T>(g9).splits == 1;
     fork();
-    if (!tail_after) tail_on(s9);
+    tail_on(s9);
     if (direct9) {
       // (A5^T here on the side stream; on the main stream before the fork measured ~35 us/step
       // slower, profiles/r02_a5t_placement_ab.txt)
@@ -801,9 +809,12 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     } else {
       gemm_to<T>(w, c.t(l.dL), Gp, Gp, c.t(l.A[5]), H, H, G, H, Bp, gr + d.off[D9W], nullptr, 0, H, 0, 0);
     }
-    if (tail_after) tail_on(s9);  // (the output bias gradient: bucket 0 as well)
     if (st.opt.grad_buckets) HIP_OK(hipEventRecord(st.bucket[0], s9));
-  }
+  };
+  int chain_pos = 0;
+  auto chain_mark = [&] {  // after each kernel of the main stream's chain
+    if (chain_pos++ == dw9_at) dw9_launch();
+  };
   // dA_j = dY . W (K-major dY, MN-major W) into the slab area; when the plan allows, the GEMM's
   // epilogue also takes BatchNorm j's backward partials (sum do, sum (y-mean) do)
   bool have_part = false;
@@ -823,6 +834,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     return have_part ? 1 : gemm_to_slabs<T>(c, dY, lddy, Bp, W, ldw, H, B, H, K, H, 1, 0);
   };
   int S = dx_pre_bn(c.t(l.dL), Gp, c.t(l.sD3), H, Gp, 5);
+  chain_mark();
   const int64_t shadow_w[6] = {l.sE0, l.sE1, l.sE2, l.sD0, l.sD1, l.sD2};
   for (int i = 5; i >= 0; --i) {
     const int64_t slab = (int64_t)Bp * H;
@@ -845,11 +857,13 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
                            c.f(l.save[i]), prm + d.off[kBlk[i][2]], prm + d.off[kBlk[i][3]], gr + d.off[kBlk[i][2]],
                            gr + d.off[kBlk[i][3]], c.t(l.dY[i]), colp, c.s, sync ? syncb : nullptr,
                            dyt ? c.t(l.dYT0) : nullptr, Bp);
+    chain_mark();
     const bool hold = i >= hold_from;
     fork_flush(hold);
     side_work(hold, [&, colp, i] { launch_colsum(colp, Bp / 64, H, H, gr + d.off[kBlk[i][1]], nullptr, 0, w.s); });
     const T* dY = c.t(l.dY[i]);
     if (i == 0) {  // input layer: weight gradient only (on the main stream: nothing left to overlap)
+      dw9_launch();  // (a dw9_at past the chain's end: here, beside dWe0)
       // dWe0[h][g] = sum_b dY0^T[h][b] X[b][g]: dY0^T (K-major copy) x X (MN-major)
       if (!dyt) launch_transpose<T>(dY, H, Bp, H, c.t(l.dYT0), Bp, c.s);
       // bucket 1 (every hidden-layer weight gradient) is final when the side stream's queue so far
@@ -907,12 +921,14 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
                    0, 0);
       });
       S = dx_pre_bn(c.t(l.dH), L2r, c.t(l.sHD), H, (int)d.K2L, 2);
+      chain_mark();
       continue;
     }
     side_work(hold, [&, dY, i] {
       gemm_to<T>(w, dY, H, H, c.t(l.A[i - 1]), H, H, H, H, Bp, gr + d.off[kBlk[i][0]], nullptr, 0, H, 0, 0);
     });
     S = dx_pre_bn(dY, H, c.t(shadow_w[i]), H, H, i - 1);
+    chain_mark();
   }
 }
 
@@ -970,18 +986,18 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
   // and the fp32 accumulation of its 3H products, exact tiles the fp32 accumulation of H products;
   // both, the reference's own fp32 accumulation of H products
   const double gH = band_gamma((double)H), g3H = band_gamma(3.0 * H);
-  const MaskBand bs{rn, cn, (float)(kSplitUnit * 1.01 + g3H + gH), ctl + DecodeCtl::kCount, list, kBandCap};
-  const MaskBand be{rn, cn, (float)(2.0 * gH), ctl + DecodeCtl::kCount, list, kBandCap};
+  const MaskBand bs{rn, cn, (float)(kSplitUnit * 1.01 + g3H + gH), ctl + DecodeCtl::kCounts, list, kBandShardCap};
+  const MaskBand be{rn, cn, (float)(2.0 * gH), ctl + DecodeCtl::kCounts, list, kBandShardCap};
   GemmArgs<bf16_t> g{a3, 2 * H, w3, 2 * H, n, G, 2 * H, Bq, Gq, 0};
   launch_gemm_mask<bf16_t>(g, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
                            true, MaskGate{ablk, wblk, 1, ctl + DecodeCtl::kTilesSplit}, bs);
   GemmArgs<float> ge{c.f(l.A[5]), H, c.f(l.sD3), H, n, G, H, (int)round_up(n, kTile), (int)d.Gp, 0};
   launch_gemm_mask<float>(ge, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
                           false, MaskGate{ablk, wblk, 2, ctl + DecodeCtl::kTilesExact}, be);
-  launch_band_fix(list, ctl + DecodeCtl::kCount, kBandCap, c.f(l.A[5]), H, w9, H, prm + d.off[D9B], H, bits, ldb, mask,
-                  ldm, ctl + DecodeCtl::kFlips, c.s);
-  launch_decode_stats(ctl + DecodeCtl::kTilesSplit, ctl + DecodeCtl::kTilesExact, ctl + DecodeCtl::kCount,
-                      ctl + DecodeCtl::kFlips, kBandCap, (unsigned long long*)(ctl + DecodeCtl::kCum), c.s);
+  launch_band_fix(list, ctl + DecodeCtl::kCounts, kBandShardCap, c.f(l.A[5]), H, w9, H, prm + d.off[D9B], H, bits, ldb,
+                  mask, ldm, ctl + DecodeCtl::kFlips, c.s);
+  launch_decode_stats(ctl + DecodeCtl::kTilesSplit, ctl + DecodeCtl::kTilesExact, ctl + DecodeCtl::kCounts,
+                      ctl + DecodeCtl::kFlips, kBandShardCap, (unsigned long long*)(ctl + DecodeCtl::kCum), c.s);
   return true;
 }
 

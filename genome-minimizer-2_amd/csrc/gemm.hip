@@ -589,14 +589,20 @@ __device__ __forceinline__ double sq4(float a, float b, float c, float d) {
   return ((double)a * a + (double)b * b) + ((double)c * c + (double)d * d);
 }
 
-template <class C, typename T, bool AK, bool BK, bool PP, int IDX>
+template <class C, typename T, bool AK, bool BK, bool PP, int IDX, int EPI>
 __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g, float* __restrict__ C0,
                                            float* __restrict__ C1, int msplit, int64_t ldc, int64_t slab,
                                            const float* __restrict__ bias, const StoreEpi& bn, char* smem);
 
 // IDX (zero-copy rows, PP only): 1 = P's rows through g.prow, 2 = Q's k-rows through g.qrow; the
 // tile's slice of the index array sits in an LDS table after the staging ring
-template <class C, typename T, bool AK, bool BK, bool PP, int IDX = 0>
+// EPI (the epilogue, fixed at compile time for the 256x256 kernels so each instantiation carries only
+// its own store code: with the general one every 256x256 kernel spilled 12-21 VGPRs, with these
+// none): 0 = general (bias, BatchNorm statistics, row split, unaligned rows, transposed store),
+// 1 = plain fp32 store (split-K slabs or one pass, rows aligned or not, optional per-tile sums of
+// squares), 2 = the transposed store straight from the accumulators (+ sums of squares), 3 = the
+// transposed store through the LDS image (+ sums of squares)
+template <class C, typename T, bool AK, bool BK, bool PP, int IDX = 0, int EPI = 0>
 __global__ __launch_bounds__(C::NT, C::MINW) void k_gemm_store(GemmArgs<T> g, float* __restrict__ C0, float* __restrict__ C1,
                                                     int msplit, int64_t ldc, int64_t slab,
                                                     const float* __restrict__ bias, StoreEpi bn) {
@@ -604,7 +610,7 @@ __global__ __launch_bounds__(C::NT, C::MINW) void k_gemm_store(GemmArgs<T> g, fl
   GM2_STAMP(0);
   const int tm = g.Mp / C::BM, tn = g.Np / C::BN;
   if (bn.ntiles == 0) {  // one tile per workgroup
-    store_tile<C, T, AK, BK, PP, IDX>(tile_of<C>(tm, tn), g, C0, C1, msplit, ldc, slab, bias, bn, smem);
+    store_tile<C, T, AK, BK, PP, IDX, EPI>(tile_of<C>(tm, tn), g, C0, C1, msplit, ldc, slab, bias, bn, smem);
     return;
   }
   // capped grid (one K pass): workgroup wg takes logical tiles wg, wg + grid, ... (every wave of
@@ -612,15 +618,19 @@ __global__ __launch_bounds__(C::NT, C::MINW) void k_gemm_store(GemmArgs<T> g, fl
   const int ntile = tm * tn;
   for (int t = xcd_wg(); t < bn.ntiles; t += gridDim.x) {
     __syncthreads();
-    store_tile<C, T, AK, BK, PP, IDX>(tile_at<C>(t % ntile, tm, tn, t / ntile), g, C0, C1, msplit, ldc, slab, bias,
+    store_tile<C, T, AK, BK, PP, IDX, EPI>(tile_at<C>(t % ntile, tm, tn, t / ntile), g, C0, C1, msplit, ldc, slab, bias,
                                       bn, smem);
   }
 }
 
-template <class C, typename T, bool AK, bool BK, bool PP, int IDX>
+template <class C, typename T, bool AK, bool BK, bool PP, int IDX, int EPI>
 __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g, float* __restrict__ C0,
                                            float* __restrict__ C1, int msplit, int64_t ldc, int64_t slab,
-                                           const float* __restrict__ bias, const StoreEpi& bn, char* smem) {
+                                           const float* __restrict__ bias_in, const StoreEpi& bn, char* smem) {
+  // (the specialised epilogues: their options fixed, so the general code below folds away)
+  const float* __restrict__ bias = EPI == 0 ? bias_in : nullptr;
+  const int bmode = EPI == 0 ? bn.mode : 0;
+  const int btrans = EPI == 0 ? bn.trans : EPI >= 2;
   const int kbeg = tl.split * g.k_per_split;
   const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = (kend - kbeg) / E<T>::KT;
@@ -653,10 +663,10 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
   // BN + 4 floats: the accumulator writes of lanes 16 apart land 16 banks apart), then store whole
   // rows with 16-byte stores (4 columns per thread; scalar where C's rows are not 16-B aligned or
   // at the N edge).
-  // Transposed store (bn.trans): 16 lanes write 4 consecutive m each of one column n (256
+  // Transposed store (btrans): 16 lanes write 4 consecutive m each of one column n (256
   // contiguous bytes of C^T's row n), reading the image down a column (odd pitch: conflict-free).
   float* img = (float*)smem;
-  const int pitch = bn.trans ? C::BN + 1 : C::BN + 4;
+  const int pitch = btrans ? C::BN + 1 : C::BN + 4;
   constexpr int BR = 64, NBANDS = C::BM / BR, BPW = C::WTM / BR;  // bands, bands per wave row
   static_assert(BR * (C::BN + 4) * 4 <= C::LDS, "epilogue band must fit the staging LDS");
   constexpr int TPR = C::BN / 4, RPI = C::NT / TPR;  // threads per row, rows per pass
@@ -668,7 +678,7 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
   // row m's elements go into the image shifted by e_m = (address of (m, n0) in floats) % 4, so
   // every image chunk of 4 is one aligned 16-B global chunk; only the two end chunks of a row are
   // partial. e_m depends on the row only through m % 4 (j of the accumulator layout).
-  const bool shiftvec = !vec && slab == 0 && !bias && bn.mode == 0 && !bn.trans && msplit >= g.M &&
+  const bool shiftvec = !vec && slab == 0 && !bias && bmode == 0 && !btrans && msplit >= g.M &&
                         (((uintptr_t)C0) & 3) == 0;
   const int e_base = (int)(((uintptr_t)(C0 + (int64_t)tl.m0 * ldc + tl.n0) >> 2) & 3), l3 = (int)(ldc & 3);
   float bb[4], sa[4], sb[4], sh[4], bmean[4], balpha[4], bbeta[4];
@@ -677,14 +687,43 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
   for (int u = 0; u < 4; ++u) {
     bb[u] = (bias && n + u < g.N) ? bias[n + u] : 0.f;
     sa[u] = sb[u] = sh[u] = bmean[u] = balpha[u] = bbeta[u] = 0.f;
-    if (bn.mode == 2 && n + u < g.N) {
+    if (bmode == 2 && n + u < g.N) {
       bmean[u] = bn.save[n + u];
       balpha[u] = bn.save[bn.H + n + u] * bn.gamma[n + u];
       bbeta[u] = fmaf(-bmean[u], balpha[u], bn.beta[n + u]);
     }
   }
+  // Transposed store straight from the accumulators (bn.trans_direct): lane l of fragment (mi, ni)
+  // holds rows m .. m + 3 (j) of column n, i.e. 16 contiguous bytes of C^T's row n -- one 16-B store
+  // per fragment, no LDS image and no barriers (each instruction writes 16 rows x 64 B; the L2 merges
+  // the two halves of each 128-B line, written by consecutive fragments)
+  const bool direct = EPI == 2;
+  if (direct) {
+#pragma unroll
+    for (int mi = 0; mi < C::FM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < C::FN; ++ni) {
+        const int nn = tl.n0 + wn * C::WTN + ni * 16 + (lane & 15);
+        const int m = tl.m0 + wm * C::WTM + mi * 16 + 4 * (lane >> 4);
+        if (nn >= g.N) continue;
+        const f32x4 v = acc[mi][ni];
+        float* dst = C0 + (int64_t)nn * ldc + m;
+        if (m + 3 < g.M) {
+          *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+          sqa += sq4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (m + u < g.M) {
+              dst[u] = v[u];
+              sqa += (double)v[u] * v[u];
+            }
+        }
+      }
+  }
 #pragma unroll
   for (int h = 0; h < NBANDS; ++h) {
+    if (direct) break;
     if (wm == h / BPW) {
       const int mi0 = (h % BPW) * (BR / 16);
 #pragma unroll
@@ -697,7 +736,7 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
                 (shiftvec ? (e_base + j * l3) & 3 : 0)] = acc[mi0 + mi][ni][j];
     }
     __syncthreads();
-    if (bn.trans) {
+    if (btrans) {
       const int q = threadIdx.x & 15;
       const int m = tl.m0 + h * BR + 4 * q;
       for (int c = threadIdx.x >> 4; c < C::BN; c += C::NT / 16) {
@@ -722,7 +761,7 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
       __syncthreads();
       continue;
     }
-    if (h == 0 && bn.mode == 1) {  // shift = the tile's first row (always < M)
+    if (h == 0 && bmode == 1) {  // shift = the tile's first row (always < M)
 #pragma unroll
       for (int u = 0; u < 4; ++u) sh[u] = img[cq + u] + bb[u];
     }
@@ -759,7 +798,7 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
       }
       const float4 w = *(const float4*)(img + r * pitch + cq);
       const float v[4] = {w.x + bb[0], w.y + bb[1], w.z + bb[2], w.w + bb[3]};
-      float* dst = (m < msplit ? Cz + (int64_t)m * ldc : C1 + (int64_t)(m - msplit) * ldc) + n;
+      float* dst = (EPI != 0 || m < msplit ? Cz + (int64_t)m * ldc : C1 + (int64_t)(m - msplit) * ldc) + n;
       if (vec && n + 3 < g.N) {
         *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
         sqa += sq4(v[0], v[1], v[2], v[3]);
@@ -771,14 +810,14 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
             sqa += (double)v[u] * v[u];
           }
       }
-      if (bn.mode == 1) {
+      if (bmode == 1) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const float dv = v[u] - sh[u];
           sa[u] += dv;
           sb[u] = fmaf(dv, dv, sb[u]);
         }
-      } else if (bn.mode == 2) {
+      } else if (bmode == 2) {
         const float4 y4 = *(const float4*)(bn.Y + (int64_t)m * bn.ldy + n);
         const float y[4] = {y4.x, y4.y, y4.z, y4.w};
 #pragma unroll
@@ -791,7 +830,7 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
     }
     __syncthreads();
   }
-  if (bn.mode) {  // (bn mode: N % 4 == 0, one K pass, 128-row tiles -- checked on the host)
+  if (bmode) {  // (bn mode: N % 4 == 0, one K pass, 128-row tiles -- checked on the host)
     float4* red = (float4*)smem;
     red[2 * threadIdx.x] = make_float4(sa[0], sa[1], sa[2], sa[3]);
     red[2 * threadIdx.x + 1] = make_float4(sb[0], sb[1], sb[2], sb[3]);
@@ -809,7 +848,7 @@ __device__ __forceinline__ void store_tile(const TileXY tl, const GemmArgs<T>& g
       const float nr = (float)min(C::BM, g.M - tl.m0);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (bn.mode == 1) {
+        if (bmode == 1) {
           const float dm = av[u] / nr;
           o[u] = make_float2(sh[u] + dm, fmaxf(fmaf(-av[u], dm, qv[u]), 0.f));
         } else {
@@ -1094,14 +1133,11 @@ __device__ __forceinline__ void recon_loss_tile(const TileXY tl, const GemmArgs<
   const float wgam = scal[kScalWGamma];
   float bce = 0.f, psum = 0.f;
   T* img = (T*)smem;  // LDS image [BN strains][BM genes + 8] of T
-  // the gene-abundance term (w*gamma != 0, presets v1-v3) adds one FMA per element: a uniform
-  // branch between the two element loops
-  if (wgam != 0.f)
-    recon_tile<C, T, FAST, true, GRAD>(acc, xbits + ((tl.m0 + wm * C::WTM) >> 5), ldxb, bias_s, g.N, tl.n0, wm, wn, q,
-                                       c, wgam, img, bce, psum, xrows ? xidx : nullptr);
-  else
-    recon_tile<C, T, FAST, false, GRAD>(acc, xbits + ((tl.m0 + wm * C::WTM) >> 5), ldxb, bias_s, g.N, tl.n0, wm, wn,
-                                        q, c, wgam, img, bce, psum, xrows ? xidx : nullptr);
+  // (one element loop with the gene-abundance FMA for every preset: at w*gamma = 0 it leaves dl bit
+  // for bit as it was, costs half a packed FMA per element, and keeps the kernel to one copy of the
+  // loop -- with a second, FMA-free copy behind a uniform branch it spilled 42 VGPRs, with one 4)
+  recon_tile<C, T, FAST, true, GRAD>(acc, xbits + ((tl.m0 + wm * C::WTM) >> 5), ldxb, bias_s, g.N, tl.n0, wm, wn, q, c,
+                                     wgam, img, bce, psum, xrows ? xidx : nullptr);
   if constexpr (FAST) bce *= -0.6931471805599453f;
   GM2_STAMP(4);
   if constexpr (GRAD) {
@@ -1209,9 +1245,32 @@ __device__ __forceinline__ void band_stage(const MaskBand& b, const TileXY& tl, 
     brn[i] = i < C::BM ? b.rn[tl.m0 + i] : b.cn[tl.n0 + i - C::BM];
 }
 
-__device__ __forceinline__ void band_push(const MaskBand& b, int r, int gcol) {
-  const unsigned slot = atomicAdd(b.count, 1u);
-  if (slot < b.cap) b.list[slot] = make_uint2((unsigned)r, (unsigned)gcol);
+// one wave's band elements: the wave's total reserved by one atomic on its shard's counter, then
+// each lane writes its elements at its prefix offset (push(i) walks the same elements in the same
+// order in both passes)
+template <class F>
+__device__ __forceinline__ void band_append(const MaskBand& b, int lane, F&& walk) {
+  unsigned mine = 0;
+  walk([&](bool in, int, int) { mine += in ? 1u : 0u; });
+  unsigned tot = mine, pre = 0;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {  // inclusive scan over the wave
+    const unsigned v = __shfl_up(tot, o, 64);
+    if (lane >= o) tot += v;
+  }
+  pre = tot - mine;
+  const unsigned wtot = __shfl(tot, 63, 64);
+  const int sh = blockIdx.x % kBandShards;
+  unsigned base = 0;
+  if (lane == 0) base = atomicAdd(b.counts + sh, wtot);
+  base = __shfl(base, 0, 64) + pre;
+  uint2* list = b.list + (size_t)sh * b.cap;
+  walk([&](bool in, int r, int gcol) {
+    if (in) {
+      if (base < b.cap) list[base] = make_uint2((unsigned)r, (unsigned)gcol);
+      ++base;
+    }
+  });
 }
 
 // PP: the 256x256 bf16 ping-pong main loop in its S3 form (the bf16x3 sampling decode: hi.hi +
@@ -1271,20 +1330,22 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
           __builtin_amdgcn_sched_barrier(0);  // (one row quad at a time: the ballots' SGPR pairs stay few)
         }
       }
-      if (__ballot(anyb)) {  // (rare) append this wave's band elements (unrolled: acc stays in registers)
+      if (__ballot(anyb)) {  // append this wave's band elements (unrolled: acc stays in registers)
+        band_append(o.band, lane, [&](auto&& visit) {
 #pragma unroll
-        for (int mi = 0; mi < C::FM; ++mi)
+          for (int mi = 0; mi < C::FM; ++mi)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int r = tl.m0 + wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
-            const float raj = brn[r - tl.m0];
+            for (int j = 0; j < 4; ++j) {
+              const int r = tl.m0 + wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
+              const float raj = brn[r - tl.m0];
 #pragma unroll
-            for (int ni = 0; ni < C::FN; ++ni) {
-              const float l = acc[mi][ni][j] + bnv[ni];
-              if (fabsf(l - kMaskLogitThreshold) <= raj * ce[ni] && r < g.M)
-                band_push(o.band, r, tl.n0 + wn * C::WTN + ni * 16 + (lane & 15));
+              for (int ni = 0; ni < C::FN; ++ni) {
+                const float l = acc[mi][ni][j] + bnv[ni];
+                visit(fabsf(l - kMaskLogitThreshold) <= raj * ce[ni] && r < g.M, r,
+                      tl.n0 + wn * C::WTN + ni * 16 + (lane & 15));
+              }
             }
-          }
+        });
       }
       __syncthreads();
       constexpr int BPR = C::BN / 8;
@@ -1332,18 +1393,20 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
       }
     }
   }
-  if (bchk && __ballot(anyb)) {  // (rare) append this wave's band elements (unrolled: acc stays in registers)
+  if (bchk && __ballot(anyb)) {  // append this wave's band elements (unrolled: acc stays in registers)
+    band_append(o.band, lane, [&](auto&& visit) {
 #pragma unroll
-    for (int mi = 0; mi < C::FM; ++mi)
+      for (int mi = 0; mi < C::FM; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < C::FN; ++ni)
+        for (int ni = 0; ni < C::FN; ++ni)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int ml = wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
-          const float l = acc[mi][ni][j] + bnv[ni];
-          if (fabsf(l - kMaskLogitThreshold) <= brn[ml] * ce[ni] && tl.m0 + ml < g.M)
-            band_push(o.band, tl.m0 + ml, tl.n0 + wn * C::WTN + ni * 16 + (lane & 15));
-        }
+          for (int j = 0; j < 4; ++j) {
+            const int ml = wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
+            const float l = acc[mi][ni][j] + bnv[ni];
+            visit(fabsf(l - kMaskLogitThreshold) <= brn[ml] * ce[ni] && tl.m0 + ml < g.M, tl.m0 + ml,
+                  tl.n0 + wn * C::WTN + ni * 16 + (lane & 15));
+          }
+    });
   }
   __syncthreads();
   const int rows = min(C::BM, g.M - tl.m0);
@@ -1553,7 +1616,7 @@ static int device_cus() {
   return cus[dev] = std::max(n, 1);
 }
 
-template <class C, typename T, bool AK, bool BK, bool PP, int IDX = 0>
+template <class C, typename T, bool AK, bool BK, bool PP, int IDX = 0, int EPI = 0>
 static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
                            const float* bias, const StoreEpi& bn, hipStream_t s) {
   // (zero-copy rows: the index table after the staging ring -- a tile's rows, or a split's k-rows)
@@ -1562,7 +1625,7 @@ static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1
   const int lds = C::LDS + (IDX == 1 ? C::BM * 4 : IDX == 2 ? a.k_per_split * 4 : 0);
   if (lds > 160 * 1024) throw Gm2Error("gemm: %d bytes of LDS", lds);
   if (IDX == 2 && a.k_per_split > kMaxIdxRows) throw Gm2Error("zero-copy rows: %d k-rows per split", a.k_per_split);
-  ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP, IDX>, C::LDS + table_max);
+  ensure_lds_attr((const void*)k_gemm_store<C, T, AK, BK, PP, IDX, EPI>, C::LDS + table_max);
   int grid = tiles;
   StoreEpi ep = bn;
   if (bn.ntiles) {  // capped grid: the same number of rounds on fewer CUs
@@ -1570,8 +1633,34 @@ static void store_launch_k(const GemmArgs<T>& a, int tiles, float* C0, float* C1
     grid = (tiles + rounds - 1) / rounds;
     ep.ntiles = grid < tiles ? tiles : 0;
   }
-  hipLaunchKernelGGL((k_gemm_store<C, T, AK, BK, PP, IDX>), dim3(grid), dim3(C::NT), lds, s, a, C0, C1 ? C1 : C0,
+  hipLaunchKernelGGL((k_gemm_store<C, T, AK, BK, PP, IDX, EPI>), dim3(grid), dim3(C::NT), lds, s, a, C0, C1 ? C1 : C0,
                      C1 ? msplit : (1 << 30), ldc, slab, bias, ep);
+}
+
+// the specialised epilogue a 256x256 launch can take (k_gemm_store EPI): 1 = plain fp32 store,
+// 2 = transposed straight from the accumulators (env GM2_TRANS_DIRECT=1, A/B), 3 = transposed
+// through LDS, 0 = general
+static int store_epi(const GemmArgs<bf16_t>& a, float* C0, float* C1, int msplit, int64_t ldc, int64_t slab,
+                     const float* bias, const StoreEpi& bn) {
+  static const bool trans_direct = [] {
+    const char* e = std::getenv("GM2_TRANS_DIRECT");
+    return e && e[0] == '1';
+  }();
+  const bool aligned = ((ldc | slab) & 3) == 0 && (((uintptr_t)C0) & 15) == 0;
+  if (bias || bn.mode || (C1 && msplit < a.M)) return 0;
+  if (bn.trans) return aligned ? (trans_direct ? 2 : 3) : 0;
+  return 1;
+}
+
+template <class C, typename T, bool AK, bool BK, bool PP, int IDX>
+static void store_launch_epi(const GemmArgs<T>& a, int tiles, float* C0, float* C1, int msplit, int64_t ldc,
+                             int64_t slab, const float* bias, const StoreEpi& bn, hipStream_t s) {
+  switch (store_epi(a, C0, C1, msplit, ldc, slab, bias, bn)) {
+    case 1: return store_launch_k<C, T, AK, BK, PP, IDX, 1>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+    case 2: return store_launch_k<C, T, AK, BK, PP, IDX, 2>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+    case 3: return store_launch_k<C, T, AK, BK, PP, IDX, 3>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+    default: return store_launch_k<C, T, AK, BK, PP, IDX, 0>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+  }
 }
 
 template <class C, typename T, bool AK, bool BK>
@@ -1581,14 +1670,14 @@ static void store_launch(const GemmArgs<T>& a, int tiles, float* C0, float* C1, 
     if (a.prow || a.qrow) {  // zero-copy rows: the input layer's two GEMMs (gemm_idx_ok checked)
       if (!pp_enabled()) throw Gm2Error("zero-copy rows need the ping-pong main loop");
       if constexpr (AK && BK) {
-        if (a.prow && !a.qrow) return store_launch_k<C, T, AK, BK, true, 1>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+        if (a.prow && !a.qrow) return store_launch_epi<C, T, AK, BK, true, 1>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
       }
       if constexpr (AK && !BK) {
-        if (a.qrow && !a.prow) return store_launch_k<C, T, AK, BK, true, 2>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+        if (a.qrow && !a.prow) return store_launch_epi<C, T, AK, BK, true, 2>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
       }
       throw Gm2Error("zero-copy rows: layout not instantiated");
     }
-    if (pp_enabled()) return store_launch_k<C, T, AK, BK, true>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
+    if (pp_enabled()) return store_launch_epi<C, T, AK, BK, true, 0>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
   }
   if (a.prow || a.qrow) throw Gm2Error("zero-copy rows: bf16 256x256 tiles only");
   store_launch_k<C, T, AK, BK, false>(a, tiles, C0, C1, msplit, ldc, slab, bias, bn, s);
@@ -1661,6 +1750,7 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
   StoreEpi ep;
   ep.trans = 1;
   ep.sq = sq;
+
   ep.ntiles = grid_cap_bits() & 1;  // dW9 bit (the launcher sets the count)
   if constexpr (sizeof(T) == 2) {
     if (use_big(g)) {
@@ -1788,7 +1878,7 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
     throw Gm2Error("mask bits: row pitch %lld must be a multiple of 16 bytes covering the padded genes", (long long)ldb);
   if (counts && (!xbits || ldxb * 32 < g.Np)) throw Gm2Error("mask counts: target bits required");
   MaskOut o{mask, ldm, bits, ldb, probs, ldpr, counts, xbits, ldxb, thr, gate, band};
-  if (band.rn && (!band.cn || !band.count || !band.list || thr != 0.5f))
+  if (band.rn && (!band.cn || !band.counts || !band.list || !band.cap || thr != 0.5f))
     throw Gm2Error("mask band: norms, counter and list required (threshold 0.5 only)");
   const int band_lds = band.rn ? (big ? 512 : 256) * 4 : 0;  // (row + column norms past the staging ring)
   TimedLaunch tl(kKcMask, s);

@@ -207,30 +207,34 @@ __device__ __forceinline__ bool split_tile_ok(const MaskGate& g, int m0, int n0)
 }
 // The certified band of the sampling decode (SURVEY.md 7 "Hard parts" (ii)): logits with
 // |l - T| <= coef * ||a_r|| * ||w_g|| (T = the mask threshold) may sit on either side of T in the
-// reference's own fp32 arithmetic; the mask epilogues append those (row, gene) pairs to `list`
-// (count = entries found, capacity cap: the rest only counted), and k_band_fix recomputes each one's
-// logit in fp64 from the same fp32 activations / weights and sets its mask bit from that.
+// reference's own fp32 arithmetic; the mask epilogues append those (row, gene) pairs to a band list
+// and k_band_fix recomputes each one's logit in fp64 from the same fp32 activations / weights and
+// sets its mask bit from that.
 //   coef (split tiles) = kSplitUnit * 1.01 + gamma_3H + gamma_H: the split's own error, its fp32
 //     accumulation of 3H products and the reference's fp32 accumulation of H products
 //   coef (exact tiles) = 2 gamma_H (gamma_n = n u / (1 - n u), u = 2^-24)
+// The list is kBandShards shards of `cap` entries (shard = blockIdx % kBandShards, each with its own
+// counter: one atomic per wave per tile, not per element, and 64 counter words instead of one);
+// entries past a shard's capacity are only counted (left as the kernel decided them).
+constexpr int kBandShards = 64;
+constexpr unsigned kBandShardCap = 1u << 16;  // entries per shard per decode call (64 x 64 K x 8 B = 32 MB)
 struct MaskBand {
   const float* rn = nullptr;  // ||a_r|| per genome row (nullptr: no band check)
   const float* cn = nullptr;  // ||w_g|| per gene
   float coef = 0.f;
-  unsigned* count = nullptr;
-  uint2* list = nullptr;      // (row, gene)
+  unsigned* counts = nullptr; // [kBandShards]
+  uint2* list = nullptr;      // [kBandShards][cap] (row, gene)
   unsigned cap = 0;
 };
 inline double band_gamma(double n) { return n * 0x1p-24 / (1.0 - n * 0x1p-24); }
-constexpr unsigned kBandCap = 1u << 22;  // band list entries per decode call (32 MB)
-// k_band_fix over list[0 .. min(count, cap)): fp64 logit of (A[row], W[gene]) + bias, mask bit =
+// k_band_fix over every shard's entries: fp64 logit of (A[row], W[gene]) + bias, mask bit =
 // (float)logit > T (the correctly rounded fp32 logit against the reference's threshold); packed
-// bits (bits != nullptr) or u8 mask. ctl: the decode's per-call counters (api.hip DecodeCtl)
-void launch_band_fix(const uint2* list, const unsigned* count, unsigned cap, const float* A, int64_t lda,
+// bits (bits != nullptr) or u8 mask. flips: the bits it changed
+void launch_band_fix(const uint2* list, const unsigned* counts, unsigned cap, const float* A, int64_t lda,
                      const float* W, int64_t ldw, const float* bias, int H, uint8_t* bits, int64_t ldb, uint8_t* mask,
                      int64_t ldm, unsigned* flips, hipStream_t s);
 // one workgroup: the decode call's per-call counters -> the workspace's cumulative ones (DecodeCtl)
-void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* count,
+void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* counts,
                          const unsigned* flips, unsigned cap, unsigned long long* cum, hipStream_t s);
 
 // output layer + threshold (sampling / metrics): u8 mask, packed bits, probs, per-row (TP, FP, FN).

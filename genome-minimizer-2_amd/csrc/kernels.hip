@@ -1198,15 +1198,20 @@ __global__ __launch_bounds__(256) void k_exchange_unpack(const bf16_t* __restric
 // Packed bits are set / cleared with 32-bit atomics (several waves may share a word), u8 masks by
 // byte stores. flips counts the bits the recompute changed.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_band_fix(const uint2* __restrict__ list, const unsigned* __restrict__ count,
+__global__ __launch_bounds__(256) void k_band_fix(const uint2* __restrict__ list, const unsigned* __restrict__ counts,
                                                 unsigned cap, const float* __restrict__ A, int64_t lda,
                                                 const float* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
                                                 int H, uint8_t* bits, int64_t ldb, uint8_t* mask, int64_t ldm,
                                                 unsigned* flips) {
-  const unsigned n = min(*count, cap);
+  // wave w takes shard w % kBandShards, its entries w / kBandShards, + waves / kBandShards, ...
   const int lane = threadIdx.x & 63;
-  for (unsigned e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4) {
-    const uint2 rg = list[e];
+  const unsigned wave = blockIdx.x * 4 + (threadIdx.x >> 6), waves = gridDim.x * 4;
+  const int sh = wave % kBandShards;
+  const unsigned per = waves / kBandShards;
+  const unsigned n = min(counts[sh], cap);
+  const uint2* sl = list + (size_t)sh * cap;
+  for (unsigned e = wave / kBandShards; e < n; e += per) {
+    const uint2 rg = sl[e];
     const float* a = A + (int64_t)rg.x * lda;
     const float* w = W + (int64_t)rg.y * ldw;
     double acc = 0.0;
@@ -1235,23 +1240,26 @@ __global__ __launch_bounds__(256) void k_band_fix(const uint2* __restrict__ list
 // list's capacity (left as the kernels decided them), [5] decodes with split tiles, [6] without
 __global__ __launch_bounds__(64) void k_decode_stats(const unsigned* __restrict__ tiles_split,
                                                      const unsigned* __restrict__ tiles_exact,
-                                                     const unsigned* __restrict__ count,
+                                                     const unsigned* __restrict__ counts,
                                                      const unsigned* __restrict__ flips, unsigned cap,
                                                      unsigned long long* cum) {
   const int t = threadIdx.x;
   unsigned long long a = t < kSplitShards ? tiles_split[t] : 0ull, b = t < kSplitShards ? tiles_exact[t] : 0ull;
+  const unsigned c = t < kBandShards ? counts[t] : 0u;
+  unsigned long long found = c, over = c > cap ? c - cap : 0u;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     a += __shfl_xor(a, o, 64);
     b += __shfl_xor(b, o, 64);
+    found += __shfl_xor(found, o, 64);
+    over += __shfl_xor(over, o, 64);
   }
   if (t == 0) {
-    const unsigned c = *count;
     cum[0] += a;
     cum[1] += b;
-    cum[2] += c;
+    cum[2] += found;
     cum[3] += *flips;
-    cum[4] += c > cap ? c - cap : 0u;
+    cum[4] += over;
     cum[a ? 5 : 6] += 1;
   }
 }
@@ -1464,20 +1472,22 @@ void launch_exchange_unpack(const bf16_t* in, int64_t n, float* x, hipStream_t s
   GM2_CHECK_LAUNCH();
 }
 
-void launch_band_fix(const uint2* list, const unsigned* count, unsigned cap, const float* A, int64_t lda,
+void launch_band_fix(const uint2* list, const unsigned* counts, unsigned cap, const float* A, int64_t lda,
                      const float* W, int64_t ldw, const float* bias, int H, uint8_t* bits, int64_t ldb, uint8_t* mask,
                      int64_t ldm, unsigned* flips, hipStream_t s) {
   if ((!bits && !mask) || (bits && (ldb & 3)))
     throw Gm2Error("band fix: an output (packed bits with 4-B aligned rows, or a u8 mask) is required");
-  // (a fixed grid: the count lives on the device; each wave takes entries e, e + 4 * grid, ...)
-  hipLaunchKernelGGL(k_band_fix, dim3(1024), dim3(256), 0, s, list, count, cap, A, lda, W, ldw, bias, H, bits, ldb,
+  // (a fixed grid, the counts live on the device: 16 waves per shard)
+  static_assert((1024 * 4) % kBandShards == 0, "band fix grid");
+  hipLaunchKernelGGL(k_band_fix, dim3(1024), dim3(256), 0, s, list, counts, cap, A, lda, W, ldw, bias, H, bits, ldb,
                      mask, ldm, flips);
   GM2_CHECK_LAUNCH();
 }
 
-void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* count,
+void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* counts,
                          const unsigned* flips, unsigned cap, unsigned long long* cum, hipStream_t s) {
-  hipLaunchKernelGGL(k_decode_stats, dim3(1), dim3(64), 0, s, tiles_split, tiles_exact, count, flips, cap, cum);
+  static_assert(kSplitShards <= 64 && kBandShards <= 64, "one wave");
+  hipLaunchKernelGGL(k_decode_stats, dim3(1), dim3(64), 0, s, tiles_split, tiles_exact, counts, flips, cap, cum);
   GM2_CHECK_LAUNCH();
 }
 

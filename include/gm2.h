@@ -359,7 +359,7 @@ int gm2_workspace_join(void* ws, void* stream);
  *   GM2_STAT_BAND_ELEMENTS  logits the gated decode found in the certified band |logit - T| <=
  *                           coef * ||a_r||_2 ||w_g||_2 and recomputed in fp64
  *   GM2_STAT_BAND_FLIPS     mask bits that recompute changed
- *   GM2_STAT_BAND_OVERFLOW  band elements beyond a call's list capacity (4,194,304), left as computed */
+ *   GM2_STAT_BAND_OVERFLOW  band elements beyond a call's list capacity (64 shards x 65,536), left as computed */
 enum {
   GM2_STAT_SPLIT_DECODES = 1,
   GM2_STAT_EXACT_DECODES = 2,
