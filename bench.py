@@ -529,7 +529,7 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
     n_dec = (n + chunk - 1) // chunk
     st = {k: v - st0[k] for k, v in m.decode_stats().items()}
     # per 256 x 256 tile (genomes x genes) the gate ran the bf16x3 split (K' = 2H, three MFMAs per
-    # fragment pair) or, for the blocks whose bound exceeds 2.5e-4, exact fp32 (128 x 128 tiles, four
+    # fragment pair) or, for the blocks whose bound exceeds 1e-3, exact fp32 (128 x 128 tiles, four
     # per block); split_fraction = the share of blocks that ran split
     blocks = st["split_tiles"] + st["exact_tiles"] / 4.0
     split_frac = st["split_tiles"] / blocks if blocks else 0.0

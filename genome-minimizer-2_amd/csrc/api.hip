@@ -939,7 +939,7 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
 //    i.e. per logit at most e = 4.62e-5 ||a_r||_2 ||w_g||_2 (Cauchy-Schwarz) on top of the fp32
 //    accumulation the exact path has as well.
 //  * Per 256 x 256 tile (genome rows x genes) the gate takes the split form when 4.62e-5 x the
-//    block's largest ||a_r|| x the block's largest ||w_g|| is at most kSplitBound (2.5e-4); every
+//    block's largest ||a_r|| x the block's largest ||w_g|| is at most kSplitBound (1e-3); every
 //    other tile runs the exact-fp32 kernel. One large activation row or weight row thus sends only
 //    its own tiles to fp32. Both kernels are launched over their full grids behind the split kernels
 //    and each tile's workgroup runs only on its verdict (the rest exit at once): no call waits on the

@@ -189,7 +189,12 @@ bool gemm_idx_ok(const GemmArgs<T>& g);
 // gate is per 256 x 256 tile: a tile runs split when kSplitUnit * max_r ||a_r|| * max_g ||w_g|| * 1.01
 // over its 256 genome rows and 256 genes (the split kernels' block maxima) is <= kSplitBound, else
 // the exact-fp32 kernel computes it.
-constexpr double kSplitBound = 2.5e-4;
+// (kSplitBound sets what the split may cost, not what the masks are: every logit within the split's
+// bound of the threshold is in the certified band and recomputed in fp64. Rounds 3-4 gated at
+// 2.5e-4, from before the band recompute existed; a v1 checkpoint trained 10 epochs then ran no
+// split tile at all (bench.py sample leg: 1.9 M genomes/s on the exact kernel). At 1e-3 the band
+// stays small (tens of thousands of logits per 65,536-genome chunk on that checkpoint))
+constexpr double kSplitBound = 1e-3;
 constexpr double kSplitUnit = 4.62e-5;  // 3.02 x 2^-16, rounded up
 constexpr int kSplitShards = 32;        // tile counters, sharded by blockIdx % kSplitShards
 // Device-side choice between the split and the exact output layer, per tile (both kernels launched

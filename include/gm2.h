@@ -323,7 +323,7 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       layer gated per 256 x 256 tile: as one bf16 GEMM over 2H (the fp32
  *                       activations and weights split into bf16 hi + lo, summing hi.hi + hi.lo +
  *                       lo.hi per K-tile) where 4.62e-5 x the tile's largest ||a_r||_2 x its largest
- *                       ||w_g||_2 is at most 2.5e-4, in exact fp32 elsewhere; logits in the certified
+ *                       ||w_g||_2 is at most 1e-3, in exact fp32 elsewhere; logits in the certified
  *                       band around the threshold are then recomputed in fp64 (GM2_STAT_BAND_*), so
  *                       a mask bit differs from the correctly rounded logit's only within the
  *                       reference's own fp32 rounding band. 0 = always the exact-fp32 output layer

@@ -11,9 +11,9 @@ lines (extras.py:196-201: z = randn(N, L); p = model.decode(z); p > 0.5) against
 `VAE.decode` (model.py:106-107) on CPU in eval mode after load_state_dict, as make_golden.py's
 sampling fixture. Scale choices (decoder-only state, random init of the reference module):
   * decoder.7 BatchNorm gamma in [0.4, 0.6] keeps the last activations' norms ~7, so the split
-    bound 4.62e-5 x max||a_r|| x max||w_g|| stays well under 2.5e-4 on most tiles;
-  * gene block 3 (genes 768..1023) has its output weights x 5 and genome block 2 (rows
-    512..767) its z x 6: the tiles of that row or column fail the bound, so the gated decode runs
+    bound 4.62e-5 x max||a_r|| x max||w_g|| stays well under the gate (1e-3) on most tiles;
+  * gene block 3 (genes 768..1023) has its output weights x 25 and genome block 2 (rows
+    512..767) its z x 20: the tiles of that row or column fail the bound, so the gated decode runs
     a mix of split and exact tiles (the fixture records the per-tile verdict computed from the
     reference module's fp64 activations, with the margin to the bound).
   * size: the decoder's weights and z are rounded to fp16-representable values BEFORE the reference
@@ -41,7 +41,7 @@ torch.set_num_threads(1)
 
 from src.genome_minimizer_2.training.model import VAE  # noqa: E402
 
-SPLIT_UNIT, SPLIT_BOUND = 4.62e-5, 2.5e-4  # gm2_kernels.hpp kSplitUnit / kSplitBound
+SPLIT_UNIT, SPLIT_BOUND = 4.62e-5, 1e-3  # gm2_kernels.hpp kSplitUnit / kSplitBound
 
 
 def main():
@@ -56,7 +56,7 @@ def main():
                 mod.weight.uniform_(0.8, 1.2)
                 mod.bias.uniform_(-0.1, 0.1)
         model.decoder[7].weight.uniform_(0.4, 0.6)
-        model.decoder[9].weight[768:1024] *= 5.0
+        model.decoder[9].weight[768:1024] *= 25.0
         model.decoder[9].bias.uniform_(-0.3, 0.3)
         for k, v in model.state_dict().items():
             if k.startswith("decoder.") and v.is_floating_point():
@@ -65,7 +65,7 @@ def main():
     torch.manual_seed(1031)
     with torch.no_grad():
         z = torch.randn(N, L)
-        z[512:768] *= 6.0
+        z[512:768] *= 20.0
         z = z.half().float()
         p = model.decode(z).numpy()  # the reference's fp32 decode (extras.py:198)
     mask = (p > 0.5).astype(np.uint8)  # extras.py:200-201
@@ -84,6 +84,7 @@ def main():
     bound = SPLIT_UNIT * 1.01 * amax[:, None] * wmax[None, :]
     verdict = bound <= SPLIT_BOUND
     margin = np.abs(np.log(bound / SPLIT_BOUND)).min()
+    print(np.array2string(bound, precision=2, max_line_width=200))
     assert margin > 0.15, f"a tile's bound is within {margin:.3f} (log) of the gate: rescale"
     assert verdict.sum() > 0 and (~verdict).sum() > 0
     print(f"split tiles {int(verdict.sum())} / {verdict.size}; bound range {bound.min():.3g} .. {bound.max():.3g}; "

@@ -172,8 +172,9 @@ def _delta(before, after):
 def test_split3_decode_equals_exact_outside_its_bound(G, H, L, N):
     """GM2_OPT_SAMPLE_SPLIT (api.hip decode_split3): the output layer of the sampling decode as one
     bf16 GEMM over K' = 2H on the (hi | lo) splits, hi.hi + hi.lo + lo.hi per K-tile. The call took
-    that path (workspace counter); its packed masks differ from the exact-fp32 path's only where the
-    fp64 logit is within the path's stated bound of the threshold (|logit64| <= 2.5e-4 + 1e-7), both
+    that path (workspace counter); its packed masks (split tiles + the certified band recomputed in
+    fp64) differ from the exact-fp32 path's (option 0: no band recompute) only where the fp64 logit is
+    within the exact path's own rounding of the threshold (|logit64| <= 2.5e-4 + 1e-7 here), both
     match the oracle outside the 1e-3 band, and the u8 and packed outputs agree -- two kernels on
     the split path: the packed one forms its bits by wave ballots from the MFMA fragments, the u8
     one through a byte image. G = 2900 leaves the last 256-gene tile past the packed row pitch (its
@@ -206,7 +207,7 @@ def test_split3_decode_equals_exact_outside_its_bound(G, H, L, N):
 
 
 def test_split3_decode_falls_back_when_the_bound_is_too_large():
-    """Output weights x 200: the bound 4.62e-5 max||a|| max||w|| exceeds 2.5e-4, so the call runs the
+    """Output weights x 200: the bound 4.62e-5 max||a|| max||w|| exceeds the gate (1e-3) on every tile, so the call runs the
     exact-fp32 output layer (workspace counter) and its masks are bit-identical to option 0's."""
     G, H, L, N = 700, 128, 16, 300
     P, S = perturb_bn(*oracle_state(G, H, L, 90), seed=91)
