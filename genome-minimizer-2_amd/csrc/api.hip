@@ -90,13 +90,14 @@ Dims make_dims(const gm2_dims* d, int gpad = kTile) {
 //              gm2_workspace_stat: split tiles, exact tiles, band elements, band flips, band
 //              overflow, decodes with split tiles, decodes without
 //   [16, 48)   split-kernel tiles of this call (sharded), [48, 80) exact-kernel tiles
-//   [80, 144)  band elements found by this call per list shard, 144 bits its recompute flipped
-//   [160, ...) block maxima of the row norms: activations (roundup(n, 256) / 256), then weights
-// Words [16, 160 + blocks) are zeroed at the start of every gated decode.
+//   [80, 144)  band elements this call put in each list shard, 144 bits its recompute flipped
+//   [160, 224) band elements this call put in tile slots (sharded)
+//   [224, ...) block maxima of the row norms: activations (roundup(n, 256) / 256), then weights
+// Words [16, 224 + blocks) are zeroed at the start of every gated decode.
 struct DecodeCtl {
   static constexpr int kCum = 0, kTilesSplit = 16, kTilesExact = 48, kCounts = 80, kFlips = 80 + kBandShards,
-                       kBlk = 160;
-  static_assert(kFlips < kBlk, "control block");
+                       kTileFound = 160, kBlk = 160 + kBandShards;
+  static_assert(kFlips < kTileFound, "control block");
 };
 
 struct Layout {
@@ -115,8 +116,9 @@ struct Layout {
   int64_t syncb;               // SyncBN all-reduce vector: 2H + 2 doubles
   // gated sampling decode (f32 workspaces; GM2_OPT_SAMPLE_SPLIT): the split activations
   // [roundup(Bm, 256)][2H] and output weights [roundup(G, 256)][2H] (bf16, (hi | lo) per 32 columns),
-  // their row norms (s3rn, s3cn), the control block (DecodeCtl) and the band list
-  int64_t s3a, s3w, s3rn, s3cn, s3ctl, s3band;
+  // their row norms (s3rn, s3cn), the control block (DecodeCtl), the band list and the split
+  // kernel's per-tile band slots (s3tlist [tiles][kBandTileSlots] (row, gene), s3tcount [tiles])
+  int64_t s3a, s3w, s3rn, s3cn, s3ctl, s3band, s3tlist, s3tcount;
   int64_t adamscal;            // scalar block of a queued output-layer Adam update
   int64_t ridx;                // zero-copy rows: int32 [roundup(Bm, 256)] resident-matrix row per batch row
 };
@@ -199,6 +201,9 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.s3cn = take(split3 ? round_up(d.G, 2 * kTile) * 4 : 0);
   o.s3ctl = take(split3 ? (DecodeCtl::kBlk + round_up(Bm, 2 * kTile) / 256 + round_up(d.G, 2 * kTile) / 256) * 4 : 0);
   o.s3band = take(split3 ? (int64_t)kBandShards * kBandShardCap * 8 : 0);
+  const int64_t s3tiles = split3 ? (round_up(Bm, 2 * kTile) / 256) * (round_up(d.G, 2 * kTile) / 256) : 0;
+  o.s3tlist = take(s3tiles * kBandTileSlots * 8);
+  o.s3tcount = take(s3tiles * 4);
   o.adamscal = take(GM2_NUM_SCALARS * 4);
   o.ridx = take(round_up(Bm, 2 * kTile) * 4);
   o.total = cur;
@@ -986,18 +991,25 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
   // and the fp32 accumulation of its 3H products, exact tiles the fp32 accumulation of H products;
   // both, the reference's own fp32 accumulation of H products
   const double gH = band_gamma((double)H), g3H = band_gamma(3.0 * H);
-  const MaskBand bs{rn, cn, (float)(kSplitUnit * 1.01 + g3H + gH), ctl + DecodeCtl::kCounts, list, kBandShardCap};
-  const MaskBand be{rn, cn, (float)(2.0 * gH), ctl + DecodeCtl::kCounts, list, kBandShardCap};
+  // (the split kernel's tiles keep their band elements in their own slots; the exact kernel's, rare,
+  // go to the shards)
+  MaskBand bs{rn, cn, (float)(kSplitUnit * 1.01 + g3H + gH), ctl + DecodeCtl::kCounts, list, kBandShardCap};
+  MaskBand be = bs;
+  be.coef = (float)(2.0 * gH);
+  bs.tlist = (uint2*)(c.ws + l.s3tlist);
+  bs.tcount = (unsigned*)(c.ws + l.s3tcount);
+  bs.tfound = ctl + DecodeCtl::kTileFound;
+  bs.tslots = kBandTileSlots;
   GemmArgs<bf16_t> g{a3, 2 * H, w3, 2 * H, n, G, 2 * H, Bq, Gq, 0};
   launch_gemm_mask<bf16_t>(g, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
                            true, MaskGate{ablk, wblk, 1, ctl + DecodeCtl::kTilesSplit}, bs);
   GemmArgs<float> ge{c.f(l.A[5]), H, c.f(l.sD3), H, n, G, H, (int)round_up(n, kTile), (int)d.Gp, 0};
   launch_gemm_mask<float>(ge, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
                           false, MaskGate{ablk, wblk, 2, ctl + DecodeCtl::kTilesExact}, be);
-  launch_band_fix(list, ctl + DecodeCtl::kCounts, kBandShardCap, c.f(l.A[5]), H, w9, H, prm + d.off[D9B], H, bits, ldb,
-                  mask, ldm, ctl + DecodeCtl::kFlips, c.s);
+  launch_band_fix(bs, (Bq / 256) * (Gq / 256), c.f(l.A[5]), H, w9, H, prm + d.off[D9B], H, bits, ldb, mask, ldm,
+                  ctl + DecodeCtl::kFlips, c.s);
   launch_decode_stats(ctl + DecodeCtl::kTilesSplit, ctl + DecodeCtl::kTilesExact, ctl + DecodeCtl::kCounts,
-                      ctl + DecodeCtl::kFlips, kBandShardCap, (unsigned long long*)(ctl + DecodeCtl::kCum), c.s);
+                      ctl + DecodeCtl::kTileFound, ctl + DecodeCtl::kFlips, kBandShardCap, (unsigned long long*)(ctl + DecodeCtl::kCum), c.s);
   return true;
 }
 
@@ -1639,7 +1651,7 @@ int gm2_debug_check_layout(const gm2_dims* d, int precision, int64_t* n_regions,
     const int64_t named[] = {o.sE0, o.sE1, o.sE2, o.sHD, o.sD0, o.sD1, o.sD2, o.sD3, o.X, o.XB, o.HD, o.Z, o.dL,
                              o.slabs, o.side_slabs, o.DA, o.dH, o.AT5, o.dYT0, o.bnpart, o.colpart, o.losspart,
                              o.klpart, o.gradpart, o.colbwd, o.nahdr, o.nasq, o.clip, o.scal0, o.X1, o.XB1, o.syncb,
-                             o.s3a, o.s3w, o.s3rn, o.s3cn, o.s3ctl, o.s3band,
+                             o.s3a, o.s3w, o.s3rn, o.s3cn, o.s3ctl, o.s3band, o.s3tlist, o.s3tcount,
                              o.adamscal, o.ridx};
     auto known = [&](int64_t off) {
       for (const auto& x : r)

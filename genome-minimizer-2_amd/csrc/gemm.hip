@@ -1234,55 +1234,149 @@ struct MaskOut {
 };
 
 // The certified band (MaskBand): the tile's row norms and column norms go to LDS past the staging
-// ring before the main loop (whose barriers order them before the epilogue); an element is in the
-// band when |l - T| <= ||a_r|| * (coef * ||w_g||). The epilogues only flag a lane (a few VALU per
-// element); a wave with a flagged lane re-walks its fragments and appends the flagged (row, gene)
-// pairs (rare: a handful per tile).
+// ring before the main loop (whose barriers order them before the epilogue), with the tile's slot
+// counter after them. Per element the epilogues add one compare, OR-ed into a wave mask by its
+// ballot (|d| <= rmax * ce + eb, MaskBand); a wave whose mask is non-zero re-walks its fragments
+// and appends the flagged (row, gene) pairs (rare: ~2 per tile of a trained model).
 template <class C>
 __device__ __forceinline__ void band_stage(const MaskBand& b, const TileXY& tl, char* smem) {
   float* brn = (float*)(smem + C::LDS);
   for (int i = threadIdx.x; i < C::BM + C::BN; i += C::NT)
     brn[i] = i < C::BM ? b.rn[tl.m0 + i] : b.cn[tl.n0 + i - C::BM];
+  if (threadIdx.x == 0) ((unsigned*)brn)[C::BM + C::BN] = 0u;
 }
+template <class C>
+constexpr int band_lds_bytes() { return (C::BM + C::BN) * 4 + 16; }
 
-// one wave's band elements: the wave's total reserved by one atomic on its shard's counter, then
-// each lane writes its elements at its prefix offset (push(i) walks the same elements in the same
-// order in both passes)
-template <class F>
-__device__ __forceinline__ void band_append(const MaskBand& b, int lane, F&& walk) {
-  unsigned mine = 0;
-  walk([&](bool in, int, int) { mine += in ? 1u : 0u; });
-  unsigned tot = mine, pre = 0;
+// the band's per-column terms of one lane (column fragment ni): bt = b - T, ce = coef ||w_g||
+// (rounded up); the rounding floor 2^-21 (|b| + T) <= 2^-21 |bt| + 2^-20 T is formed per fragment.
+// Pad genes: bt = -inf, ce = -inf (never in the band)
+template <class C>
+struct BandCols {
+  float bt[C::FN], ce[C::FN];
+  __device__ __forceinline__ BandCols(const float* __restrict__ bias, const float* brn, const MaskBand& band, bool bchk,
+                                      int n0, int N, int lane, int wn) {
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {  // inclusive scan over the wave
-    const unsigned v = __shfl_up(tot, o, 64);
-    if (lane >= o) tot += v;
+    for (int ni = 0; ni < C::FN; ++ni) {
+      const int nl = wn * C::WTN + ni * 16 + (lane & 15);
+      const bool in = n0 + nl < N;
+      bt[ni] = in ? bias[n0 + nl] - kMaskLogitThreshold : -INFINITY;
+      ce[ni] = !in ? -INFINITY : bchk ? band.coef * brn[C::BM + nl] * (1.0f + 0x1p-20f) : 0.f;
+    }
   }
-  pre = tot - mine;
-  const unsigned wtot = __shfl(tot, 63, 64);
+  // this lane's band half-widths for row fragment mi (the largest of its four rows' norms); without
+  // a band check: -1 (nothing is in it)
+  __device__ __forceinline__ void widths(const float* brn, bool bchk, int r0, float (&e)[C::FN]) const {
+    if (!bchk) {
+#pragma unroll
+      for (int ni = 0; ni < C::FN; ++ni) e[ni] = -1.f;
+      return;
+    }
+    const float4 r4 = *(const float4*)(brn + r0);
+    const float rmax = fmaxf(fmaxf(r4.x, r4.y), fmaxf(r4.z, r4.w));
+#pragma unroll
+    for (int ni = 0; ni < C::FN; ++ni)
+      e[ni] = fmaf(rmax, ce[ni], fmaf(0x1p-21f, fabsf(bt[ni]), 0x1p-20f * kMaskLogitThreshold));
+  }
+};
+
+// one wave's band elements: walk(visit) calls visit(in, row, gene) for every fragment position in a
+// fixed order; per position with flagged lanes, one reservation for all of them (an LDS counter
+// for the tile's slots, else the shard's counter) and each flagged lane's entry at its prefix
+template <class C, class F>
+__device__ __forceinline__ void band_walk(const MaskBand& b, int tile, char* smem, int lane, F&& walk) {
+  unsigned* lcount = (unsigned*)(smem + C::LDS) + C::BM + C::BN;
   const int sh = blockIdx.x % kBandShards;
-  unsigned base = 0;
-  if (lane == 0) base = atomicAdd(b.counts + sh, wtot);
-  base = __shfl(base, 0, 64) + pre;
-  uint2* list = b.list + (size_t)sh * b.cap;
+  uint2* shard = b.list + (size_t)sh * b.cap;
   walk([&](bool in, int r, int gcol) {
-    if (in) {
-      if (base < b.cap) list[base] = make_uint2((unsigned)r, (unsigned)gcol);
-      ++base;
+    const uint64_t bal = __ballot(in);
+    if (!bal) return;
+    const unsigned pre = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(b.tslots ? lcount : b.counts + sh, (unsigned)__popcll(bal));
+    const unsigned i = __shfl(base, 0, 64) + pre;
+    if (!in) return;
+    const uint2 e = make_uint2((unsigned)r, (unsigned)gcol);
+    if (!b.tslots) {
+      if (i < b.cap) shard[i] = e;
+    } else if (i < (unsigned)b.tslots) {
+      b.tlist[(size_t)tile * b.tslots + i] = e;
+    } else {  // past the tile's slots: the shard (rare)
+      const unsigned k = atomicAdd(b.counts + sh, 1u);
+      if (k < b.cap) shard[k] = e;
     }
   });
 }
+// after the epilogue's barrier: the tile's slot count
+template <class C>
+__device__ __forceinline__ void band_close(const MaskBand& b, int tile, char* smem) {
+  if (!b.tslots || threadIdx.x != 0) return;
+  const unsigned n = min(((const unsigned*)(smem + C::LDS))[C::BM + C::BN], (unsigned)b.tslots);
+  b.tcount[tile] = n;
+  if (n) atomicAdd(b.tfound + blockIdx.x % kBandShards, n);
+}
+
+template <class C, typename T, bool PP, bool BITS>
+__device__ __forceinline__ void mask_tile(const TileXY tl, const GemmArgs<T>& g, const float* __restrict__ bias,
+                                          const MaskOut& o, char* smem);
 
 // PP: the 256x256 bf16 ping-pong main loop in its S3 form (the bf16x3 sampling decode: hi.hi +
-// hi.lo + lo.hi over operands split by launch_split3, K' = 2H, decode_split3)
-template <class C, typename T, bool PP = false, bool BITS = false>
+// hi.lo + lo.hi over operands split by launch_split3, K' = 2H, decode_split3). LOOP (gated 128 x
+// 128 launches, usually the complement of the split kernel with few tiles to run): a grid of a few
+// workgroups per CU loops over the tiles t, t + grid, ... instead of one workgroup per tile.
+template <class C, typename T, bool PP = false, bool BITS = false, bool LOOP = false>
 __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float* __restrict__ bias, MaskOut o) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const TileXY tl = tile_of<C>(g.Mp / C::BM, g.Np / C::BN);
-  if (o.gate.run) {  // per tile: the verdict of the 256 x 256 block this tile lies in (uniform per workgroup)
-    if (split_tile_ok(o.gate, tl.m0, tl.n0) != (o.gate.run == 1)) return;
-    if (threadIdx.x == 0) atomicAdd(o.gate.tiles + blockIdx.x % kSplitShards, 1u);
+  const int tm = g.Mp / C::BM, tn = g.Np / C::BN, ntile = tm * tn;
+  if constexpr (!LOOP) {
+    const TileXY tl = tile_of<C>(tm, tn);
+    if (o.gate.run) {  // the verdict of the tile's 256 x 256 block (uniform per workgroup)
+      if (split_tile_ok(o.gate, tl.m0, tl.n0) != (o.gate.run == 1)) {
+        if (o.band.tslots && threadIdx.x == 0) o.band.tcount[tl.t] = 0u;
+        return;
+      }
+      if (threadIdx.x == 0) atomicAdd(o.gate.tiles + blockIdx.x % kSplitShards, 1u);
+    }
+    mask_tile<C, T, PP, BITS>(tl, g, bias, o, smem);
+  } else {
+    static_assert(!PP && !BITS, "tile loop: the 128 x 128 kernel");
+    // the workgroup's tiles t0 + k G: their gate verdicts NT at a time, in parallel (one ballot word
+    // per wave in LDS past the band region), then the runnable ones in order
+    const int G = gridDim.x, t0 = xcd_wg(), lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t* vm = (uint64_t*)(smem + C::LDS + band_lds_bytes<C>());
+    for (int kb = 0; t0 + kb * G < ntile; kb += C::NT) {
+      __syncthreads();  // (the previous pass's words are read)
+      const int t = t0 + (kb + (int)threadIdx.x) * G;
+      bool run = false;
+      if (t < ntile) {
+        const TileXY tl = tile_at<C>(t, tm, tn, 0);
+        run = !o.gate.run || split_tile_ok(o.gate, tl.m0, tl.n0) == (o.gate.run == 1);
+      }
+      const uint64_t bw = __ballot(run);
+      if (lane == 0) vm[wid] = bw;
+      __syncthreads();
+      unsigned nrun = 0;
+#pragma unroll 1
+      for (int w = 0; w < C::NT / 64; ++w) {
+        const uint64_t v = vm[w];
+        uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
+                     __builtin_amdgcn_readfirstlane((unsigned)v);
+        while (m) {
+          const int i = __builtin_ctzll(m);
+          m &= m - 1;
+          ++nrun;
+          __syncthreads();  // (the previous tile's epilogue is done with LDS)
+          mask_tile<C, T, PP, BITS>(tile_at<C>(t0 + (kb + w * 64 + i) * G, tm, tn, 0), g, bias, o, smem);
+        }
+      }
+      if (o.gate.run && nrun && threadIdx.x == 0) atomicAdd(o.gate.tiles + blockIdx.x % kSplitShards, nrun);
+    }
   }
+}
+
+template <class C, typename T, bool PP, bool BITS>
+__device__ __forceinline__ void mask_tile(const TileXY tl, const GemmArgs<T>& g, const float* __restrict__ bias,
+                                          const MaskOut& o, char* smem) {
   const bool bchk = o.band.rn != nullptr;
   if (bchk) band_stage<C>(o.band, tl, smem);
   const float* brn = (const float*)(smem + C::LDS);  // [BM] row norms, then [BN] column norms
@@ -1294,60 +1388,57 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
     mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
+  const BandCols<C> bc(bias, brn, o.band, bchk, tl.n0, g.N, lane, wn);
+  uint64_t bandw = 0;  // this wave's band flags, OR-ed over its fragment positions
   if constexpr (BITS) {
     static_assert(PP, "bit-image epilogue: the split decode's kernel");
     {
       // packed bits straight from the fragments: lane l of a 16x16 fragment holds row 4(l>>4) + j,
       // column l&15, so one ballot per (mi, ni, j) yields 16 gene bits for each of 4 rows; lane r < 4
       // gathers row r's 64 bits over the wave's 4 column fragments and writes them to a [BM][32 B]
-      // bit image (one ds_write_b64 per (mi, j), where the u8 image took one byte store per logit)
-      float bnv[C::FN], ce[C::FN];
-#pragma unroll
-      for (int ni = 0; ni < C::FN; ++ni) {
-        const int n = tl.n0 + wn * C::WTN + ni * 16 + (lane & 15);
-        bnv[ni] = n < g.N ? bias[n] : -INFINITY;  // (pad genes: never set, never in the band)
-        ce[ni] = bchk ? o.band.coef * brn[C::BM + wn * C::WTN + ni * 16 + (lane & 15)] : 0.f;
-      }
+      // bit image (one ds_write_b64 per (mi, j), where the u8 image took one byte store per logit).
+      // The bit is d = acc + (b - T) > 0 (pad genes: d = -inf); d and acc + b round differently
+      // only inside the band, which the recompute decides.
       const int sh = 16 * (lane & 3);
-      bool anyb = false;
 #pragma unroll
       for (int mi = 0; mi < C::FM; ++mi) {
-        const float4 ra4 = bchk ? *(const float4*)(brn + wm * C::WTM + mi * 16 + 4 * (lane >> 4))
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float ra[4] = {ra4.x, ra4.y, ra4.z, ra4.w};
+        float e[C::FN];
+        bc.widths(brn, bchk, wm * C::WTM + mi * 16 + 4 * (lane >> 4), e);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           uint64_t rb = 0;
 #pragma unroll
           for (int ni = 0; ni < C::FN; ++ni) {
-            const float l = acc[mi][ni][j] + bnv[ni];
-            const uint64_t bal = __ballot(l > kMaskLogitThreshold);
+            const float d = acc[mi][ni][j] + bc.bt[ni];
+            const uint64_t bal = __ballot(d > 0.f);
             rb |= ((bal >> sh) & 0xFFFFull) << (16 * ni);
-            anyb |= fabsf(l - kMaskLogitThreshold) <= ra[j] * ce[ni];
+            bandw |= __ballot(fabsf(d) <= e[ni]);
           }
           if (lane < 4)
             *(uint64_t*)(smem + (wm * C::WTM + mi * 16 + 4 * lane + j) * (C::BN / 8) + wn * (C::WTN / 8)) = rb;
           __builtin_amdgcn_sched_barrier(0);  // (one row quad at a time: the ballots' SGPR pairs stay few)
         }
       }
-      if (__ballot(anyb)) {  // append this wave's band elements (unrolled: acc stays in registers)
-        band_append(o.band, lane, [&](auto&& visit) {
+      if (bandw) {  // append this wave's band elements (unrolled: acc stays in registers)
+        band_walk<C>(o.band, tl.t, smem, lane, [&](auto&& visit) {
 #pragma unroll
-          for (int mi = 0; mi < C::FM; ++mi)
+          for (int mi = 0; mi < C::FM; ++mi) {
+            float e[C::FN];
+            bc.widths(brn, bchk, wm * C::WTM + mi * 16 + 4 * (lane >> 4), e);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int r = tl.m0 + wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
-              const float raj = brn[r - tl.m0];
 #pragma unroll
               for (int ni = 0; ni < C::FN; ++ni) {
-                const float l = acc[mi][ni][j] + bnv[ni];
-                visit(fabsf(l - kMaskLogitThreshold) <= raj * ce[ni] && r < g.M, r,
-                      tl.n0 + wn * C::WTN + ni * 16 + (lane & 15));
+                const float d = acc[mi][ni][j] + bc.bt[ni];
+                visit(fabsf(d) <= e[ni] && r < g.M, r, tl.n0 + wn * C::WTN + ni * 16 + (lane & 15));
               }
             }
+          }
         });
       }
       __syncthreads();
+      band_close<C>(o.band, tl.t, smem);
       constexpr int BPR = C::BN / 8;
       const int rows = min(C::BM, g.M - tl.m0);
       for (int i = threadIdx.x; i < rows * (BPR / 16); i += C::NT) {
@@ -1361,54 +1452,48 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
   constexpr int PI = C::BN + 16;  // u8 image pitch
   uint8_t* img = (uint8_t*)smem;  // [BM][PI] (mainloop staging is free after its last barrier)
   const bool half = o.thr == 0.5f;
-  bool anyb = false;
-  float bnv[C::FN], ce[C::FN];
-#pragma unroll
-  for (int ni = 0; ni < C::FN; ++ni) {
-    const int nl = wn * C::WTN + ni * 16 + (lane & 15);
-    const int n = tl.n0 + nl;
-    bnv[ni] = n < g.N ? bias[n] : 0.f;
-    ce[ni] = (bchk && n < g.N) ? o.band.coef * brn[C::BM + nl] : -1.f;  // (pad genes: never in the band)
-  }
 #pragma unroll
   for (int mi = 0; mi < C::FM; ++mi) {
-    const float4 ra4 = bchk ? *(const float4*)(brn + wm * C::WTM + mi * 16 + 4 * (lane >> 4))
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float ra[4] = {ra4.x, ra4.y, ra4.z, ra4.w};
+    float e[C::FN];
+    bc.widths(brn, bchk, wm * C::WTM + mi * 16 + 4 * (lane >> 4), e);
 #pragma unroll
     for (int ni = 0; ni < C::FN; ++ni) {
       const int nl = wn * C::WTN + ni * 16 + (lane & 15);
       const int n = tl.n0 + nl;
+      const float bnv = n < g.N ? bias[n] : 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int ml = wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
         const int m = tl.m0 + ml;
-        const float l = acc[mi][ni][j] + bnv[ni];
+        const float l = acc[mi][ni][j] + bnv;
         float p = 0.f;
         if (o.probs || !half) p = 1.0f / (1.0f + expf(-l));
         const bool pred = n < g.N && (half ? l > kMaskLogitThreshold : p > o.thr);
         img[ml * PI + nl] = pred ? 1 : 0;
         if (o.probs && m < g.M && n < g.N) o.probs[(int64_t)m * o.ldpr + n] = p;
-        anyb |= fabsf(l - kMaskLogitThreshold) <= ra[j] * ce[ni];
+        if (bchk) bandw |= __ballot(fabsf(acc[mi][ni][j] + bc.bt[ni]) <= e[ni]);
       }
     }
   }
-  if (bchk && __ballot(anyb)) {  // append this wave's band elements (unrolled: acc stays in registers)
-    band_append(o.band, lane, [&](auto&& visit) {
+  if (bandw) {  // append this wave's band elements (unrolled: acc stays in registers)
+    band_walk<C>(o.band, tl.t, smem, lane, [&](auto&& visit) {
 #pragma unroll
-      for (int mi = 0; mi < C::FM; ++mi)
+      for (int mi = 0; mi < C::FM; ++mi) {
+        float e[C::FN];
+        bc.widths(brn, bchk, wm * C::WTM + mi * 16 + 4 * (lane >> 4), e);
 #pragma unroll
         for (int ni = 0; ni < C::FN; ++ni)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int ml = wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
-            const float l = acc[mi][ni][j] + bnv[ni];
-            visit(fabsf(l - kMaskLogitThreshold) <= brn[ml] * ce[ni] && tl.m0 + ml < g.M, tl.m0 + ml,
+            visit(fabsf(acc[mi][ni][j] + bc.bt[ni]) <= e[ni] && tl.m0 + ml < g.M, tl.m0 + ml,
                   tl.n0 + wn * C::WTN + ni * 16 + (lane & 15));
           }
+      }
     });
   }
   __syncthreads();
+  band_close<C>(o.band, tl.t, smem);
   const int rows = min(C::BM, g.M - tl.m0);
   if (o.mask) {
     // one row per 8 threads' 16-byte pieces (or byte runs when the rows are not 16-B aligned)
@@ -1880,13 +1965,15 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
   MaskOut o{mask, ldm, bits, ldb, probs, ldpr, counts, xbits, ldxb, thr, gate, band};
   if (band.rn && (!band.cn || !band.counts || !band.list || !band.cap || thr != 0.5f))
     throw Gm2Error("mask band: norms, counter and list required (threshold 0.5 only)");
-  const int band_lds = band.rn ? (big ? 512 : 256) * 4 : 0;  // (row + column norms past the staging ring)
+  if (band.tslots && (!band.tlist || !band.tcount || !band.tfound || !big))
+    throw Gm2Error("mask band: tile slots need their list, counters and the 256 x 256 kernel");
+  const int band_lds = band.rn ? (big ? band_lds_bytes<Big>() : band_lds_bytes<Small>()) : 0;  // (norms + slot counter)
   TimedLaunch tl(kKcMask, s);
   if constexpr (sizeof(T) == 2) {
     if (big) {
       if (g.Mp % 256 || g.Np % 256 || g.K % 64) throw Gm2Error("mask (256x256): padded extents");
       static_assert(Big::LDS >= 256 * (256 + 16), "u8 image inside the staging ring");
-      constexpr int lds_max = Big::LDS + 512 * 4;
+      constexpr int lds_max = Big::LDS + band_lds_bytes<Big>();
       const int lds = Big::LDS + band_lds;
       const dim3 grid((g.Mp / 256) * (g.Np / 256));
       if (bits && !mask && !probs && !counts && thr == 0.5f) {  // packed bits only: ballot epilogue
@@ -1902,9 +1989,17 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
   }
   if (big) throw Gm2Error("mask (256x256): bf16 only");
   static_assert(Small::LDS >= 128 * (128 + 16), "u8 image inside the staging ring");
-  if (band_lds) ensure_lds_attr((const void*)k_gemm_mask<Small, T>, Small::LDS + 256 * 4);
-  hipLaunchKernelGGL((k_gemm_mask<Small, T>), dim3((g.Mp / 128) * (g.Np / 128)), dim3(Small::NT), Small::LDS + band_lds,
-                     s, g, bias, o);
+  const int ntile = (g.Mp / 128) * (g.Np / 128);
+  if (gate.run) {  // (the tile loop, from a grid of at most 1024 workgroups)
+    // (LDS: the band region always, then the verdict words)
+    constexpr int lds = Small::LDS + band_lds_bytes<Small>() + (Small::NT / 64) * 8;
+    ensure_lds_attr((const void*)k_gemm_mask<Small, T, false, false, true>, lds);
+    hipLaunchKernelGGL((k_gemm_mask<Small, T, false, false, true>), dim3(std::min(ntile, 1024)), dim3(Small::NT), lds,
+                       s, g, bias, o);
+  } else {
+    if (band_lds) ensure_lds_attr((const void*)k_gemm_mask<Small, T>, Small::LDS + band_lds_bytes<Small>());
+    hipLaunchKernelGGL((k_gemm_mask<Small, T>), dim3(ntile), dim3(Small::NT), Small::LDS + band_lds, s, g, bias, o);
+  }
   GM2_CHECK_LAUNCH();
 }
 

@@ -218,11 +218,18 @@ __device__ __forceinline__ bool split_tile_ok(const MaskGate& g, int m0, int n0)
 //   coef (split tiles) = kSplitUnit * 1.01 + gamma_3H + gamma_H: the split's own error, its fp32
 //     accumulation of 3H products and the reference's fp32 accumulation of H products
 //   coef (exact tiles) = 2 gamma_H (gamma_n = n u / (1 - n u), u = 2^-24)
-// The list is kBandShards shards of `cap` entries (shard = blockIdx % kBandShards, each with its own
-// counter: one atomic per wave per tile, not per element, and 64 counter words instead of one);
-// entries past a shard's capacity are only counted (left as the kernel decided them).
+// The epilogues test |d| <= rmax * coef * ||w_g|| (1 + 2^-20) + 2^-21 (|b| + T), d = acc + b - T
+// as they form it and rmax the largest of the four row norms a lane holds in one fragment: a
+// superset of the band (the extra terms cover the rounding of d and of the product).
+// Each flagged element goes to its tile's slots when the launch has them (tslots > 0: slot index
+// from a counter in LDS, the tile's count stored once at the end of the tile; no global atomic on
+// the common path), else (and for a tile's elements past its slots) to the list's kBandShards
+// shards of `cap` entries (shard = blockIdx % kBandShards, each with its own counter: one atomic per
+// wave per fragment position that holds band elements); entries past a shard's capacity are only
+// counted (left as the kernel decided them).
 constexpr int kBandShards = 64;
 constexpr unsigned kBandShardCap = 1u << 16;  // entries per shard per decode call (64 x 64 K x 8 B = 32 MB)
+constexpr int kBandTileSlots = 32;            // per 256 x 256 split tile (a trained model: ~2 per tile)
 struct MaskBand {
   const float* rn = nullptr;  // ||a_r|| per genome row (nullptr: no band check)
   const float* cn = nullptr;  // ||w_g|| per gene
@@ -230,17 +237,22 @@ struct MaskBand {
   unsigned* counts = nullptr; // [kBandShards]
   uint2* list = nullptr;      // [kBandShards][cap] (row, gene)
   unsigned cap = 0;
+  uint2* tlist = nullptr;     // [tiles][tslots] (row, gene), tile = TileXY::t of the launch's grid
+  unsigned* tcount = nullptr; // [tiles] entries in the tile's slots (every tile of the grid writes its own)
+  unsigned* tfound = nullptr; // [kBandShards] sum of tcount (statistics)
+  int tslots = 0;
 };
 inline double band_gamma(double n) { return n * 0x1p-24 / (1.0 - n * 0x1p-24); }
-// k_band_fix over every shard's entries: fp64 logit of (A[row], W[gene]) + bias, mask bit =
-// (float)logit > T (the correctly rounded fp32 logit against the reference's threshold); packed
-// bits (bits != nullptr) or u8 mask. flips: the bits it changed
-void launch_band_fix(const uint2* list, const unsigned* counts, unsigned cap, const float* A, int64_t lda,
-                     const float* W, int64_t ldw, const float* bias, int H, uint8_t* bits, int64_t ldb, uint8_t* mask,
-                     int64_t ldm, unsigned* flips, hipStream_t s);
+// k_band_fix over every shard's entries and every tile's slots: fp64 logit of (A[row], W[gene]) +
+// bias, mask bit = (float)logit > T (the correctly rounded fp32 logit against the reference's
+// threshold); packed bits (bits != nullptr) or u8 mask. flips: the bits it changed
+void launch_band_fix(const MaskBand& band, int ntiles, const float* A, int64_t lda, const float* W, int64_t ldw,
+                     const float* bias, int H, uint8_t* bits, int64_t ldb, uint8_t* mask, int64_t ldm, unsigned* flips,
+                     hipStream_t s);
 // one workgroup: the decode call's per-call counters -> the workspace's cumulative ones (DecodeCtl)
 void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* counts,
-                         const unsigned* flips, unsigned cap, unsigned long long* cum, hipStream_t s);
+                         const unsigned* tfound, const unsigned* flips, unsigned cap, unsigned long long* cum,
+                         hipStream_t s);
 
 // output layer + threshold (sampling / metrics): u8 mask, packed bits, probs, per-row (TP, FP, FN).
 // big (bf16 only): the bf16x3 split decode -- 256x256 ping-pong tiles over operands in

@@ -1198,41 +1198,55 @@ __global__ __launch_bounds__(256) void k_exchange_unpack(const bf16_t* __restric
 // Packed bits are set / cleared with 32-bit atomics (several waves may share a word), u8 masks by
 // byte stores. flips counts the bits the recompute changed.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_band_fix(const uint2* __restrict__ list, const unsigned* __restrict__ counts,
-                                                unsigned cap, const float* __restrict__ A, int64_t lda,
+__device__ __forceinline__ void band_fix_one(const uint2 rg, int lane, const float* __restrict__ A, int64_t lda,
+                                             const float* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
+                                             int H, uint8_t* bits, int64_t ldb, uint8_t* mask, int64_t ldm,
+                                             unsigned* flips) {
+  const float* a = A + (int64_t)rg.x * lda;
+  const float* w = W + (int64_t)rg.y * ldw;
+  double acc = 0.0;
+  for (int k = lane; k < H; k += 64) acc = fma((double)a[k], (double)w[k], acc);
+  acc = wave_sum_d(acc) + (double)bias[rg.y];
+  const bool pred = (float)acc > kMaskLogitThreshold;
+  if (lane == 0) {
+    bool was;
+    if (bits) {
+      unsigned* word = (unsigned*)(bits + (int64_t)rg.x * ldb) + (rg.y >> 5);
+      const unsigned bit = 1u << (rg.y & 31);
+      const unsigned old = pred ? atomicOr(word, bit) : atomicAnd(word, ~bit);
+      was = (old & bit) != 0;
+    } else {
+      uint8_t* p = mask + (int64_t)rg.x * ldm + rg.y;
+      was = *p != 0;
+      *p = pred ? 1 : 0;
+    }
+    if (was != pred) atomicAdd(flips, 1u);
+  }
+}
+
+// workgroups [0, kBandFixShardWgs): the shards (wave w takes shard w % kBandShards, its entries
+// w / kBandShards, + waves / kBandShards, ...); the rest: one wave per tile's slots
+constexpr int kBandFixShardWgs = 256;
+__global__ __launch_bounds__(256) void k_band_fix(MaskBand band, int ntiles, const float* __restrict__ A, int64_t lda,
                                                 const float* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
                                                 int H, uint8_t* bits, int64_t ldb, uint8_t* mask, int64_t ldm,
                                                 unsigned* flips) {
-  // wave w takes shard w % kBandShards, its entries w / kBandShards, + waves / kBandShards, ...
   const int lane = threadIdx.x & 63;
-  const unsigned wave = blockIdx.x * 4 + (threadIdx.x >> 6), waves = gridDim.x * 4;
-  const int sh = wave % kBandShards;
-  const unsigned per = waves / kBandShards;
-  const unsigned n = min(counts[sh], cap);
-  const uint2* sl = list + (size_t)sh * cap;
-  for (unsigned e = wave / kBandShards; e < n; e += per) {
-    const uint2 rg = sl[e];
-    const float* a = A + (int64_t)rg.x * lda;
-    const float* w = W + (int64_t)rg.y * ldw;
-    double acc = 0.0;
-    for (int k = lane; k < H; k += 64) acc = fma((double)a[k], (double)w[k], acc);
-    acc = wave_sum_d(acc) + (double)bias[rg.y];
-    const bool pred = (float)acc > kMaskLogitThreshold;
-    if (lane == 0) {
-      bool was;
-      if (bits) {
-        unsigned* word = (unsigned*)(bits + (int64_t)rg.x * ldb) + (rg.y >> 5);
-        const unsigned bit = 1u << (rg.y & 31);
-        const unsigned old = pred ? atomicOr(word, bit) : atomicAnd(word, ~bit);
-        was = (old & bit) != 0;
-      } else {
-        uint8_t* p = mask + (int64_t)rg.x * ldm + rg.y;
-        was = *p != 0;
-        *p = pred ? 1 : 0;
-      }
-      if (was != pred) atomicAdd(flips, 1u);
-    }
+  if (blockIdx.x < kBandFixShardWgs) {
+    const unsigned wave = blockIdx.x * 4 + (threadIdx.x >> 6), waves = kBandFixShardWgs * 4;
+    const int sh = wave % kBandShards;
+    const unsigned per = waves / kBandShards;
+    const unsigned n = min(band.counts[sh], band.cap);
+    const uint2* sl = band.list + (size_t)sh * band.cap;
+    for (unsigned e = wave / kBandShards; e < n; e += per)
+      band_fix_one(sl[e], lane, A, lda, W, ldw, bias, H, bits, ldb, mask, ldm, flips);
+    return;
   }
+  const int t = (blockIdx.x - kBandFixShardWgs) * 4 + (threadIdx.x >> 6);
+  if (t >= ntiles) return;
+  const unsigned n = band.tcount[t];
+  const uint2* tl = band.tlist + (size_t)t * band.tslots;
+  for (unsigned e = 0; e < n; ++e) band_fix_one(tl[e], lane, A, lda, W, ldw, bias, H, bits, ldb, mask, ldm, flips);
 }
 
 // the decode call's counters -> the workspace's cumulative ones: cum[0] split tiles, [1] exact
@@ -1241,12 +1255,13 @@ __global__ __launch_bounds__(256) void k_band_fix(const uint2* __restrict__ list
 __global__ __launch_bounds__(64) void k_decode_stats(const unsigned* __restrict__ tiles_split,
                                                      const unsigned* __restrict__ tiles_exact,
                                                      const unsigned* __restrict__ counts,
+                                                     const unsigned* __restrict__ tfound,
                                                      const unsigned* __restrict__ flips, unsigned cap,
                                                      unsigned long long* cum) {
   const int t = threadIdx.x;
   unsigned long long a = t < kSplitShards ? tiles_split[t] : 0ull, b = t < kSplitShards ? tiles_exact[t] : 0ull;
   const unsigned c = t < kBandShards ? counts[t] : 0u;
-  unsigned long long found = c, over = c > cap ? c - cap : 0u;
+  unsigned long long found = (unsigned long long)c + (t < kBandShards ? tfound[t] : 0u), over = c > cap ? c - cap : 0u;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     a += __shfl_xor(a, o, 64);
@@ -1472,22 +1487,26 @@ void launch_exchange_unpack(const bf16_t* in, int64_t n, float* x, hipStream_t s
   GM2_CHECK_LAUNCH();
 }
 
-void launch_band_fix(const uint2* list, const unsigned* counts, unsigned cap, const float* A, int64_t lda,
-                     const float* W, int64_t ldw, const float* bias, int H, uint8_t* bits, int64_t ldb, uint8_t* mask,
-                     int64_t ldm, unsigned* flips, hipStream_t s) {
+void launch_band_fix(const MaskBand& band, int ntiles, const float* A, int64_t lda, const float* W, int64_t ldw,
+                     const float* bias, int H, uint8_t* bits, int64_t ldb, uint8_t* mask, int64_t ldm, unsigned* flips,
+                     hipStream_t s) {
   if ((!bits && !mask) || (bits && (ldb & 3)))
     throw Gm2Error("band fix: an output (packed bits with 4-B aligned rows, or a u8 mask) is required");
-  // (a fixed grid, the counts live on the device: 16 waves per shard)
-  static_assert((1024 * 4) % kBandShards == 0, "band fix grid");
-  hipLaunchKernelGGL(k_band_fix, dim3(1024), dim3(256), 0, s, list, counts, cap, A, lda, W, ldw, bias, H, bits, ldb,
-                     mask, ldm, flips);
+  if (!band.counts || !band.list || !band.cap || ntiles < 0 || (ntiles && (!band.tlist || !band.tcount || band.tslots <= 0)))
+    throw Gm2Error("band fix: shard list and counters (and tile slots for %d tiles) required", ntiles);
+  // (a fixed grid for the shards, the counts live on the device: 16 waves per shard; then one wave per tile)
+  static_assert((kBandFixShardWgs * 4) % kBandShards == 0, "band fix grid");
+  const unsigned grid = kBandFixShardWgs + (unsigned)((ntiles + 3) / 4);
+  hipLaunchKernelGGL(k_band_fix, dim3(grid), dim3(256), 0, s, band, ntiles, A, lda, W, ldw, bias, H, bits, ldb, mask,
+                     ldm, flips);
   GM2_CHECK_LAUNCH();
 }
 
 void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* counts,
-                         const unsigned* flips, unsigned cap, unsigned long long* cum, hipStream_t s) {
+                         const unsigned* tfound, const unsigned* flips, unsigned cap, unsigned long long* cum,
+                         hipStream_t s) {
   static_assert(kSplitShards <= 64 && kBandShards <= 64, "one wave");
-  hipLaunchKernelGGL(k_decode_stats, dim3(1), dim3(64), 0, s, tiles_split, tiles_exact, counts, flips, cap, cum);
+  hipLaunchKernelGGL(k_decode_stats, dim3(1), dim3(64), 0, s, tiles_split, tiles_exact, counts, tfound, flips, cap, cum);
   GM2_CHECK_LAUNCH();
 }
 
