@@ -793,9 +793,12 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   // forward tail (loss slot sums, output bias gradient, norm-ahead header) runs right in front of
   // it, on CUs dA5 no longer holds. (Rounds 3-4 had the tail in front of dW9 right after the first
   // fork: starved beside dA5 for ~360 us, it was what held dW9 back; profiles/r04_fwd_tail_after_dw9.txt.)
+  // Default 2 with dW9 on its capped grid (GM2_OPT_GRID_CAP bit 1, 215 workgroups x 4 tiles): the
+  // chain's BatchNorm partial and apply run before dW9 takes 215 CUs, and 41 CUs stay with the
+  // chain -- 6 of 6 same-box pairs faster than 0 on the full grid (profiles/r05_dw9_cap_ab.txt).
   static const int dw9_at = [] {
     const char* e = std::getenv("GM2_DW9_AT");
-    return e ? std::max(0, std::atoi(e)) : 0;
+    return e ? std::max(0, std::atoi(e)) : 2;
   }();
   const hipStream_t s9 = sr ? w.s : c.s;
   bool dw9_done = false;

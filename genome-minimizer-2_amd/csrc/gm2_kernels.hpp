@@ -85,7 +85,7 @@ struct Options {
   int small_split = 1;   // GM2_OPT_SMALL_SPLIT  split-K of the chip-filling short-K 128-tile GEMMs
   int bn_epilogue = 1;   // GM2_OPT_BN_EPILOGUE  BatchNorm statistics in the GEMM store epilogue
   int small_waves = 8;   // GM2_OPT_SMALL_WAVES  waves of the 128x128 fp32-store tiles (4 or 8)
-  int grid_cap = 2;      // GM2_OPT_GRID_CAP     capped grids: 1 dW9, 2 dWe0, 4 recon
+  int grid_cap = 3;      // GM2_OPT_GRID_CAP     capped grids: 1 dW9, 2 dWe0, 4 recon
   int input_chunks = 1;  // GM2_OPT_INPUT_CHUNKS launches of the input-layer weight gradient (1 or 4)
   int sync_bn = 0;       // GM2_OPT_SYNC_BN      train-mode BatchNorm over every rank's rows (collective)
   int defer_adam = 0;    // GM2_OPT_DEFER_OUTPUT_ADAM  output-layer Adam update beside the next step's hidden

@@ -45,6 +45,71 @@ __global__ __launch_bounds__(256) void k_count_groups(const uint8_t* __restrict_
   if (lane == 0) counts[row] = cnt;
 }
 
+// The same count from whole-row reads: each workgroup first turns the groups into an LDS bit mask of
+// the single-position groups (one atomicOr per group; a position already in the mask -- a second
+// group on the same gene -- and every multi-position group go to an LDS list instead), then its
+// waves stream their rows with 16-byte loads: count = popcount(row AND mask) + the listed groups
+// evaluated as above. The same integer as k_count_groups; a row's ~300 scattered byte reads touched
+// nearly every line of the row anyway, now one coalesced pass reads it.
+constexpr int kCountRowsPerWg = 16;
+__global__ __launch_bounds__(256) void k_count_groups_rows(const uint8_t* __restrict__ bits, int64_t n, int64_t ldb,
+                                                         const int32_t* __restrict__ goff, int ngroups,
+                                                         const int32_t* __restrict__ pos, int32_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lmask[];  // [ldb / 4] words, then the list
+  const int nw = (int)(ldb / 4);
+  int* glist = (int*)(lmask + nw);
+  int* gcount = glist + ngroups;
+  for (int i = threadIdx.x; i < nw; i += 256) lmask[i] = 0u;
+  if (threadIdx.x == 0) *gcount = 0;
+  __syncthreads();
+  for (int g = threadIdx.x; g < ngroups; g += 256) {
+    const int k0 = goff[g], k1 = goff[g + 1];
+    GM2_DBG(k0 >= 0 && k0 <= k1, kDbgMaskPos);
+    if (k1 == k0) continue;  // (an empty group never counts)
+    if (k1 - k0 == 1) {
+      const int p = pos[k0];
+      GM2_DBG(p >= 0 && (int64_t)(p >> 3) < ldb, kDbgMaskPos);
+      const uint32_t bit = 1u << (p & 31);
+      if (!(atomicOr(&lmask[p >> 5], bit) & bit)) continue;
+    }
+    glist[atomicAdd(gcount, 1)] = g;
+  }
+  __syncthreads();
+  const int ng = *gcount, lane = threadIdx.x & 63;
+  const int64_t r1 = min(n, (int64_t)(blockIdx.x + 1) * kCountRowsPerWg);
+  for (int64_t row = (int64_t)blockIdx.x * kCountRowsPerWg + (threadIdx.x >> 6); row < r1; row += 4) {
+    const uint8_t* rb = bits + row * ldb;
+    const uint4* r = (const uint4*)rb;
+    const uint4* m = (const uint4*)lmask;
+    int c = 0;
+    // (four 16-byte loads per lane in flight before their first use)
+    for (int i0 = lane; i0 < nw / 4; i0 += 4 * 64) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = i0 + u * 64 < nw / 4 ? r[i0 + u * 64] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (i0 + u * 64 >= nw / 4) break;
+        const uint4 k = m[i0 + u * 64];
+        c += __builtin_popcount(v[u].x & k.x) + __builtin_popcount(v[u].y & k.y) +
+             __builtin_popcount(v[u].z & k.z) + __builtin_popcount(v[u].w & k.w);
+      }
+    }
+    for (int j = lane; j < ng; j += 64) {
+      const int g = glist[j];
+      int any = 0;
+      for (int k = goff[g]; k < goff[g + 1] && !any; ++k) {
+        const int p = pos[k];
+        GM2_DBG(p >= 0 && (int64_t)(p >> 3) < ldb, kDbgMaskPos);
+        any = (rb[p >> 3] >> (p & 7)) & 1;
+      }
+      c += any;
+    }
+    c = wave_sum_i(c);
+    if (lane == 0) counts[row] = c;
+  }
+}
+
 // popcount of each row (AND keep mask) -> out[row]; one wave per row, 16-byte loads
 __global__ __launch_bounds__(256) void k_row_popcount(const uint8_t* __restrict__ bits, int64_t n, int64_t ldb,
                                                     const uint8_t* __restrict__ keep, int64_t* __restrict__ out) {
@@ -130,8 +195,15 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ bit
 void launch_count_groups(const uint8_t* bits, int64_t n, int64_t ldb, const int32_t* goff, int64_t ngroups,
                          const int32_t* pos, int32_t* counts, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_count_groups, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, bits, n, ldb, goff, (int)ngroups,
-                     pos, counts);
+  // (whole-row form when the rows are 16-B pieces and the mask + list fit in 64 KB of LDS)
+  const int64_t lds = ldb + (ngroups + 1) * 4;
+  if ((ldb & 15) == 0 && (((uintptr_t)bits) & 15) == 0 && lds <= 64 * 1024) {
+    hipLaunchKernelGGL(k_count_groups_rows, dim3((unsigned)((n + kCountRowsPerWg - 1) / kCountRowsPerWg)), dim3(256),
+                       (unsigned)lds, s, bits, n, ldb, goff, (int)ngroups, pos, counts);
+  } else {
+    hipLaunchKernelGGL(k_count_groups, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, bits, n, ldb, goff,
+                       (int)ngroups, pos, counts);
+  }
   GM2_CHECK_LAUNCH();
 }
 

@@ -289,7 +289,8 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       hidden-layer GEMMs).
  *   GM2_OPT_GRID_CAP    bit 1 = the output-layer, bit 2 = the input-layer weight-gradient GEMM,
  *                       bit 4 = the output-layer loss GEMM runs on a capped grid (workgroups loop over tiles; same rounds, fewer CUs)
- *                       so the work beside it keeps CUs (default 2); 0 = one workgroup per tile.
+ *                       so the work beside it keeps CUs (default 3: both weight gradients); 0 = one
+ *                       workgroup per tile.
  *   GM2_OPT_INPUT_CHUNKS 1 (default) or 4: launches of the input-layer weight-gradient GEMM, one
  *                       per gradient bucket 2..5 (when H/4 is a multiple of 256; else 1). Same
  *                       results bit for bit; 4 lets a data-parallel exchange start early.
@@ -356,10 +357,12 @@ int gm2_workspace_join(void* ws, void* stream);
  *                           GM2_OPT_SAMPLE_SPLIT off, or the split path's preconditions)
  *   GM2_STAT_SPLIT_TILES / GM2_STAT_EXACT_TILES  output-layer tiles (256 x 256 split, 128 x 128 exact)
  *                           each kernel of the gated decode ran
- *   GM2_STAT_BAND_ELEMENTS  logits the gated decode found in the certified band |logit - T| <=
- *                           coef * ||a_r||_2 ||w_g||_2 and recomputed in fp64
+ *   GM2_STAT_BAND_ELEMENTS  logits the gated decode flagged in the certified band |logit - T| <=
+ *                           coef * ||a_r||_2 ||w_g||_2 (evaluated with the largest
+ *                           of 4 neighbouring rows' norms, so a small superset) and recomputed in fp64
  *   GM2_STAT_BAND_FLIPS     mask bits that recompute changed
- *   GM2_STAT_BAND_OVERFLOW  band elements beyond a call's list capacity (64 shards x 65,536), left as computed */
+ *   GM2_STAT_BAND_OVERFLOW  band elements beyond a call's list capacity (32 slots per split tile,
+ *                           then 64 shards x 65,536), left as computed */
 enum {
   GM2_STAT_SPLIT_DECODES = 1,
   GM2_STAT_EXACT_DECODES = 2,

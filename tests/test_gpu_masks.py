@@ -61,6 +61,39 @@ def test_count_essential_on_device_matches_reference(name):
     np.testing.assert_array_equal(count_essential_genes(pm, d), g[f"{name}_counts"])
 
 
+@pytest.mark.parametrize("G,N,ngroups", [(55039, 1000, 300), (1000, 130, 900), (4100, 70, 0)])
+def test_count_groups_whole_row_kernel(G, N, ngroups):
+    """gm2_mask_count_groups (whole-row form: single-position groups through an LDS bit mask, the
+    rest listed) == a numpy count of the reference's rule (a group counts when any of its positions
+    is set) with single-position groups on distinct and on shared genes, multi-position groups,
+    empty groups and positions at the row's last bits; G = 1000 with 900 groups puts most groups on
+    genes another group already holds."""
+    rng = np.random.Generator(np.random.PCG64(G + ngroups))
+    M = rng.random((N, G)) < 0.3
+    M[0] = True
+    M[1] = False
+    groups = []
+    for i in range(ngroups):
+        k = int(rng.integers(0, 4)) if i % 7 else 1
+        groups.append([int(x) for x in rng.integers(0, G, size=k)])
+    if ngroups:
+        groups[0] = [G - 1]
+        groups[1] = [G - 1]  # the same gene again
+        groups[2] = []
+    offs = np.concatenate([[0], np.cumsum([len(x) for x in groups])]).astype(np.int32)
+    pos = np.array([p for x in groups for p in x] or [0], dtype=np.int32)
+    want = np.zeros(N, dtype=np.int32)
+    for x in groups:
+        if x:
+            want += M[:, x].any(axis=1)
+    pm = PackedMasks.from_host(M, threshold=True)
+    counts = torch.zeros(N, dtype=torch.int32, device="cuda")
+    native.mask_count_groups(pm.bits, N, pm.bits.shape[1], torch.from_numpy(offs).cuda(), ngroups,
+                             torch.from_numpy(pos).cuda(), counts)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(counts.cpu().numpy(), want)
+
+
 def test_gene_index_csr_vs_numpy():
     rng = np.random.Generator(np.random.PCG64(5))
     M = rng.random((777, 4100)) < 0.3
