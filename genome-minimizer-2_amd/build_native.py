@@ -45,6 +45,10 @@ VARIANTS = {
                  flags=["-DGM2_DEBUG", "-g", "-fno-omit-frame-pointer", "-Xarch_host", "-fsanitize=address"],
                  link=["-Xarch_host", "-fsanitize=address"],
                  extra=[os.path.join(ROOT, "tools", "asan", "host_asan.cpp")]),
+    # the second build of a same-box A/B (tools/ab_lib.sh; GM2_LIB_PATH selects it; not part of
+    # build()): an experiment's code sits behind #ifdef GM2_AB
+    "ab": dict(build=os.path.join(HERE, "build_ab"), out=os.path.join(HERE, "gm2", "libgm2_ab.so"),
+               flags=["-DGM2_AB"], link=["-shared"]),
 }
 
 
