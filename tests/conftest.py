@@ -37,3 +37,21 @@ def _one_thread():
     torch.set_num_threads(1)
     yield
     torch.set_num_threads(n)
+
+
+@pytest.fixture(autouse=True)
+def _debug_build_flags(request):
+    """Under the debug build (GM2_LIB_PATH=.../libgm2_debug.so, the whole -m gpu suite run against
+    it): every kernel check of index data ORs a bit into a device flag word instead of trapping
+    (include/gm2_debug.h); after each GPU test the flags are read (and cleared) and must be 0."""
+    yield
+    if not os.environ.get("GM2_LIB_PATH", "").endswith("libgm2_debug.so") or "gpu" not in request.keywords:
+        return
+    import ctypes
+
+    import torch
+    from gm2 import native
+    torch.cuda.synchronize()
+    v = ctypes.c_uint(0)
+    native.check(native.lib().gm2_debug_flags(ctypes.byref(v)), "gm2_debug_flags")
+    assert v.value == 0, f"debug build: index check flags {v.value:#x} after {request.node.nodeid}"
