@@ -528,37 +528,44 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
     gps = n_all / dt
     n_dec = (n + chunk - 1) // chunk
     st = {k: v - st0[k] for k, v in m.decode_stats().items()}
-    # per 256 x 256 tile (genomes x genes) the gate ran the bf16x3 split (K' = 2H, three MFMAs per
-    # fragment pair) or, for the blocks whose bound exceeds 1e-3, exact fp32 (128 x 128 tiles, four
-    # per block); split_fraction = the share of blocks that ran split
-    blocks = st["split_tiles"] + st["exact_tiles"] / 4.0
+    # per 256 x 256 tile (genomes x genes) the gate ran one bf16 product over the rounded operands
+    # (single tier, K = H), the bf16x3 split (K' = 2H, three MFMAs per fragment pair) or, for the
+    # blocks whose bound exceeds both, exact fp32 (128 x 128 tiles, four per block); the fractions are
+    # shares of the blocks
+    blocks = st["single_tiles"] + st["split_tiles"] + st["exact_tiles"] / 4.0
+    single_frac = st["single_tiles"] / blocks if blocks else 0.0
     split_frac = st["split_tiles"] / blocks if blocks else 0.0
-    split = split_frac > 0.5
-    kflops = 2.0 * chunk * H * G * (3 if split else 1)  # executed by one full-chunk launch
-    # both output-layer kernels are launched per decode and each tile runs in the one its block's
-    # verdict picks: executed FLOPs (3 products per split element, 1 per exact element) and useful
-    # FLOPs (1 per element) over the time of every mask-kernel launch, against the bf16 peak when the
-    # split dominates (the exact kernel runs on the fp32 peak)
-    ach = 2.0 * n * H * G * (3 * split_frac + (1 - split_frac)) / (k_ms * 1e-3) / 1e12
+    exact_frac = max(0.0, 1.0 - single_frac - split_frac)
+    bf16 = single_frac + split_frac > 0.5
+    prod = 3 if split_frac > single_frac else 1  # products per element of the dominant bf16 tier
+    kflops = 2.0 * chunk * H * G * (prod if bf16 else 1)  # executed by one full-chunk launch
+    # every output-layer kernel is launched per decode and each tile runs in the one its block's
+    # verdict picks: executed FLOPs (1 product per single element, 3 per split element, 1 per exact
+    # element) and useful FLOPs (1 per element) over the time of every mask-kernel launch, against
+    # the bf16 peak when the bf16 tiers dominate (the exact kernel runs on the fp32 peak)
+    ach = 2.0 * n * H * G * (single_frac + 3 * split_frac + exact_frac) / (k_ms * 1e-3) / 1e12
     useful = 2.0 * n * H * G / (k_ms * 1e-3) / 1e12
-    peak = PEAK_BF16_TFLOPS if split else PEAK_F32_TFLOPS
+    peak = PEAK_BF16_TFLOPS if bf16 else PEAK_F32_TFLOPS
     # the packed masks that reached the host are the decode's: spot-check the last chunk on device
     last = (n - 1) // chunk * chunk
     assert torch.equal(host_bits[last:n].to(dev), dbits[((n - 1) // chunk) & 1][:n - last])
     # (the bf16x3 kernel is k_gemm_mask<Cfg<256, ...>, unsigned short, true>, the exact one <..., float>)
-    traffic, traffic_src = pmc_traffic(a, "k_gemm_mask<Cfg<256" if split else "k_gemm_mask<Cfg<128")
+    traffic, traffic_src = pmc_traffic(a, "k_gemm_mask<Cfg<256" if bf16 else "k_gemm_mask<Cfg<128")
     return {"genomes_per_s": round(gps, 1), "preset": "v1", "genomes": n_all, "n_gpus": world, "chunk": chunk,
             "checkpoint": (f"v1 trained {a.sample_train_epochs} epochs (lr 1e-3, batch 4096, L1 0.01) on the synthetic "
                            f"{a.strains}x{G} matrix" if trained is not None else "untrained (xavier init)"),
-            "split_fraction": round(split_frac, 4), "split_tiles": st["split_tiles"], "exact_tiles": st["exact_tiles"],
+            "single_fraction": round(single_frac, 4), "split_fraction": round(split_frac, 4),
+            "single_tiles": st["single_tiles"], "split_tiles": st["split_tiles"], "exact_tiles": st["exact_tiles"],
             "band_elements": st["band_elements"], "band_flips": st["band_flips"], "band_overflow": st["band_overflow"],
-            "dtype": "bf16x3 (fp32 split hi/lo, output layer) + f32 (hidden layers)" if split else "f32",
+            "dtype": ("bf16 (output layer, rounded operands; fp64 band recompute) + f32 (hidden layers)" if bf16 and prod == 1
+                      else "bf16x3 (fp32 split hi/lo, output layer) + f32 (hidden layers)" if bf16 else "f32"),
             "mask_format": "packed bits (numpy packbits, little)", "includes": "z draw, decode, threshold, pack, "
             "essential-gene counts, D2H of packed masks + counts to pinned host memory",
             "decode_tflops": round(gps * decode_flops_per_genome(G, H, L) / 1e12, 2),
             "mean_essential_present": round(float(host_cnt.float().mean()), 2),
-            "roofline": {"bound": "mfma", "kernel": "k_gemm_mask<bf16, 256x256 pp> (K' = 2H, 3 products)" if split
-                         else "k_gemm_mask<f32>", "achieved": round(ach, 2),
+            "roofline": {"bound": "mfma", "kernel": ("k_gemm_mask<bf16, 256x256 pp> (K = H, 1 product)" if bf16 and prod == 1
+                                                     else "k_gemm_mask<bf16, 256x256 pp> (K' = 2H, 3 products)" if bf16
+                                                     else "k_gemm_mask<f32>"), "achieved": round(ach, 2),
                          "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                          "useful_tflops": round(useful, 2), "useful_frac": round(useful / peak, 4),
                          "flops_per_launch": kflops,

@@ -92,12 +92,13 @@ Dims make_dims(const gm2_dims* d, int gpad = kTile) {
 //   [16, 48)   split-kernel tiles of this call (sharded), [48, 80) exact-kernel tiles
 //   [80, 144)  band elements this call put in each list shard, 144 bits its recompute flipped
 //   [160, 224) band elements this call put in tile slots (sharded)
-//   [224, ...) block maxima of the row norms: activations (roundup(n, 256) / 256), then weights
-// Words [16, 224 + blocks) are zeroed at the start of every gated decode.
+//   [224, 256) single-product-kernel tiles of this call
+//   [256, ...) block maxima of the row norms: activations (roundup(n, 256) / 256), then weights
+// Words [16, 256 + blocks) are zeroed at the start of every gated decode.
 struct DecodeCtl {
   static constexpr int kCum = 0, kTilesSplit = 16, kTilesExact = 48, kCounts = 80, kFlips = 80 + kBandShards,
-                       kTileFound = 160, kBlk = 160 + kBandShards;
-  static_assert(kFlips < kTileFound, "control block");
+                       kTileFound = 160, kTilesSingle = 160 + kBandShards, kBlk = kTilesSingle + kSplitShards;
+  static_assert(kFlips < kTileFound && kBlk == 256, "control block");
 };
 
 struct Layout {
@@ -119,6 +120,7 @@ struct Layout {
   // their row norms (s3rn, s3cn), the control block (DecodeCtl), the band list and the split
   // kernel's per-tile band slots (s3tlist [tiles][kBandTileSlots] (row, gene), s3tcount [tiles])
   int64_t s3a, s3w, s3rn, s3cn, s3ctl, s3band, s3tlist, s3tcount;
+  int64_t s3a1, s3w1;          // the single-product tier's operands: the hi parts alone, [rows][H] bf16
   int64_t adamscal;            // scalar block of a queued output-layer Adam update
   int64_t ridx;                // zero-copy rows: int32 [roundup(Bm, 256)] resident-matrix row per batch row
 };
@@ -204,6 +206,8 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   const int64_t s3tiles = split3 ? (round_up(Bm, 2 * kTile) / 256) * (round_up(d.G, 2 * kTile) / 256) : 0;
   o.s3tlist = take(s3tiles * kBandTileSlots * 8);
   o.s3tcount = take(s3tiles * 4);
+  o.s3a1 = take(split3 ? round_up(Bm, 2 * kTile) * H * 2 : 0);
+  o.s3w1 = take(split3 ? round_up(d.G, 2 * kTile) * H * 2 : 0);
   o.adamscal = take(GM2_NUM_SCALARS * 4);
   o.ridx = take(round_up(Bm, 2 * kTile) * 4);
   o.total = cur;
@@ -987,15 +991,20 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
   const float* w9 = prm + d.off[D9W];
   HIP_OK(hipMemsetAsync(ctl + DecodeCtl::kTilesSplit, 0, (DecodeCtl::kBlk - DecodeCtl::kTilesSplit + Bq / 256 + Gq / 256) * 4,
                         c.s));
-  launch_split3(c.f(l.A[5]), H, n, Bq, H, a3, 2 * H, rn, ablk, c.s);
-  launch_split3(w9, H, G, Gq, H, w3, 2 * H, cn, wblk, c.s);
+  const bool single = opts().sample_single != 0 && H % 64 == 0;  // (the single GEMM's K = H: 64-wide K-tiles)
+  bf16_t* a1 = (bf16_t*)(c.ws + l.s3a1);
+  bf16_t* w1 = (bf16_t*)(c.ws + l.s3w1);
+  launch_split3(c.f(l.A[5]), H, n, Bq, H, a3, 2 * H, rn, ablk, c.s, single ? a1 : nullptr);
+  launch_split3(w9, H, G, Gq, H, w3, 2 * H, cn, wblk, c.s, single ? w1 : nullptr);
   if (c.st) c.st->decode_cum = (const unsigned long long*)(ctl + DecodeCtl::kCum);
-  // band half-widths per unit ||a_r|| ||w_g|| (MaskBand): split tiles also carry the split's own error
-  // and the fp32 accumulation of its 3H products, exact tiles the fp32 accumulation of H products;
-  // both, the reference's own fp32 accumulation of H products
+  // band half-widths per unit ||a_r|| ||w_g|| (MaskBand): single tiles carry the operands' bf16
+  // rounding and the fp32 accumulation of their H products, split tiles the split's own error and the
+  // fp32 accumulation of its 3H products, exact tiles the fp32 accumulation of H products; all, the
+  // reference's own fp32 accumulation of H products
   const double gH = band_gamma((double)H), g3H = band_gamma(3.0 * H);
-  // (the split kernel's tiles keep their band elements in their own slots; the exact kernel's, rare,
-  // go to the shards)
+  // (the split and single kernels' tiles keep their band elements in their own slots -- the tile
+  // grid is the same and each tile runs in one of them; the exact kernel's, rare, go to the shards)
+  const int tiles = (Bq / 256) * (Gq / 256);
   MaskBand bs{rn, cn, (float)(kSplitUnit * 1.01 + g3H + gH), ctl + DecodeCtl::kCounts, list, kBandShardCap};
   MaskBand be = bs;
   be.coef = (float)(2.0 * gH);
@@ -1003,16 +1012,34 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
   bs.tcount = (unsigned*)(c.ws + l.s3tcount);
   bs.tfound = ctl + DecodeCtl::kTileFound;
   bs.tslots = kBandTileSlots;
+  MaskBand b1 = bs;
+  b1.coef = (float)(kSingleUnit * 1.01 + 2.0 * gH);
+  b1.drop_overflow = 1;
+  b1.tiles_done = ctl + DecodeCtl::kTilesSingle;
+  HIP_OK(hipMemsetAsync(bs.tcount, 0, (size_t)tiles * 4, c.s));
+  const int on = single ? 1 : 0;
+  static const double single_bound = [] {  // (env GM2_SINGLE_BOUND: the tier's gate, for A/Bs)
+    const char* e = std::getenv("GM2_SINGLE_BOUND");
+    return e ? std::atof(e) : kSingleBound;
+  }();
   GemmArgs<bf16_t> g{a3, 2 * H, w3, 2 * H, n, G, 2 * H, Bq, Gq, 0};
-  launch_gemm_mask<bf16_t>(g, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
-                           true, MaskGate{ablk, wblk, 1, ctl + DecodeCtl::kTilesSplit}, bs);
+  const MaskGate gs{ablk, wblk, 1, ctl + DecodeCtl::kTilesSplit, on, single_bound};
+  if (single) {  // both bf16 tiers in one launch (a single tile whose band overflows re-runs as split)
+    GemmArgs<bf16_t> g1{a1, H, w1, H, n, G, H, Bq, Gq, 0};
+    launch_gemm_mask_tiered(g1, g, prm + d.off[D9B], mask, ldm, bits, ldb, c.s,
+                            MaskGate{ablk, wblk, 3, ctl + DecodeCtl::kTilesSingle, on, single_bound}, b1, gs, bs);
+  } else {
+    launch_gemm_mask<bf16_t>(g, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
+                             true, gs, bs);
+  }
   GemmArgs<float> ge{c.f(l.A[5]), H, c.f(l.sD3), H, n, G, H, (int)round_up(n, kTile), (int)d.Gp, 0};
   launch_gemm_mask<float>(ge, prm + d.off[D9B], mask, ldm, nullptr, 0, c.s, bits, ldb, nullptr, nullptr, 0, 0.5f,
-                          false, MaskGate{ablk, wblk, 2, ctl + DecodeCtl::kTilesExact}, be);
-  launch_band_fix(bs, (Bq / 256) * (Gq / 256), c.f(l.A[5]), H, w9, H, prm + d.off[D9B], H, bits, ldb, mask, ldm,
+                          false, MaskGate{ablk, wblk, 2, ctl + DecodeCtl::kTilesExact, on, single_bound}, be);
+  launch_band_fix(bs, tiles, c.f(l.A[5]), H, w9, H, prm + d.off[D9B], H, bits, ldb, mask, ldm,
                   ctl + DecodeCtl::kFlips, c.s);
-  launch_decode_stats(ctl + DecodeCtl::kTilesSplit, ctl + DecodeCtl::kTilesExact, ctl + DecodeCtl::kCounts,
-                      ctl + DecodeCtl::kTileFound, ctl + DecodeCtl::kFlips, kBandShardCap, (unsigned long long*)(ctl + DecodeCtl::kCum), c.s);
+  launch_decode_stats(ctl + DecodeCtl::kTilesSplit, ctl + DecodeCtl::kTilesExact, ctl + DecodeCtl::kTilesSingle,
+                      ctl + DecodeCtl::kCounts, ctl + DecodeCtl::kTileFound, ctl + DecodeCtl::kFlips, kBandShardCap,
+                      (unsigned long long*)(ctl + DecodeCtl::kCum), c.s);
   return true;
 }
 
@@ -1595,7 +1622,8 @@ int gm2_workspace_stat(void* ws, int key, int64_t* value) {
       case GM2_STAT_EXACT_TILES:
       case GM2_STAT_BAND_ELEMENTS:
       case GM2_STAT_BAND_FLIPS:
-      case GM2_STAT_BAND_OVERFLOW: {
+      case GM2_STAT_BAND_OVERFLOW:
+      case GM2_STAT_SINGLE_TILES: {
         unsigned long long cum[8] = {};  // (the gated decodes' device counters: waits for the device)
         if (st.decode_cum) {
           HIP_OK(hipDeviceSynchronize());
@@ -1608,6 +1636,7 @@ int gm2_workspace_stat(void* ws, int key, int64_t* value) {
           case GM2_STAT_EXACT_TILES: *value = (int64_t)cum[1]; break;
           case GM2_STAT_BAND_ELEMENTS: *value = (int64_t)cum[2]; break;
           case GM2_STAT_BAND_FLIPS: *value = (int64_t)cum[3]; break;
+          case GM2_STAT_SINGLE_TILES: *value = (int64_t)cum[7]; break;
           default: *value = (int64_t)cum[4]; break;
         }
         break;
@@ -1654,7 +1683,7 @@ int gm2_debug_check_layout(const gm2_dims* d, int precision, int64_t* n_regions,
     const int64_t named[] = {o.sE0, o.sE1, o.sE2, o.sHD, o.sD0, o.sD1, o.sD2, o.sD3, o.X, o.XB, o.HD, o.Z, o.dL,
                              o.slabs, o.side_slabs, o.DA, o.dH, o.AT5, o.dYT0, o.bnpart, o.colpart, o.losspart,
                              o.klpart, o.gradpart, o.colbwd, o.nahdr, o.nasq, o.clip, o.scal0, o.X1, o.XB1, o.syncb,
-                             o.s3a, o.s3w, o.s3rn, o.s3cn, o.s3ctl, o.s3band, o.s3tlist, o.s3tcount,
+                             o.s3a, o.s3w, o.s3rn, o.s3cn, o.s3ctl, o.s3band, o.s3tlist, o.s3tcount, o.s3a1, o.s3w1,
                              o.adamscal, o.ridx};
     auto known = [&](int64_t off) {
       for (const auto& x : r)

@@ -1234,17 +1234,10 @@ struct MaskOut {
 };
 
 // The certified band (MaskBand): the tile's row norms and column norms go to LDS past the staging
-// ring before the main loop (whose barriers order them before the epilogue), with the tile's slot
-// counter after them. Per element the epilogues add one compare, OR-ed into a wave mask by its
-// ballot (|d| <= rmax * ce + eb, MaskBand); a wave whose mask is non-zero re-walks its fragments
-// and appends the flagged (row, gene) pairs (rare: ~2 per tile of a trained model).
-template <class C>
-__device__ __forceinline__ void band_stage(const MaskBand& b, const TileXY& tl, char* smem) {
-  float* brn = (float*)(smem + C::LDS);
-  for (int i = threadIdx.x; i < C::BM + C::BN; i += C::NT)
-    brn[i] = i < C::BM ? b.rn[tl.m0 + i] : b.cn[tl.n0 + i - C::BM];
-  if (threadIdx.x == 0) ((unsigned*)brn)[C::BM + C::BN] = 0u;
-}
+// ring after the main loop (mask_tile), with the tile's slot counter after them. Per element the
+// epilogues add one compare (|d| <= rmax * ce + eb, MaskBand) and its wave ballot: the packed-bits
+// epilogue appends a position's flagged (row, gene) pairs right there (a uniform branch, rarely
+// taken); the u8 epilogue ORs the ballots and a flagged wave re-walks its fragments.
 template <class C>
 constexpr int band_lds_bytes() { return (C::BM + C::BN) * 4 + 16; }
 
@@ -1301,22 +1294,48 @@ __device__ __forceinline__ void band_walk(const MaskBand& b, int tile, char* sme
       if (i < b.cap) shard[i] = e;
     } else if (i < (unsigned)b.tslots) {
       b.tlist[(size_t)tile * b.tslots + i] = e;
-    } else {  // past the tile's slots: the shard (rare)
+    } else if (!b.drop_overflow) {  // past the tile's slots: the shard (rare)
       const unsigned k = atomicAdd(b.counts + sh, 1u);
       if (k < b.cap) shard[k] = e;
     }
   });
 }
+// one fragment position's band elements (bal = the wave's ballot of `in`; wave-uniform call): one
+// reservation for all of them, as band_walk's visitor
+template <class C>
+__device__ __forceinline__ void band_add(const MaskBand& b, int tile, char* smem, int lane, uint64_t bal, bool in,
+                                         int r, int gcol) {
+  unsigned* lcount = (unsigned*)(smem + C::LDS) + C::BM + C::BN;
+  const int sh = blockIdx.x % kBandShards;
+  const unsigned pre = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+  unsigned base = 0;
+  if (lane == 0) base = atomicAdd(b.tslots ? lcount : b.counts + sh, (unsigned)__popcll(bal));
+  const unsigned i = __shfl(base, 0, 64) + pre;
+  if (!in) return;
+  const uint2 e = make_uint2((unsigned)r, (unsigned)gcol);
+  uint2* shard = b.list + (size_t)sh * b.cap;
+  if (!b.tslots) {
+    if (i < b.cap) shard[i] = e;
+  } else if (i < (unsigned)b.tslots) {
+    b.tlist[(size_t)tile * b.tslots + i] = e;
+  } else if (!b.drop_overflow) {
+    const unsigned k = atomicAdd(b.counts + sh, 1u);
+    if (k < b.cap) shard[k] = e;
+  }
+}
+
 // after the epilogue's barrier: the tile's slot count
 template <class C>
 __device__ __forceinline__ void band_close(const MaskBand& b, int tile, char* smem) {
   if (!b.tslots || threadIdx.x != 0) return;
-  const unsigned n = min(((const unsigned*)(smem + C::LDS))[C::BM + C::BN], (unsigned)b.tslots);
+  const unsigned n = ((const unsigned*)(smem + C::LDS))[C::BM + C::BN];
   b.tcount[tile] = n;
-  if (n) atomicAdd(b.tfound + blockIdx.x % kBandShards, n);
+  if (b.drop_overflow && n > (unsigned)b.tslots) return;  // (re-run by the split kernel, counted there)
+  if (n) atomicAdd(b.tfound + blockIdx.x % kBandShards, min(n, (unsigned)b.tslots));
+  if (b.tiles_done) atomicAdd(b.tiles_done + blockIdx.x % kSplitShards, 1u);
 }
 
-template <class C, typename T, bool PP, bool BITS>
+template <class C, typename T, bool PP, bool BITS, bool S3>
 __device__ __forceinline__ void mask_tile(const TileXY tl, const GemmArgs<T>& g, const float* __restrict__ bias,
                                           const MaskOut& o, char* smem);
 
@@ -1324,20 +1343,17 @@ __device__ __forceinline__ void mask_tile(const TileXY tl, const GemmArgs<T>& g,
 // hi.lo + lo.hi over operands split by launch_split3, K' = 2H, decode_split3). LOOP (gated 128 x
 // 128 launches, usually the complement of the split kernel with few tiles to run): a grid of a few
 // workgroups per CU loops over the tiles t, t + grid, ... instead of one workgroup per tile.
-template <class C, typename T, bool PP = false, bool BITS = false, bool LOOP = false>
+template <class C, typename T, bool PP = false, bool BITS = false, bool LOOP = false, bool S3 = true>
 __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float* __restrict__ bias, MaskOut o) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tm = g.Mp / C::BM, tn = g.Np / C::BN, ntile = tm * tn;
   if constexpr (!LOOP) {
     const TileXY tl = tile_of<C>(tm, tn);
     if (o.gate.run) {  // the verdict of the tile's 256 x 256 block (uniform per workgroup)
-      if (split_tile_ok(o.gate, tl.m0, tl.n0) != (o.gate.run == 1)) {
-        if (o.band.tslots && threadIdx.x == 0) o.band.tcount[tl.t] = 0u;
-        return;
-      }
+      if (tile_level(o.gate, tl.m0, tl.n0) != o.gate.run) return;  // (tcount: zeroed by the caller)
       if (threadIdx.x == 0) atomicAdd(o.gate.tiles + blockIdx.x % kSplitShards, 1u);
     }
-    mask_tile<C, T, PP, BITS>(tl, g, bias, o, smem);
+    mask_tile<C, T, PP, BITS, S3>(tl, g, bias, o, smem);
   } else {
     static_assert(!PP && !BITS, "tile loop: the 128 x 128 kernel");
     // the workgroup's tiles t0 + k G: their gate verdicts NT at a time, in parallel (one ballot word
@@ -1350,7 +1366,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
       bool run = false;
       if (t < ntile) {
         const TileXY tl = tile_at<C>(t, tm, tn, 0);
-        run = !o.gate.run || split_tile_ok(o.gate, tl.m0, tl.n0) == (o.gate.run == 1);
+        run = !o.gate.run || tile_level(o.gate, tl.m0, tl.n0) == o.gate.run;
       }
       const uint64_t bw = __ballot(run);
       if (lane == 0) vm[wid] = bw;
@@ -1366,7 +1382,7 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
           m &= m - 1;
           ++nrun;
           __syncthreads();  // (the previous tile's epilogue is done with LDS)
-          mask_tile<C, T, PP, BITS>(tile_at<C>(t0 + (kb + w * 64 + i) * G, tm, tn, 0), g, bias, o, smem);
+          mask_tile<C, T, PP, BITS, S3>(tile_at<C>(t0 + (kb + w * 64 + i) * G, tm, tn, 0), g, bias, o, smem);
         }
       }
       if (o.gate.run && nrun && threadIdx.x == 0) atomicAdd(o.gate.tiles + blockIdx.x % kSplitShards, nrun);
@@ -1374,18 +1390,50 @@ __global__ __launch_bounds__(C::NT) void k_gemm_mask(GemmArgs<T> g, const float*
   }
 }
 
-template <class C, typename T, bool PP, bool BITS>
+// The tiered output layer (GM2_OPT_SAMPLE_SINGLE): one 256x256 workgroup per tile takes its block's
+// verdict -- exact tiles return at once (the exact kernel's), single-product tiles run one bf16
+// product over the rounded operands (o1: K = H, the wide band, overflow dropped) and, when their band
+// overflowed its slots, the same tile again as bf16x3 (o3) in place; split tiles run bf16x3 alone.
+// One launch for both bf16 tiers: no second grid of workgroups that mostly exit.
+template <class C, typename T, bool BITS>
+__global__ __launch_bounds__(C::NT) void k_gemm_mask_tiered(GemmArgs<T> g1, GemmArgs<T> g3,
+                                                            const float* __restrict__ bias, MaskOut o1, MaskOut o3) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const TileXY tl = tile_of<C>(g3.Mp / C::BM, g3.Np / C::BN);
+  const int lv = tile_level(o3.gate, tl.m0, tl.n0);
+  if (lv == 2) return;
+  if (lv == 3) {
+    mask_tile<C, T, true, BITS, false>(tl, g1, bias, o1, smem);
+    __syncthreads();  // (band_close's count in LDS, read by every thread)
+    if (((const unsigned*)(smem + C::LDS))[C::BM + C::BN] <= (unsigned)o1.band.tslots) return;  // (counted)
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicAdd(o3.gate.tiles + blockIdx.x % kSplitShards, 1u);
+  mask_tile<C, T, true, BITS, true>(tl, g3, bias, o3, smem);
+}
+
+template <class C, typename T, bool PP, bool BITS, bool S3>
 __device__ __forceinline__ void mask_tile(const TileXY tl, const GemmArgs<T>& g, const float* __restrict__ bias,
                                           const MaskOut& o, char* smem) {
   const bool bchk = o.band.rn != nullptr;
-  if (bchk) band_stage<C>(o.band, tl, smem);
+  // the tile's row and column norms (one per thread: NT = BM + BN), loaded before the main loop and
+  // staged to LDS after it (its first counted wait covers the load; no stall in front of the loop)
+  static_assert(C::NT == C::BM + C::BN, "one norm per thread");
+  float nrm = 0.f;
+  if (bchk) nrm = threadIdx.x < C::BM ? o.band.rn[tl.m0 + threadIdx.x] : o.band.cn[tl.n0 + threadIdx.x - C::BM];
   const float* brn = (const float*)(smem + C::LDS);  // [BM] row norms, then [BN] column norms
   f32x4 acc[C::FM][C::FN];
   if constexpr (PP) {
     static_assert(std::is_same_v<C, Big> && sizeof(T) == 2, "ping-pong: 256x256 bf16");
-    mainloop_pp<true, true, 0, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+    // (S3: the split's K' = 2H form; else one product over K = H, the single-product tier)
+    mainloop_pp<true, true, 0, S3>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
   } else {
     mainloop<C, T, true, true>(g.P, g.ldp, g.Q, g.ldq, tl.m0, tl.n0, 0, g.K / E<T>::KT, smem, acc);
+  }
+  if (bchk) {
+    ((float*)(smem + C::LDS))[threadIdx.x] = nrm;
+    if (threadIdx.x == 0) ((unsigned*)(smem + C::LDS))[C::BM + C::BN] = 0u;
+    __syncthreads();
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   const BandCols<C> bc(bias, brn, o.band, bchk, tl.n0, g.N, lane, wn);
@@ -1407,35 +1455,22 @@ __device__ __forceinline__ void mask_tile(const TileXY tl, const GemmArgs<T>& g,
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           uint64_t rb = 0;
+          const int r = tl.m0 + wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
+          const bool rok = r < g.M;
 #pragma unroll
           for (int ni = 0; ni < C::FN; ++ni) {
             const float d = acc[mi][ni][j] + bc.bt[ni];
             const uint64_t bal = __ballot(d > 0.f);
             rb |= ((bal >> sh) & 0xFFFFull) << (16 * ni);
-            bandw |= __ballot(fabsf(d) <= e[ni]);
+            // the band elements of this position appended at once (a uniform branch, rarely taken)
+            const bool inb = fabsf(d) <= e[ni] && rok;
+            const uint64_t bb = __ballot(inb);
+            if (bb) band_add<C>(o.band, tl.t, smem, lane, bb, inb, r, tl.n0 + wn * C::WTN + ni * 16 + (lane & 15));
           }
           if (lane < 4)
             *(uint64_t*)(smem + (wm * C::WTM + mi * 16 + 4 * lane + j) * (C::BN / 8) + wn * (C::WTN / 8)) = rb;
           __builtin_amdgcn_sched_barrier(0);  // (one row quad at a time: the ballots' SGPR pairs stay few)
         }
-      }
-      if (bandw) {  // append this wave's band elements (unrolled: acc stays in registers)
-        band_walk<C>(o.band, tl.t, smem, lane, [&](auto&& visit) {
-#pragma unroll
-          for (int mi = 0; mi < C::FM; ++mi) {
-            float e[C::FN];
-            bc.widths(brn, bchk, wm * C::WTM + mi * 16 + 4 * (lane >> 4), e);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int r = tl.m0 + wm * C::WTM + mi * 16 + 4 * (lane >> 4) + j;
-#pragma unroll
-              for (int ni = 0; ni < C::FN; ++ni) {
-                const float d = acc[mi][ni][j] + bc.bt[ni];
-                visit(fabsf(d) <= e[ni] && r < g.M, r, tl.n0 + wn * C::WTN + ni * 16 + (lane & 15));
-              }
-            }
-          }
-        });
       }
       __syncthreads();
       band_close<C>(o.band, tl.t, smem);
@@ -1953,11 +1988,37 @@ bool gemm_idx_ok(const GemmArgs<T>& g) {
   return kps <= kMaxIdxRows;  // (Q k-rows: a split's k-rows in the table)
 }
 
+void launch_gemm_mask_tiered(const GemmArgs<bf16_t>& g1, const GemmArgs<bf16_t>& g3, const float* bias, uint8_t* mask,
+                             int64_t ldm, uint8_t* bits, int64_t ldb, hipStream_t s, MaskGate gate1, MaskBand band1,
+                             MaskGate gate3, MaskBand band3) {
+  check_gemm(g1, 256);
+  check_gemm(g3, 256);
+  if (g1.Mp != g3.Mp || g1.Np != g3.Np || g1.Mp % 256 || g1.Np % 256 || g1.K % 64 || g3.K % 64)
+    throw Gm2Error("tiered mask: the two GEMMs' tile grids differ");
+  if (bits && ((ldb & 15) || (((uintptr_t)bits) & 15) || ldb * 8 < g3.N))
+    throw Gm2Error("mask bits: row pitch %lld must be a multiple of 16 bytes covering the padded genes", (long long)ldb);
+  if (!band1.rn || !band3.rn || !band1.tslots || !band3.tslots || !band1.drop_overflow || !gate3.run)
+    throw Gm2Error("tiered mask: both bands with tile slots (the single tier's dropping its overflow) and the gate");
+  const MaskOut o1{mask, ldm, bits, ldb, nullptr, 0, nullptr, nullptr, 0, 0.5f, gate1, band1};
+  const MaskOut o3{mask, ldm, bits, ldb, nullptr, 0, nullptr, nullptr, 0, 0.5f, gate3, band3};
+  constexpr int lds = Big::LDS + band_lds_bytes<Big>();
+  const dim3 grid((g3.Mp / 256) * (g3.Np / 256));
+  TimedLaunch tl(kKcMask, s);
+  auto go = [&](auto kern) {
+    ensure_lds_attr((const void*)kern, lds);
+    hipLaunchKernelGGL(kern, grid, dim3(Big::NT), lds, s, g1, g3, bias, o1, o3);
+  };
+  if (bits && !mask) go(k_gemm_mask_tiered<Big, bf16_t, true>);
+  else go(k_gemm_mask_tiered<Big, bf16_t, false>);
+  GM2_CHECK_LAUNCH();
+}
+
 template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs, int64_t ldpr,
                       hipStream_t s, uint8_t* bits, int64_t ldb, int* counts, const uint32_t* xbits, int64_t ldxb,
-                      float thr, bool big, MaskGate gate, MaskBand band) {
+                      float thr, bool big, MaskGate gate, MaskBand band, bool single) {
   check_gemm(g, big ? 256 : 128);
+  if (single && !big) throw Gm2Error("mask: the single-product form is the 256x256 kernel");
   // (the 256-column tiles may reach past the row pitch: their bits stores stop at ldb, past G)
   if (bits && ((ldb & 15) || (((uintptr_t)bits) & 15) || ldb * 8 < (big ? g.N : g.Np)))
     throw Gm2Error("mask bits: row pitch %lld must be a multiple of 16 bytes covering the padded genes", (long long)ldb);
@@ -1976,12 +2037,17 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
       constexpr int lds_max = Big::LDS + band_lds_bytes<Big>();
       const int lds = Big::LDS + band_lds;
       const dim3 grid((g.Mp / 256) * (g.Np / 256));
-      if (bits && !mask && !probs && !counts && thr == 0.5f) {  // packed bits only: ballot epilogue
-        ensure_lds_attr((const void*)k_gemm_mask<Big, T, true, true>, lds_max);
-        hipLaunchKernelGGL((k_gemm_mask<Big, T, true, true>), grid, dim3(Big::NT), lds, s, g, bias, o);
+      auto go = [&](auto kern) {
+        ensure_lds_attr((const void*)kern, lds_max);
+        hipLaunchKernelGGL(kern, grid, dim3(Big::NT), lds, s, g, bias, o);
+      };
+      const bool ballot = bits && !mask && !probs && !counts && thr == 0.5f;  // packed bits only: ballot epilogue
+      if (single) {
+        if (ballot) go(k_gemm_mask<Big, T, true, true, false, false>);
+        else go(k_gemm_mask<Big, T, true, false, false, false>);
       } else {
-        ensure_lds_attr((const void*)k_gemm_mask<Big, T, true>, lds_max);
-        hipLaunchKernelGGL((k_gemm_mask<Big, T, true>), grid, dim3(Big::NT), lds, s, g, bias, o);
+        if (ballot) go(k_gemm_mask<Big, T, true, true>);
+        else go(k_gemm_mask<Big, T, true>);
       }
       GM2_CHECK_LAUNCH();
       return;
@@ -2022,10 +2088,10 @@ GM2_INST(bf16_t)
 #undef GM2_INST
 template void launch_gemm_mask<float>(const GemmArgs<float>&, const float*, uint8_t*, int64_t, float*, int64_t,
                                       hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float, bool,
-                                      MaskGate, MaskBand);
+                                      MaskGate, MaskBand, bool);
 template void launch_gemm_mask<bf16_t>(const GemmArgs<bf16_t>&, const float*, uint8_t*, int64_t, float*, int64_t,
                                        hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float, bool,
-                                       MaskGate, MaskBand);
+                                       MaskGate, MaskBand, bool);
 
 #ifdef GM2_DEBUG
 GM2_DBG_TAKE_FN(dbg_take_gemm)

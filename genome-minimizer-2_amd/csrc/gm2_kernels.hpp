@@ -92,6 +92,7 @@ struct Options {
                          //   layers on this many workgroups per CU (0 = not deferred)
   int grad_buckets = 1;  // GM2_OPT_GRAD_BUCKETS  record the gradient-bucket events (gm2_wait_grad_bucket)
   int sample_split = 1;  // GM2_OPT_SAMPLE_SPLIT  bf16x3 output layer of the sampling decode (bound permitting)
+  int sample_single = 1; // GM2_OPT_SAMPLE_SINGLE the single-product bf16 tier of that gate (bound permitting)
 };
 // validated edit of one option (throws on an unknown key or a bad value)
 void option_set(Options& o, int key, int value);
@@ -197,18 +198,28 @@ bool gemm_idx_ok(const GemmArgs<T>& g);
 constexpr double kSplitBound = 1e-3;
 constexpr double kSplitUnit = 4.62e-5;  // 3.02 x 2^-16, rounded up
 constexpr int kSplitShards = 32;        // tile counters, sharded by blockIdx % kSplitShards
-// Device-side choice between the split and the exact output layer, per tile (both kernels launched
-// over their full grids; a tile's workgroup runs only when the gate's verdict for its 256 x 256
-// block is its `run`: 1 split, 2 exact), counting the tiles it ran into tiles[blockIdx % 32]
+// The single-product tier (GM2_OPT_SAMPLE_SINGLE): one bf16 GEMM over the rounded operands (hi
+// only, K = H) errs per logit by at most kSingleUnit * ||a_r|| ||w_g|| * 1.01 (each operand rounded
+// to 8 significant bits: 2 x 2^-8 + 2^-16, rounded up). A tile takes it when kSingleUnit *
+// max ||a_r|| * max ||w_g|| * 1.01 <= kSingleBound: its certified band is then ~170x the split's,
+// i.e. more logits for the fp64 recompute, for a third of the split's MFMA work.
+constexpr double kSingleBound = 0.25;
+constexpr double kSingleUnit = 7.83e-3;
+// Device-side choice of the output layer per 256 x 256 tile (every kernel launched over its full
+// grid or a tile loop; a tile's workgroup runs only when the gate's verdict for its block is its
+// `run`: 1 split, 2 exact, 3 single), counting the tiles it ran into tiles[blockIdx % 32]
 struct MaskGate {
   const unsigned* ablk = nullptr;  // per 256-genome-row block: max ||a_r|| (fp32 bits)
   const unsigned* wblk = nullptr;  // per 256-gene block: max ||w_g|| (fp32 bits)
   int run = 0;
   unsigned* tiles = nullptr;
+  int single = 0;                  // the single-product tier is on
+  double single_bound = kSingleBound;
 };
-__device__ __forceinline__ bool split_tile_ok(const MaskGate& g, int m0, int n0) {
+__device__ __forceinline__ int tile_level(const MaskGate& g, int m0, int n0) {
   const double a = (double)__uint_as_float(g.ablk[m0 >> 8]), w = (double)__uint_as_float(g.wblk[n0 >> 8]);
-  return kSplitUnit * a * w * 1.01 <= kSplitBound;  // (NaN / inf: false, the exact path)
+  if (g.single && kSingleUnit * a * w * 1.01 <= g.single_bound) return 3;
+  return kSplitUnit * a * w * 1.01 <= kSplitBound ? 1 : 2;  // (NaN / inf: 2, the exact path)
 }
 // The certified band of the sampling decode (SURVEY.md 7 "Hard parts" (ii)): logits with
 // |l - T| <= coef * ||a_r|| * ||w_g|| (T = the mask threshold) may sit on either side of T in the
@@ -229,7 +240,7 @@ __device__ __forceinline__ bool split_tile_ok(const MaskGate& g, int m0, int n0)
 // counted (left as the kernel decided them).
 constexpr int kBandShards = 64;
 constexpr unsigned kBandShardCap = 1u << 16;  // entries per shard per decode call (64 x 64 K x 8 B = 32 MB)
-constexpr int kBandTileSlots = 32;            // per 256 x 256 split tile (a trained model: ~2 per tile)
+constexpr int kBandTileSlots = 256;           // per 256 x 256 tile (a trained model: ~2 per split, ~80 per single tile)
 struct MaskBand {
   const float* rn = nullptr;  // ||a_r|| per genome row (nullptr: no band check)
   const float* cn = nullptr;  // ||w_g|| per gene
@@ -238,11 +249,22 @@ struct MaskBand {
   uint2* list = nullptr;      // [kBandShards][cap] (row, gene)
   unsigned cap = 0;
   uint2* tlist = nullptr;     // [tiles][tslots] (row, gene), tile = TileXY::t of the launch's grid
-  unsigned* tcount = nullptr; // [tiles] entries in the tile's slots (every tile of the grid writes its own)
-  unsigned* tfound = nullptr; // [kBandShards] sum of tcount (statistics)
+  unsigned* tcount = nullptr; // [tiles] the tile's band count, of which min(count, tslots) in its slots
+                              // (zeroed by the caller; a tile's kernel writes its own)
+  unsigned* tfound = nullptr; // [kBandShards] sum of the slot entries (statistics)
   int tslots = 0;
+  // the single-product tier: a tile whose band exceeds its slots drops the rest (no shard entries)
+  // and is re-run as bf16x3 in place (k_gemm_mask_tiered); its tile is then counted as split
+  int drop_overflow = 0;
+  unsigned* tiles_done = nullptr;  // [kSplitShards] tiles completed with drop_overflow (statistics)
 };
 inline double band_gamma(double n) { return n * 0x1p-24 / (1.0 - n * 0x1p-24); }
+// the two bf16 tiers of the gated decode in one launch (gemm.hip k_gemm_mask_tiered): g1 / band1
+// the single product (K = H), g3 / band3 the bf16x3 split (K' = 2H), gate3 the verdicts (run 1) and
+// the split tiles' counter; gate1.tiles unused (band1.tiles_done counts the single tiles)
+void launch_gemm_mask_tiered(const GemmArgs<bf16_t>& g1, const GemmArgs<bf16_t>& g3, const float* bias, uint8_t* mask,
+                             int64_t ldm, uint8_t* bits, int64_t ldb, hipStream_t s, MaskGate gate1, MaskBand band1,
+                             MaskGate gate3, MaskBand band3);
 // k_band_fix over every shard's entries and every tile's slots: fp64 logit of (A[row], W[gene]) +
 // bias, mask bit = (float)logit > T (the correctly rounded fp32 logit against the reference's
 // threshold); packed bits (bits != nullptr) or u8 mask. flips: the bits it changed
@@ -250,9 +272,9 @@ void launch_band_fix(const MaskBand& band, int ntiles, const float* A, int64_t l
                      const float* bias, int H, uint8_t* bits, int64_t ldb, uint8_t* mask, int64_t ldm, unsigned* flips,
                      hipStream_t s);
 // one workgroup: the decode call's per-call counters -> the workspace's cumulative ones (DecodeCtl)
-void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* counts,
-                         const unsigned* tfound, const unsigned* flips, unsigned cap, unsigned long long* cum,
-                         hipStream_t s);
+void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* tiles_single,
+                         const unsigned* counts, const unsigned* tfound, const unsigned* flips, unsigned cap,
+                         unsigned long long* cum, hipStream_t s);
 
 // output layer + threshold (sampling / metrics): u8 mask, packed bits, probs, per-row (TP, FP, FN).
 // big (bf16 only): the bf16x3 split decode -- 256x256 ping-pong tiles over operands in
@@ -261,7 +283,7 @@ template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs,
                       int64_t ldpr, hipStream_t s, uint8_t* bits = nullptr, int64_t ldb = 0, int* counts = nullptr,
                       const uint32_t* xbits = nullptr, int64_t ldxb = 0, float thr = 0.5f, bool big = false,
-                      MaskGate gate = {}, MaskBand band = {});
+                      MaskGate gate = {}, MaskBand band = {}, bool single = false);
 
 // ---- kernels.hip ----
 constexpr int kBnRowChunk = 128;  // rows per BatchNorm partial-statistics chunk
@@ -290,7 +312,7 @@ void launch_bn_bwd_partial(const float* dslabs, int S, int64_t slab, const float
 // 2-norm (rounded up; 0 for pad rows), blk[r / 256] = max of rn over each 256-row block (fp32 bits,
 // atomic max: zero it first). rows_pad % 256 == 0.
 void launch_split3(const float* X, int64_t ldx, int rows, int rows_pad, int K, bf16_t* out, int64_t ldo, float* rn,
-                   unsigned* blk, hipStream_t s);
+                   unsigned* blk, hipStream_t s, bf16_t* out1 = nullptr);
 // dst[c][r] = src[r][c] for an R x Cn block (multiples of 64)
 template <typename T>
 void launch_transpose(const T* src, int64_t lds_, int R, int Cn, T* dst, int64_t ldd, hipStream_t s);

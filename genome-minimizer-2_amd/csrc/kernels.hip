@@ -1060,7 +1060,7 @@ __global__ __launch_bounds__(256) void k_bn_sync_running(const double* __restric
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_split3(const float* __restrict__ X, int64_t ldx, int rows, int K,
                                               bf16_t* __restrict__ out, int64_t ldo, float* __restrict__ rn,
-                                              unsigned* __restrict__ blk) {
+                                              unsigned* __restrict__ blk, bf16_t* __restrict__ out1) {
   __shared__ float wmax[4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float mx = 0.f;
@@ -1090,6 +1090,7 @@ __global__ __launch_bounds__(256) void k_split3(const float* __restrict__ X, int
       bf16_t* o = out + (int64_t)r * ldo + 2 * (k0 & ~31) + (k0 & 31);
       *(uint4*)(o) = hv;
       *(uint4*)(o + 32) = lv;
+      if (out1) *(uint4*)(out1 + (int64_t)r * K + k0) = hv;  // (the single-product tier's operand: hi only)
     }
     // (the bound uses the norm rounded up: sqrt of a sum of squares carried in fp32 is within a few
     // ulps of the true norm; x 1.0001 covers that with room)
@@ -1198,74 +1199,99 @@ __global__ __launch_bounds__(256) void k_exchange_unpack(const bf16_t* __restric
 // Packed bits are set / cleared with 32-bit atomics (several waves may share a word), u8 masks by
 // byte stores. flips counts the bits the recompute changed.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void band_fix_one(const uint2 rg, int lane, const float* __restrict__ A, int64_t lda,
-                                             const float* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
-                                             int H, uint8_t* bits, int64_t ldb, uint8_t* mask, int64_t ldm,
-                                             unsigned* flips) {
-  const float* a = A + (int64_t)rg.x * lda;
-  const float* w = W + (int64_t)rg.y * ldw;
+// one band element per 16-lane group (four per wave): fp64 dot of the fp32 rows in a fixed order
+// (each lane a strided slice of float4s, then a fixed 16-lane tree) + bias; the group's first lane
+// sets or clears the bit. H % 4 == 0 and 16-B aligned rows (decode_split3's preconditions).
+__device__ __forceinline__ void band_fix_one(const uint2 rg, bool valid, int lane, const float* __restrict__ A,
+                                             int64_t lda, const float* __restrict__ W, int64_t ldw,
+                                             const float* __restrict__ bias, int H, uint8_t* bits, int64_t ldb,
+                                             uint8_t* mask, int64_t ldm, unsigned* flips) {
+  const int q = lane & 15;
   double acc = 0.0;
-  for (int k = lane; k < H; k += 64) acc = fma((double)a[k], (double)w[k], acc);
-  acc = wave_sum_d(acc) + (double)bias[rg.y];
-  const bool pred = (float)acc > kMaskLogitThreshold;
-  if (lane == 0) {
-    bool was;
-    if (bits) {
-      unsigned* word = (unsigned*)(bits + (int64_t)rg.x * ldb) + (rg.y >> 5);
-      const unsigned bit = 1u << (rg.y & 31);
-      const unsigned old = pred ? atomicOr(word, bit) : atomicAnd(word, ~bit);
-      was = (old & bit) != 0;
-    } else {
-      uint8_t* p = mask + (int64_t)rg.x * ldm + rg.y;
-      was = *p != 0;
-      *p = pred ? 1 : 0;
+  if (valid) {
+    const float4* a = (const float4*)(A + (int64_t)rg.x * lda);
+    const float4* w = (const float4*)(W + (int64_t)rg.y * ldw);
+    for (int k = q; k < H / 4; k += 16) {
+      const float4 x = a[k], y = w[k];
+      acc = fma((double)x.x, (double)y.x, acc);
+      acc = fma((double)x.y, (double)y.y, acc);
+      acc = fma((double)x.z, (double)y.z, acc);
+      acc = fma((double)x.w, (double)y.w, acc);
     }
-    if (was != pred) atomicAdd(flips, 1u);
   }
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (!valid || q != 0) return;
+  acc += (double)bias[rg.y];
+  const bool pred = (float)acc > kMaskLogitThreshold;
+  bool was;
+  if (bits) {
+    unsigned* word = (unsigned*)(bits + (int64_t)rg.x * ldb) + (rg.y >> 5);
+    const unsigned bit = 1u << (rg.y & 31);
+    const unsigned old = pred ? atomicOr(word, bit) : atomicAnd(word, ~bit);
+    was = (old & bit) != 0;
+  } else {
+    uint8_t* p = mask + (int64_t)rg.x * ldm + rg.y;
+    was = *p != 0;
+    *p = pred ? 1 : 0;
+  }
+  if (was != pred) atomicAdd(flips, 1u);
 }
 
 // workgroups [0, kBandFixShardWgs): the shards (wave w takes shard w % kBandShards, its entries
-// w / kBandShards, + waves / kBandShards, ...); the rest: one wave per tile's slots
+// 4 (w / kBandShards) + group, + 4 waves / kBandShards, ...); the rest: one wave per tile's slots,
+// four entries at a time
 constexpr int kBandFixShardWgs = 256;
 __global__ __launch_bounds__(256) void k_band_fix(MaskBand band, int ntiles, const float* __restrict__ A, int64_t lda,
                                                 const float* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
                                                 int H, uint8_t* bits, int64_t ldb, uint8_t* mask, int64_t ldm,
                                                 unsigned* flips) {
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, grp = lane >> 4;
   if (blockIdx.x < kBandFixShardWgs) {
     const unsigned wave = blockIdx.x * 4 + (threadIdx.x >> 6), waves = kBandFixShardWgs * 4;
     const int sh = wave % kBandShards;
     const unsigned per = waves / kBandShards;
     const unsigned n = min(band.counts[sh], band.cap);
     const uint2* sl = band.list + (size_t)sh * band.cap;
-    for (unsigned e = wave / kBandShards; e < n; e += per)
-      band_fix_one(sl[e], lane, A, lda, W, ldw, bias, H, bits, ldb, mask, ldm, flips);
+    for (unsigned e0 = 4 * (wave / kBandShards); e0 < n; e0 += 4 * per) {
+      const unsigned e = e0 + grp;
+      band_fix_one(e < n ? sl[e] : make_uint2(0u, 0u), e < n, lane, A, lda, W, ldw, bias, H, bits, ldb, mask, ldm,
+                   flips);
+    }
     return;
   }
   const int t = (blockIdx.x - kBandFixShardWgs) * 4 + (threadIdx.x >> 6);
   if (t >= ntiles) return;
-  const unsigned n = band.tcount[t];
+  const unsigned n = min(band.tcount[t], (unsigned)band.tslots);
   const uint2* tl = band.tlist + (size_t)t * band.tslots;
-  for (unsigned e = 0; e < n; ++e) band_fix_one(tl[e], lane, A, lda, W, ldw, bias, H, bits, ldb, mask, ldm, flips);
+  for (unsigned e0 = 0; e0 < n; e0 += 4) {
+    const unsigned e = e0 + grp;
+    band_fix_one(e < n ? tl[e] : make_uint2(0u, 0u), e < n, lane, A, lda, W, ldw, bias, H, bits, ldb, mask, ldm,
+                 flips);
+  }
 }
 
 // the decode call's counters -> the workspace's cumulative ones: cum[0] split tiles, [1] exact
 // tiles, [2] band elements found, [3] bits the recompute flipped, [4] band elements beyond the
-// list's capacity (left as the kernels decided them), [5] decodes with split tiles, [6] without
+// list's capacity (left as the kernels decided them), [5] decodes with split or single tiles, [6]
+// without, [7] single-product tiles
 __global__ __launch_bounds__(64) void k_decode_stats(const unsigned* __restrict__ tiles_split,
                                                      const unsigned* __restrict__ tiles_exact,
+                                                     const unsigned* __restrict__ tiles_single,
                                                      const unsigned* __restrict__ counts,
                                                      const unsigned* __restrict__ tfound,
                                                      const unsigned* __restrict__ flips, unsigned cap,
                                                      unsigned long long* cum) {
   const int t = threadIdx.x;
   unsigned long long a = t < kSplitShards ? tiles_split[t] : 0ull, b = t < kSplitShards ? tiles_exact[t] : 0ull;
+  unsigned long long g = t < kSplitShards ? tiles_single[t] : 0ull;
   const unsigned c = t < kBandShards ? counts[t] : 0u;
   unsigned long long found = (unsigned long long)c + (t < kBandShards ? tfound[t] : 0u), over = c > cap ? c - cap : 0u;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     a += __shfl_xor(a, o, 64);
     b += __shfl_xor(b, o, 64);
+    g += __shfl_xor(g, o, 64);
     found += __shfl_xor(found, o, 64);
     over += __shfl_xor(over, o, 64);
   }
@@ -1275,7 +1301,8 @@ __global__ __launch_bounds__(64) void k_decode_stats(const unsigned* __restrict_
     cum[2] += found;
     cum[3] += *flips;
     cum[4] += over;
-    cum[a ? 5 : 6] += 1;
+    cum[a || g ? 5 : 6] += 1;
+    cum[7] += g;
   }
 }
 
@@ -1452,11 +1479,11 @@ void launch_bn_bwd_apply(const float* da, const float* Y, int64_t ld, const floa
 }
 
 void launch_split3(const float* X, int64_t ldx, int rows, int rows_pad, int K, bf16_t* out, int64_t ldo, float* rn,
-                   unsigned* blk, hipStream_t s) {
+                   unsigned* blk, hipStream_t s, bf16_t* out1) {
   if (K % 32 || ldx % 4 || ldo % 8 || ldo < 2 * K || rows > rows_pad || rows_pad % 256 || (((uintptr_t)X) & 15) ||
-      (((uintptr_t)out) & 15))
+      (((uintptr_t)out) & 15) || (((uintptr_t)out1) & 15))
     throw Gm2Error("split3: K %d, ld %lld / %lld, rows %d / %d", K, (long long)ldx, (long long)ldo, rows, rows_pad);
-  hipLaunchKernelGGL(k_split3, dim3(rows_pad / 16), dim3(256), 0, s, X, ldx, rows, K, out, ldo, rn, blk);
+  hipLaunchKernelGGL(k_split3, dim3(rows_pad / 16), dim3(256), 0, s, X, ldx, rows, K, out, ldo, rn, blk, out1);
   GM2_CHECK_LAUNCH();
 }
 
@@ -1502,11 +1529,12 @@ void launch_band_fix(const MaskBand& band, int ntiles, const float* A, int64_t l
   GM2_CHECK_LAUNCH();
 }
 
-void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* counts,
-                         const unsigned* tfound, const unsigned* flips, unsigned cap, unsigned long long* cum,
-                         hipStream_t s) {
+void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* tiles_single,
+                         const unsigned* counts, const unsigned* tfound, const unsigned* flips, unsigned cap,
+                         unsigned long long* cum, hipStream_t s) {
   static_assert(kSplitShards <= 64 && kBandShards <= 64, "one wave");
-  hipLaunchKernelGGL(k_decode_stats, dim3(1), dim3(64), 0, s, tiles_split, tiles_exact, counts, tfound, flips, cap, cum);
+  hipLaunchKernelGGL(k_decode_stats, dim3(1), dim3(64), 0, s, tiles_split, tiles_exact, tiles_single, counts, tfound, flips, cap,
+                     cum);
   GM2_CHECK_LAUNCH();
 }
 

@@ -61,6 +61,7 @@ void option_set(Options& o, int key, int value) {
       break;
     case GM2_OPT_GRAD_BUCKETS: o.grad_buckets = value ? 1 : 0; break;
     case GM2_OPT_SAMPLE_SPLIT: o.sample_split = value ? 1 : 0; break;
+    case GM2_OPT_SAMPLE_SINGLE: o.sample_single = value ? 1 : 0; break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -79,6 +80,7 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_DEFER_OUTPUT_ADAM: return o.defer_adam;
     case GM2_OPT_GRAD_BUCKETS: return o.grad_buckets;
     case GM2_OPT_SAMPLE_SPLIT: return o.sample_split;
+    case GM2_OPT_SAMPLE_SINGLE: return o.sample_single;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

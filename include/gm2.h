@@ -328,7 +328,12 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       band around the threshold are then recomputed in fp64 (GM2_STAT_BAND_*), so
  *                       a mask bit differs from the correctly rounded logit's only within the
  *                       reference's own fp32 rounding band. 0 = always the exact-fp32 output layer
- *                       without band recompute (as do probs requests). */
+ *                       without band recompute (as do probs requests).
+ *   GM2_OPT_SAMPLE_SINGLE 1 (default) = a third tier of that gate: tiles where 7.83e-3 x the tile's
+ *                       largest ||a_r||_2 x its largest ||w_g||_2 is at most 0.25 run ONE bf16 GEMM
+ *                       over the rounded operands (a third of the split's MFMA work) with a
+ *                       correspondingly wider certified band, recomputed in fp64 the same way;
+ *                       0 = split or exact only. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -341,7 +346,8 @@ enum {
   GM2_OPT_SYNC_BN = 10,
   GM2_OPT_DEFER_OUTPUT_ADAM = 11,
   GM2_OPT_GRAD_BUCKETS = 15,
-  GM2_OPT_SAMPLE_SPLIT = 18
+  GM2_OPT_SAMPLE_SPLIT = 18,
+  GM2_OPT_SAMPLE_SINGLE = 20
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);
@@ -352,8 +358,9 @@ int gm2_workspace_get_option(void* ws, int key, int* value);
 int gm2_workspace_join(void* ws, void* stream);
 /* Counters of a workspace's sampling decodes (gm2_decode_mask / gm2_decode_bits), cumulative since
  * gm2_workspace_init; reading one waits for the device.
- *   GM2_STAT_SPLIT_DECODES  decodes whose output layer ran at least one tile as bf16x3 (GM2_OPT_SAMPLE_SPLIT)
- *   GM2_STAT_EXACT_DECODES  decodes with no bf16x3 tile (the gate's verdict, a probs request,
+ *   GM2_STAT_SPLIT_DECODES  decodes whose output layer ran at least one tile as bf16x3 or single
+ *                           bf16 (GM2_OPT_SAMPLE_SPLIT, GM2_OPT_SAMPLE_SINGLE)
+ *   GM2_STAT_EXACT_DECODES  decodes with no such tile (the gate's verdict, a probs request,
  *                           GM2_OPT_SAMPLE_SPLIT off, or the split path's preconditions)
  *   GM2_STAT_SPLIT_TILES / GM2_STAT_EXACT_TILES  output-layer tiles (256 x 256 split, 128 x 128 exact)
  *                           each kernel of the gated decode ran
@@ -361,8 +368,9 @@ int gm2_workspace_join(void* ws, void* stream);
  *                           coef * ||a_r||_2 ||w_g||_2 (evaluated with the largest
  *                           of 4 neighbouring rows' norms, so a small superset) and recomputed in fp64
  *   GM2_STAT_BAND_FLIPS     mask bits that recompute changed
- *   GM2_STAT_BAND_OVERFLOW  band elements beyond a call's list capacity (32 slots per split tile,
- *                           then 64 shards x 65,536), left as computed */
+ *   GM2_STAT_BAND_OVERFLOW  band elements beyond a call's list capacity (256 slots per split or
+ *                           single tile, then 64 shards x 65,536), left as computed
+ *   GM2_STAT_SINGLE_TILES   output-layer tiles (256 x 256) the single-product kernel ran */
 enum {
   GM2_STAT_SPLIT_DECODES = 1,
   GM2_STAT_EXACT_DECODES = 2,
@@ -370,7 +378,8 @@ enum {
   GM2_STAT_EXACT_TILES = 4,
   GM2_STAT_BAND_ELEMENTS = 5,
   GM2_STAT_BAND_FLIPS = 6,
-  GM2_STAT_BAND_OVERFLOW = 7
+  GM2_STAT_BAND_OVERFLOW = 7,
+  GM2_STAT_SINGLE_TILES = 8
 };
 int gm2_workspace_stat(void* ws, int key, int64_t* value);
 

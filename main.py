@@ -210,7 +210,8 @@ def run_sampling(args):
     packed, _ = model.decode_bits(z[lo:hi])   # masks stay on the GPU, 8 genes per byte
     st = {k: v - st0[k] for k, v in model.decode_stats().items()}
     # (this rank's decode: output-layer tiles per path and the certified band)
-    print(f"- Decode (rank {rank}): {st['split_tiles']} bf16x3 / {st['exact_tiles']} fp32 output tiles; "
+    print(f"- Decode (rank {rank}): {st['single_tiles']} bf16 / {st['split_tiles']} bf16x3 / {st['exact_tiles']} fp32 "
+          f"output tiles; "
           f"{st['band_elements']} band logits recomputed in fp64, {st['band_flips']} bits changed"
           + (f", {st['band_overflow']} past the list" if st["band_overflow"] else ""))
     if dist is not None:

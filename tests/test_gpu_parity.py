@@ -160,20 +160,32 @@ def test_decode_masks_golden_bit_exact():
     np.testing.assert_allclose(p.cpu().numpy(), g[f"{tag}_p"], rtol=1e-5, atol=1e-6)
     # the default path (no probs): gated per 256 x 256 tile. The focused z (one latent point plus
     # 0.1 noise, main.py:351-370) keeps the activations small enough that both tiles (64 genomes x
-    # 300 genes) pass the split bound: this reference vector pins the bf16x3 kernel bit for bit
+    # 300 genes) pass the single-product bound: this reference vector pins the single bf16 kernel
+    # (+ its band recompute) bit for bit, and with that tier off (GM2_OPT_SAMPLE_SINGLE = 0) the
+    # bf16x3 kernel
     fm, _ = m.decode_mask(torch.tensor(g[f"{tag}_focused_z"]))
     st2 = m.decode_stats()
     d = {k: st2[k] - st1[k] for k in st2}
     print(f"focused decode path: {d}")
-    assert d["split_decodes"] == 1 and d["split_tiles"] == 2 and d["exact_tiles"] == 0, d
+    assert d["split_decodes"] == 1 and d["single_tiles"] + d["split_tiles"] == 2 and d["exact_tiles"] == 0, d
     np.testing.assert_array_equal(fm.cpu().numpy(), g[f"{tag}_focused_mask"])
+    ws = m.workspace(native.GM2_F32, 1)
+    ws.set_option(native.OPT_SAMPLE_SINGLE, 0)
+    fm, _ = m.decode_mask(torch.tensor(g[f"{tag}_focused_z"]))
+    ws.set_option(native.OPT_SAMPLE_SINGLE, 1)
+    st2b = m.decode_stats()
+    d = {k: st2b[k] - st2[k] for k in st2b}
+    print(f"focused decode path, single tier off: {d}")
+    assert d["split_decodes"] == 1 and d["split_tiles"] == 2 and d["single_tiles"] == 0 and d["exact_tiles"] == 0, d
+    np.testing.assert_array_equal(fm.cpu().numpy(), g[f"{tag}_focused_mask"])
+    st2 = st2b
     # the fixture's main z without probs: the gated path, whatever each tile's verdict, bit-exact to
     # the reference outside the fp64 band
     gm, _ = m.decode_mask(torch.tensor(g[f"{tag}_z"]))
     st3 = m.decode_stats()
     d = {k: st3[k] - st2[k] for k in st3}
     print(f"main decode path: {d}")
-    assert d["split_decodes"] + d["exact_decodes"] == 1 and d["split_tiles"] + d["exact_tiles"] > 0, d
+    assert d["split_decodes"] + d["exact_decodes"] == 1 and d["single_tiles"] + d["split_tiles"] + d["exact_tiles"] > 0, d
     bad, band = _band_ok(gm.cpu().numpy(), g[f"{tag}_mask"], g[f"{tag}_logit64"])
     assert bad == 0, (bad, band)
 

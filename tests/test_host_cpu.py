@@ -52,7 +52,7 @@ def test_header_constants_match_binding():
     for k, v in opts.items():
         assert getattr(native, "OPT_" + k) == v, k
     stats = dict((k, int(v)) for k, v in re.findall(r"GM2_STAT_([A-Z_]+) = (\d+)", txt))
-    assert len(stats) == 7 and set(native.DECODE_STATS.values()) == set(stats.values())
+    assert len(stats) == 8 and set(native.DECODE_STATS.values()) == set(stats.values())
     for k, v in stats.items():
         assert getattr(native, "STAT_" + k) == v, k
     assert [f[0] for f in native.Batch._fields_] == ["data", "ld_data", "rows", "n", "eps", "next", "resident",

@@ -123,7 +123,7 @@ static void options() {
       }
     }
   std::printf("option values accepted %d, rejected %d\n", accepted, rejected);
-  for (int bad : {0, -1, 20, 1000}) {
+  for (int bad : {0, -1, 21, 1000}) {
     int v = 0;
     expect_error(gm2_set_option(bad, 1), "unknown option", "set unknown key");
     expect_error(gm2_get_option(bad, &v), "unknown option", "get unknown key");
