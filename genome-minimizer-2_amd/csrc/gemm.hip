@@ -2016,9 +2016,8 @@ void launch_gemm_mask_tiered(const GemmArgs<bf16_t>& g1, const GemmArgs<bf16_t>&
 template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs, int64_t ldpr,
                       hipStream_t s, uint8_t* bits, int64_t ldb, int* counts, const uint32_t* xbits, int64_t ldxb,
-                      float thr, bool big, MaskGate gate, MaskBand band, bool single) {
+                      float thr, bool big, MaskGate gate, MaskBand band) {
   check_gemm(g, big ? 256 : 128);
-  if (single && !big) throw Gm2Error("mask: the single-product form is the 256x256 kernel");
   // (the 256-column tiles may reach past the row pitch: their bits stores stop at ldb, past G)
   if (bits && ((ldb & 15) || (((uintptr_t)bits) & 15) || ldb * 8 < (big ? g.N : g.Np)))
     throw Gm2Error("mask bits: row pitch %lld must be a multiple of 16 bytes covering the padded genes", (long long)ldb);
@@ -2042,13 +2041,8 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
         hipLaunchKernelGGL(kern, grid, dim3(Big::NT), lds, s, g, bias, o);
       };
       const bool ballot = bits && !mask && !probs && !counts && thr == 0.5f;  // packed bits only: ballot epilogue
-      if (single) {
-        if (ballot) go(k_gemm_mask<Big, T, true, true, false, false>);
-        else go(k_gemm_mask<Big, T, true, false, false, false>);
-      } else {
-        if (ballot) go(k_gemm_mask<Big, T, true, true>);
-        else go(k_gemm_mask<Big, T, true>);
-      }
+      if (ballot) go(k_gemm_mask<Big, T, true, true>);
+      else go(k_gemm_mask<Big, T, true>);
       GM2_CHECK_LAUNCH();
       return;
     }
@@ -2088,10 +2082,10 @@ GM2_INST(bf16_t)
 #undef GM2_INST
 template void launch_gemm_mask<float>(const GemmArgs<float>&, const float*, uint8_t*, int64_t, float*, int64_t,
                                       hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float, bool,
-                                      MaskGate, MaskBand, bool);
+                                      MaskGate, MaskBand);
 template void launch_gemm_mask<bf16_t>(const GemmArgs<bf16_t>&, const float*, uint8_t*, int64_t, float*, int64_t,
                                        hipStream_t, uint8_t*, int64_t, int*, const uint32_t*, int64_t, float, bool,
-                                       MaskGate, MaskBand, bool);
+                                       MaskGate, MaskBand);
 
 #ifdef GM2_DEBUG
 GM2_DBG_TAKE_FN(dbg_take_gemm)

@@ -283,7 +283,7 @@ template <typename T>
 void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, int64_t ldm, float* probs,
                       int64_t ldpr, hipStream_t s, uint8_t* bits = nullptr, int64_t ldb = 0, int* counts = nullptr,
                       const uint32_t* xbits = nullptr, int64_t ldxb = 0, float thr = 0.5f, bool big = false,
-                      MaskGate gate = {}, MaskBand band = {}, bool single = false);
+                      MaskGate gate = {}, MaskBand band = {});
 
 // ---- kernels.hip ----
 constexpr int kBnRowChunk = 128;  // rows per BatchNorm partial-statistics chunk
