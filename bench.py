@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sample", action="store_true")
     ap.add_argument("--sample-genomes", type=int, default=1000000)
+    ap.add_argument("--copy-streams", type=int, default=1,
+                    help="sample leg: copy streams the packed masks leave on (each a share of a chunk's rows)")
     ap.add_argument("--sample-train-epochs", type=int, default=10,
                     help="epochs of v1 training (lr 1e-3, batch 4096, the synthetic matrix) before the sample leg "
                          "decodes from that checkpoint; 0 = the untrained (xavier) model")
@@ -488,8 +490,10 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
     host_cnt = torch.empty(n, dtype=torch.int32, pin_memory=True)
     dbits = [torch.empty(chunk, ldb, dtype=torch.uint8, device=dev) for _ in range(2)]
     dcnt = [torch.empty(chunk, dtype=torch.int32, device=dev) for _ in range(2)]
-    copy = torch.cuda.Stream(device=dev)
-    done = [torch.cuda.Event(), torch.cuda.Event()]
+    # the packed masks leave on a.copy_streams copy streams, each a contiguous share of the chunk's rows
+    ncs = max(1, a.copy_streams)
+    copies = [torch.cuda.Stream(device=dev) for _ in range(ncs)]
+    done = [[torch.cuda.Event() for _ in range(ncs)] for _ in range(2)]
     ws = m.workspace(native.GM2_F32, chunk)
 
     def run(timed):
@@ -498,14 +502,18 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
         for k, s in enumerate(range(0, n, chunk)):
             b = k & 1
             cnt = min(chunk, n - s)
-            cur.wait_event(done[b])  # the copy of the chunk that last used this buffer has finished
+            for ev in done[b]:
+                cur.wait_event(ev)  # the copies of the chunk that last used this buffer have finished
             native.decode_bits(ws, m.params, m.bn, z[s:s + cnt], cnt, dbits[b], ldb)
             native.mask_count_groups(dbits[b], cnt, ldb, go, len(offs) - 1, po, dcnt[b])
-            copy.wait_stream(cur)
-            with torch.cuda.stream(copy):
-                host_bits[s:s + cnt].copy_(dbits[b][:cnt], non_blocking=True)
-                host_cnt[s:s + cnt].copy_(dcnt[b][:cnt], non_blocking=True)
-                done[b].record(copy)
+            for i, cs in enumerate(copies):
+                lo, hi = cnt * i // ncs, cnt * (i + 1) // ncs
+                cs.wait_stream(cur)
+                with torch.cuda.stream(cs):
+                    host_bits[s + lo:s + hi].copy_(dbits[b][lo:hi], non_blocking=True)
+                    if i == 0:
+                        host_cnt[s:s + cnt].copy_(dcnt[b][:cnt], non_blocking=True)
+                    done[b][i].record(cs)
         torch.cuda.synchronize()
 
     # warm-up on one chunk's worth
