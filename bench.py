@@ -558,7 +558,11 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
     last = (n - 1) // chunk * chunk
     assert torch.equal(host_bits[last:n].to(dev), dbits[((n - 1) // chunk) & 1][:n - last])
     # (the bf16x3 kernel is k_gemm_mask<Cfg<256, ...>, unsigned short, true>, the exact one <..., float>)
-    traffic, traffic_src = pmc_traffic(a, "k_gemm_mask<Cfg<256" if bf16 else "k_gemm_mask<Cfg<128")
+    # (the bf16 tiers run in k_gemm_mask_tiered when the single tier is on, else k_gemm_mask<..., true>;
+    # the PMC passes decode from an untrained model, tools/prof.sh)
+    tiered = ws.get_option(native.OPT_SAMPLE_SINGLE) != 0
+    traffic, traffic_src = pmc_traffic(a, ("k_gemm_mask_tiered<Cfg<256" if tiered else "k_gemm_mask<Cfg<256") if bf16
+                                       else "k_gemm_mask<Cfg<128")
     return {"genomes_per_s": round(gps, 1), "preset": "v1", "genomes": n_all, "n_gpus": world, "chunk": chunk,
             "checkpoint": (f"v1 trained {a.sample_train_epochs} epochs (lr 1e-3, batch 4096, L1 0.01) on the synthetic "
                            f"{a.strains}x{G} matrix" if trained is not None else "untrained (xavier init)"),
