@@ -1,5 +1,6 @@
 // Tuning options of libgm2 (gm2.h GM2_OPT_*): per-workspace copies, process defaults, and the
 // per-call scope through which the launchers read them. Host code only.
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 
@@ -22,6 +23,19 @@ Options& defaults_locked() {
     if (pp && pp[0] == '0') o.gemm_pp = 0;
     const char* side = std::getenv("GM2_SIDE_STREAM");
     if (side && side[0] == '0') o.side_stream = 0;
+    // GM2_OPTS="key=value,key=value" (gm2.h GM2_OPT_* numbers): process defaults for same-box A/Bs;
+    // a malformed or refused entry is ignored
+    if (const char* e = std::getenv("GM2_OPTS")) {
+      int key = 0, value = 0, used = 0;
+      while (*e && std::sscanf(e, "%d=%d%n", &key, &value, &used) == 2) {
+        try {
+          option_set(o, key, value);
+        } catch (const Gm2Error&) {
+        }
+        e += used;
+        if (*e == ',') ++e;
+      }
+    }
     return o;
   }();
   return d;
