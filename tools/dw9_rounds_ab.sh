@@ -1,0 +1,5 @@
+# same-box A/B of the capped dW9 grid's rounds (GM2_DW9_ROUNDS) and start point
+cd "$GRAFT_REPO_ROOT" || exit 2
+mkdir -p gpurun_out
+export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
+bash tools/ab_bench.sh rounds 3 "X=0|" "GM2_DW9_ROUNDS=5|" "GM2_DW9_ROUNDS=6|" "GM2_DW9_ROUNDS=5 GM2_DW9_AT=0|"
