@@ -89,6 +89,22 @@ def test_header_constants_match_binding():
     assert all(cover[i][1] == cover[i + 1][0] for i in range(len(cover) - 1))
 
 
+def test_process_default_options_from_env():
+    """GM2_OPTS="key=value,..." (options.hip) sets process defaults at library load for same-box A/Bs:
+    valid entries apply, a refused value and an unknown key are ignored, parsing stops at garbage."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, 'genome-minimizer-2_amd'); from gm2 import native as n; "
+            "print(n.get_option(n.OPT_SMALL_WAVES), n.get_option(n.OPT_SMALL_SPLIT), n.get_option(n.OPT_GRID_CAP), "
+            "n.get_option(n.OPT_SAMPLE_SINGLE))")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GM2_OPTS="6=4,4=3,9=99,999=1,20=0,x,6=8")
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    # 6=4 and 4=3 applied, 9=99 refused (grid cap stays 3), 999 unknown, 20=0 applied, "x" ends parsing
+    assert out.stdout.split() == ["4", "3", "3", "0"], out.stdout
+
+
 def test_layout_queries_and_errors():
     from gm2 import native
     G, H, L = 55039, 1024, 64
