@@ -102,6 +102,8 @@ def parse():
     ap.add_argument("--input-chunks", type=int, choices=[1, 4], default=None,
                     help="input-layer weight-gradient launches (default: 4 under DDP, else 1)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5-shaped (G=20,000) step line")
+    ap.add_argument("--no-presets", action="store_true", help="skip the v1 / v2 / v3 step lines (C3 / C4 per GPU)")
+    ap.add_argument("--no-c1", action="store_true", help="skip the batch-64 / batch-32 GPU lines (C1 workload)")
     ap.add_argument("--defer-adam", type=int, default=None,
                     help="output layer's Adam update launched beside the next step's hidden layers on this many "
                          "workgroups per CU, 0 = not deferred (GM2_OPT_DEFER_OUTPUT_ADAM; bit-identical; default 1, as the "
@@ -208,13 +210,33 @@ def gpu_precision_line(mat, G, H, L, B, prec, steps, dev):
             "value": round(B * steps / dt, 1), "unit": "strain-vectors/s", "steps": steps}
 
 
-def scalar_table(nsteps):
-    """Per-step scalar table of the v0 preset at epoch 0 (beta 0.1, no abundance / L1)."""
+# preset hyper-parameters of the loss terms (utils/experiments.py:42-114, trainer.py:193-257):
+# KL schedule (type, min, max, T), gene abundance (gamma_start, gamma_end, weight) or None, L1 lambda
+PRESET_TERMS = {"v0": (("linear", 0.1, 1.0, 10), None, 0.0),
+                "v1": (("linear", 0.1, 1.0, 10), (1.0, 0.1, 1.0), 0.01),
+                "v2": (("cosine", 0.0, 1.0, 10), (1.0, 0.1, 1.0), 0.01),
+                "v3": (("cosine", 0.1, 1.0, 50), (2.0, 0.1, 1.0), 0.01)}
+
+
+def scalar_table(nsteps, preset="v0", n_epochs=10000):
+    """Per-step scalar table of `preset` at epoch 0 of an n_epochs run, from the host schedule code
+    the trainer uses (gm2.loss_components: the KL beta -- linear, or cosine advancing its counter per
+    batch -- w * gamma of the gene abundance, lambda of L1)."""
     from gm2 import native
+    from gm2.loss_components import GeneAbundanceLoss, KLDivergenceLoss
+    (kind, bmin, bmax, T), ab, lam = PRESET_TERMS[preset]
+    kl = KLDivergenceLoss(scheduler_type=kind, min_beta=bmin, max_beta=bmax, T=T)
+    kl.n_epochs = n_epochs
+    ga = None
+    if ab is not None:
+        ga = GeneAbundanceLoss(gamma_start=ab[0], gamma_end=ab[1], weight=ab[2])
+        ga.n_epochs = n_epochs
     tab = np.zeros((nsteps, native.NUM_SCALARS), np.float64)
     for i in range(nsteps):
         t = i + 1
-        tab[i, native.S_BETA] = 0.1
+        tab[i, native.S_BETA] = kl.scalars(0)["beta"]
+        tab[i, native.S_WGAMMA] = ga.scalars(0)["wgamma"] if ga is not None else 0.0
+        tab[i, native.S_LAMBDA] = lam
         tab[i, native.S_MAX_NORM] = 1.0
         tab[i, native.S_NEG_STEP] = -(1e-3 / (1 - 0.9 ** t))
         tab[i, native.S_BC2_SQRT] = math.sqrt(1 - 0.999 ** t)
@@ -223,28 +245,35 @@ def scalar_table(nsteps):
     return tab
 
 
-def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12345):
-    """K timed v0 training steps (after W warm-up steps) of `B` rows per rank, on a resident
-    synthetic pan-genome shard of `strains` x G per rank: gather, forward, fused loss, backward,
-    (bucketed all-reduce when world > 1), clip statistics, Adam. Returns the max-over-ranks wall
-    time of the K steps, the live-timed output-layer loss kernel, and the per-step loss record
-    (every step's losses and gradient norm must be finite)."""
+def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12345, preset="v0", x=None,
+              steps=None, warmup=None):
+    """K timed training steps of `preset` (v0 unless given; after W warm-up steps) of `B` rows per
+    rank, on a resident synthetic pan-genome shard of `strains` x G per rank (or the given host
+    matrix x): forward, fused loss, backward, (bucketed all-reduce when world > 1), clip statistics
+    (+ L1), Adam. Returns the max-over-ranks wall time of the K steps, the live-timed output-layer
+    loss kernel, and the per-step loss record (every step's losses and gradient norm must be
+    finite)."""
     from gm2 import native
     from gm2.data import ResidentMatrix, synthetic_pangenome
     from gm2.ddp import GradSync
     from gm2.model import VAE
     from gm2.trainer import Adam
 
-    x = synthetic_pangenome(strains, G, seed=seed_base + rank)
+    K = a.steps if steps is None else steps
+    W = a.warmup if warmup is None else warmup
+    if x is None:
+        x = synthetic_pangenome(strains, G, seed=seed_base + rank)
+    strains = x.shape[0]
     mat = ResidentMatrix(x, device=dev)
     torch.manual_seed(0)  # identical init on every rank
     model = VAE(G, H, L, device=dev, precision=prec)
     opt = Adam(model, lr=1e-3)
     ws = model.workspace(prec, B)
     grads = torch.zeros_like(model.params)
-    nsteps = a.warmup + a.steps
-    # per-step scalar table (v0: linear beta over 10000 epochs at epoch 0 -> 0.1; no abundance/L1)
-    tab = scalar_table(nsteps)
+    nsteps = W + K
+    # per-step scalar table (the preset's schedules at epoch 0 of a 10000-epoch run: v0 beta 0.1, no
+    # abundance / L1; v1-v3 add w * gamma and lambda 0.01, v2 / v3 a cosine beta advancing per batch)
+    tab = scalar_table(nsteps, preset)
     # one process: grads reach gm2_grad_norm as gm2_train_fwd_bwd wrote them (no all-reduce between)
     tab[:, native.S_NORM_AHEAD] = 1.0 if dist is None else 0.0
     scal = torch.tensor(tab, dtype=torch.float32, device=dev)
@@ -288,7 +317,7 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         native.adam_step(ws, model.params, grads, opt.exp_avg, opt.exp_avg_sq, scal[i])
 
     torch.cuda.synchronize()
-    for i in range(a.warmup):
+    for i in range(W):
         step(i)
     ws.join()  # (a queued output-layer update runs before the timed region, the timed steps' inside it)
     torch.cuda.synchronize()
@@ -298,14 +327,14 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
     native.timing_begin(native.KC_RECON_LOSS)
     t0 = time.perf_counter()
     host_s = 0.0
-    for i in range(a.warmup, nsteps):
+    for i in range(W, nsteps):
         h0 = time.perf_counter()
         step(i)
         host_s += time.perf_counter() - h0
     ws.join()
     torch.cuda.synchronize()
     if a.host_timing:  # (stderr: the host's enqueue time per step, the GPU running asynchronously)
-        print(f"host enqueue {1e3 * host_s / max(1, nsteps - a.warmup):.3f} ms/step", file=sys.stderr)
+        print(f"host enqueue {1e3 * host_s / max(1, nsteps - W):.3f} ms/step", file=sys.stderr)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -332,9 +361,10 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
     return elapsed, k_ms, k_n, info
 
 
-def roofline_entry(a, prec, G, H, B, k_ms, k_n):
+def roofline_entry(a, prec, G, H, B, k_ms, k_n, pmc=True):
     """Output-layer loss GEMM [B,H]x[H,G] + fused BCE/dlogits epilogue against the MFMA roofline:
-    achieved = 2*B*H*G FLOP per launch / its average live-timed launch duration."""
+    achieved = 2*B*H*G FLOP per launch / its average live-timed launch duration (pmc=False: no
+    committed PMC pass covers this launch shape -> traffic null)."""
     from gm2 import native
     k_avg_ms = k_ms / max(k_n, 1)
     k_flops = 2.0 * B * H * G
@@ -342,7 +372,7 @@ def roofline_entry(a, prec, G, H, B, k_ms, k_n):
     peak = PEAK_BF16_TFLOPS if prec == native.GM2_BF16 else PEAK_F32_TFLOPS
     # (the launch's grid: one 512-thread workgroup per 256x256 genes x strains tile)
     grid = ((G + 255) // 256) * ((B + 255) // 256) * 512 if prec == native.GM2_BF16 else None
-    traffic, traffic_src = pmc_traffic(a, "k_gemm_recon_loss", grid)
+    traffic, traffic_src = pmc_traffic(a, "k_gemm_recon_loss", grid) if pmc else (None, None)
     return {"bound": "mfma", "kernel": "k_gemm_recon_loss<bf16>" if prec == native.GM2_BF16
             else "k_gemm_recon_loss<f32>", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
@@ -414,6 +444,38 @@ def main():
                      "n_gpus": world, "ms_per_step": round(el5 / a.steps * 1e3, 3),
                      "train_tflops": round(v5 * train_flops_per_vector(Gc, H, L) / 1e12, 2),
                      "roofline": roofline_entry(a, prec, Gc, H, B, k5, n5)}
+    if not a.no_presets:
+        # C3 / C4 per-GPU work: the v1, v2 and v3 presets' training step (hidden 512, latent 32, gene
+        # abundance + L1 0.01; v2 / v3 with the cosine KL) on the same F4-shaped shard, B rows per GPU
+        Hv, Lv = 512, 32
+        out["presets"] = {}
+        for pv in ("v1", "v2", "v3"):
+            elp, kp, np_, infp = train_leg(a, dev, dist, rank, world, G, Hv, Lv, B, a.strains, prec, preset=pv, x=x)
+            del infp
+            torch.cuda.empty_cache()
+            vp = world * B * a.steps / elp
+            out["presets"][pv] = {
+                "workload": f"{pv} train step (fwd+bwd+clip+L1+Adam, {PRESET_TERMS[pv][0][0]} KL, gene abundance), "
+                            f"G={G} H={Hv} L={Lv}, batch {B}/GPU, same synthetic {a.strains}x{G} shard",
+                "value": round(vp, 1), "unit": "strain-vectors/s", "n_gpus": world,
+                "ms_per_step": round(elp / a.steps * 1e3, 3),
+                "train_tflops": round(vp * train_flops_per_vector(G, Hv, Lv) / 1e12, 2),
+                "roofline": roofline_entry(a, prec, G, Hv, B, kp, np_, pmc=False)}
+    if rank == 0 and world == 1 and not a.no_c1:
+        # C1 (configs[0]) on the GPU: the reference's own training batches at F4 width -- v0 at batch 64
+        # (C1) and at the CLI default batch 32 (utils/custom_config.py:25) -- one step per batch as
+        # trainer.py:109-120 runs it (fwd+bwd+clip+Adam; rows gathered from the resident matrix)
+        out["c1_gpu"] = {}
+        for bc in (64, 32):
+            elc, kc, nc, infc = train_leg(a, dev, None, 0, 1, G, H, L, bc, a.strains, prec, x=x, steps=100, warmup=10)
+            del infc
+            torch.cuda.empty_cache()
+            vc = bc * 100 / elc
+            out["c1_gpu"][f"b{bc}"] = {
+                "workload": f"v0 train step, G={G} H={H} L={L}, batch {bc}, synthetic {a.strains}x{G} matrix resident",
+                "value": round(vc, 1), "unit": "strain-vectors/s", "ms_per_step": round(elc / 100 * 1e3, 4),
+                "steps": 100, "train_tflops": round(vc * train_flops_per_vector(G, H, L) / 1e12, 2),
+                "roofline": roofline_entry(a, prec, G, H, bc, kc, nc, pmc=False)}
     if rank == 0 and world == 1 and not a.no_f32_line:
         from gm2.data import ResidentMatrix
         other = native.GM2_F32 if prec == native.GM2_BF16 else native.GM2_BF16

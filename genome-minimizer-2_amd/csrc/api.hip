@@ -121,6 +121,11 @@ struct Layout {
   // kernel's per-tile band slots (s3tlist [tiles][kBandTileSlots] (row, gene), s3tcount [tiles])
   int64_t s3a, s3w, s3rn, s3cn, s3ctl, s3band, s3tlist, s3tcount;
   int64_t s3a1, s3w1;          // the single-product tier's operands: the hi parts alone, [rows][H] bf16
+  // band-list overflow (MaskBand.oflag / olist / ocount, k_band_tile_fix), uint32 words: [0, 2) the
+  // cumulative count of recomputed blocks (uint64), [4] this call's block count, [64, 64 + tiles) the
+  // per-block flags, then [tiles] the listed block ids. Words [4, 64 + tiles) zeroed per decode.
+  int64_t s3ovf;
+  static constexpr int kOvfCount = 4, kOvfFlags = 64;
   int64_t adamscal;            // scalar block of a queued output-layer Adam update
   int64_t ridx;                // zero-copy rows: int32 [roundup(Bm, 256)] resident-matrix row per batch row
 };
@@ -208,6 +213,7 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.s3tcount = take(s3tiles * 4);
   o.s3a1 = take(split3 ? round_up(Bm, 2 * kTile) * H * 2 : 0);
   o.s3w1 = take(split3 ? round_up(d.G, 2 * kTile) * H * 2 : 0);
+  o.s3ovf = take(split3 ? (Layout::kOvfFlags + 2 * s3tiles) * 4 : 0);
   o.adamscal = take(GM2_NUM_SCALARS * 4);
   o.ridx = take(round_up(Bm, 2 * kTile) * 4);
   o.total = cur;
@@ -316,6 +322,7 @@ struct WsState {
   int64_t exact_decodes = 0;        // decodes the host sent to the exact-fp32 kernel alone (probs requests,
                                     // GM2_OPT_SAMPLE_SPLIT = 0, preconditions): GM2_STAT_EXACT_DECODES
   const unsigned long long* decode_cum = nullptr;  // the gated decodes' cumulative device counters (DecodeCtl)
+  const unsigned long long* decode_ovf = nullptr;  // their cumulative count of overflow-recomputed blocks
   // the queued (not yet launched) output-layer update: launched by kick() beside the next training
   // call's hidden layers, or by join() on the joining stream
   struct QueuedAdam {
@@ -428,11 +435,13 @@ WsState& ws_reset(void* ws) {
   return *slot;
 }
 
-void ws_release(void* ws) {
+// true: a queued output-layer update was discarded (gm2_workspace_release then returns 1)
+bool ws_release(void* ws) {
   std::lock_guard<std::mutex> lk(ws_mutex());
   auto it = ws_map().find(ws);
-  if (it == ws_map().end()) return;
+  if (it == ws_map().end()) return false;
   WsState& st = *it->second;
+  const bool dropped = st.qadam.queued;
   // A still-QUEUED output-layer update is dropped, not launched: release can run at garbage-collection
   // time, after the parameter / moment buffers it would write were freed (callers join with
   // gm2_workspace_join before releasing, as gm2.h says; the Python host does). A RUNNING one is
@@ -445,6 +454,7 @@ void ws_release(void* ws) {
   }
   st.destroy();
   ws_map().erase(it);
+  return dropped;
 }
 
 // first row of quarter q (0..4) of the input-layer weight gradient [H][G]
@@ -996,7 +1006,10 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
   bf16_t* w1 = (bf16_t*)(c.ws + l.s3w1);
   launch_split3(c.f(l.A[5]), H, n, Bq, H, a3, 2 * H, rn, ablk, c.s, single ? a1 : nullptr);
   launch_split3(w9, H, G, Gq, H, w3, 2 * H, cn, wblk, c.s, single ? w1 : nullptr);
-  if (c.st) c.st->decode_cum = (const unsigned long long*)(ctl + DecodeCtl::kCum);
+  if (c.st) {
+    c.st->decode_cum = (const unsigned long long*)(ctl + DecodeCtl::kCum);
+    c.st->decode_ovf = (const unsigned long long*)(c.ws + l.s3ovf);
+  }
   // band half-widths per unit ||a_r|| ||w_g|| (MaskBand): single tiles carry the operands' bf16
   // rounding and the fp32 accumulation of their H products, split tiles the split's own error and the
   // fp32 accumulation of its 3H products, exact tiles the fp32 accumulation of H products; all, the
@@ -1017,11 +1030,22 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
   b1.drop_overflow = 1;
   b1.tiles_done = ctl + DecodeCtl::kTilesSingle;
   HIP_OK(hipMemsetAsync(bs.tcount, 0, (size_t)tiles * 4, c.s));
+  // band-list overflow: entries past a shard's capacity flag their 256 x 256 block, which
+  // k_band_tile_fix then recomputes whole in fp64 (no bit is left as a bf16 tier decided it)
+  unsigned* ovf = (unsigned*)(c.ws + l.s3ovf);
+  HIP_OK(hipMemsetAsync(ovf + Layout::kOvfCount, 0, (size_t)(Layout::kOvfFlags - Layout::kOvfCount + tiles) * 4, c.s));
+  bs.cap = (unsigned)std::min<int>(opts().band_cap, (int)kBandShardCap);
+  bs.oflag = ovf + Layout::kOvfFlags;
+  bs.olist = bs.oflag + tiles;
+  bs.ocount = ovf + Layout::kOvfCount;
+  bs.obn = Gq / 256;
+  be.cap = bs.cap;
+  be.oflag = bs.oflag;
+  be.olist = bs.olist;
+  be.ocount = bs.ocount;
+  be.obn = bs.obn;
   const int on = single ? 1 : 0;
-  static const double single_bound = [] {  // (env GM2_SINGLE_BOUND: the tier's gate, for A/Bs)
-    const char* e = std::getenv("GM2_SINGLE_BOUND");
-    return e ? std::atof(e) : kSingleBound;
-  }();
+  const double single_bound = opts().single_bound_milli * 1e-3;  // (GM2_OPT_SAMPLE_SINGLE_BOUND, for A/Bs and tests)
   GemmArgs<bf16_t> g{a3, 2 * H, w3, 2 * H, n, G, 2 * H, Bq, Gq, 0};
   const MaskGate gs{ablk, wblk, 1, ctl + DecodeCtl::kTilesSplit, on, single_bound};
   if (single) {  // both bf16 tiers in one launch (a single tile whose band overflows re-runs as split)
@@ -1037,9 +1061,11 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
                           false, MaskGate{ablk, wblk, 2, ctl + DecodeCtl::kTilesExact, on, single_bound}, be);
   launch_band_fix(bs, tiles, c.f(l.A[5]), H, w9, H, prm + d.off[D9B], H, bits, ldb, mask, ldm,
                   ctl + DecodeCtl::kFlips, c.s);
+  launch_band_tile_fix(bs, c.f(l.A[5]), H, w9, H, prm + d.off[D9B], H, n, G, bits, ldb, mask, ldm,
+                       ctl + DecodeCtl::kFlips, c.s);
   launch_decode_stats(ctl + DecodeCtl::kTilesSplit, ctl + DecodeCtl::kTilesExact, ctl + DecodeCtl::kTilesSingle,
-                      ctl + DecodeCtl::kCounts, ctl + DecodeCtl::kTileFound, ctl + DecodeCtl::kFlips, kBandShardCap,
-                      (unsigned long long*)(ctl + DecodeCtl::kCum), c.s);
+                      ctl + DecodeCtl::kCounts, ctl + DecodeCtl::kTileFound, ctl + DecodeCtl::kFlips, bs.cap,
+                      (unsigned long long*)(ctl + DecodeCtl::kCum), bs.ocount, (unsigned long long*)ovf, c.s);
   return true;
 }
 
@@ -1623,11 +1649,13 @@ int gm2_workspace_stat(void* ws, int key, int64_t* value) {
       case GM2_STAT_BAND_ELEMENTS:
       case GM2_STAT_BAND_FLIPS:
       case GM2_STAT_BAND_OVERFLOW:
-      case GM2_STAT_SINGLE_TILES: {
-        unsigned long long cum[8] = {};  // (the gated decodes' device counters: waits for the device)
+      case GM2_STAT_SINGLE_TILES:
+      case GM2_STAT_OVERFLOW_TILES: {
+        unsigned long long cum[8] = {}, ovf = 0;  // (the gated decodes' device counters: waits for the device)
         if (st.decode_cum) {
           HIP_OK(hipDeviceSynchronize());
           HIP_OK(hipMemcpy(cum, st.decode_cum, sizeof cum, hipMemcpyDeviceToHost));
+          HIP_OK(hipMemcpy(&ovf, st.decode_ovf, sizeof ovf, hipMemcpyDeviceToHost));
         }
         switch (key) {
           case GM2_STAT_SPLIT_DECODES: *value = (int64_t)cum[5]; break;
@@ -1637,6 +1665,7 @@ int gm2_workspace_stat(void* ws, int key, int64_t* value) {
           case GM2_STAT_BAND_ELEMENTS: *value = (int64_t)cum[2]; break;
           case GM2_STAT_BAND_FLIPS: *value = (int64_t)cum[3]; break;
           case GM2_STAT_SINGLE_TILES: *value = (int64_t)cum[7]; break;
+          case GM2_STAT_OVERFLOW_TILES: *value = (int64_t)ovf; break;
           default: *value = (int64_t)cum[4]; break;
         }
         break;
@@ -1647,7 +1676,14 @@ int gm2_workspace_stat(void* ws, int key, int64_t* value) {
 }
 
 int gm2_workspace_release(void* ws) {
-  return guarded([&] { ws_release(ws); });
+  bool dropped = false;
+  const int rc = guarded([&] { dropped = ws_release(ws); });
+  if (rc == 0 && dropped) {
+    g_err = "gm2_workspace_release: a queued output-layer Adam update (GM2_OPT_DEFER_OUTPUT_ADAM) was discarded; "
+            "call gm2_workspace_join before releasing to keep it";
+    return 1;
+  }
+  return rc;
 }
 
 int gm2_timing_begin(int kernel_classes) {

@@ -1273,6 +1273,13 @@ struct BandCols {
   }
 };
 
+// a band entry past its shard's capacity: its 256 x 256 block is flagged (the first lane to flag it
+// lists it) for k_band_tile_fix's whole-block fp64 recompute
+__device__ __forceinline__ void band_spill(const MaskBand& b, unsigned r, unsigned gcol) {
+  const unsigned blk = (r >> 8) * (unsigned)b.obn + (gcol >> 8);
+  if (atomicExch(b.oflag + blk, 1u) == 0u) b.olist[atomicAdd(b.ocount, 1u)] = blk;
+}
+
 // one wave's band elements: walk(visit) calls visit(in, row, gene) for every fragment position in a
 // fixed order; per position with flagged lanes, one reservation for all of them (an LDS counter
 // for the tile's slots, else the shard's counter) and each flagged lane's entry at its prefix
@@ -1292,11 +1299,13 @@ __device__ __forceinline__ void band_walk(const MaskBand& b, int tile, char* sme
     const uint2 e = make_uint2((unsigned)r, (unsigned)gcol);
     if (!b.tslots) {
       if (i < b.cap) shard[i] = e;
+      else band_spill(b, e.x, e.y);
     } else if (i < (unsigned)b.tslots) {
       b.tlist[(size_t)tile * b.tslots + i] = e;
     } else if (!b.drop_overflow) {  // past the tile's slots: the shard (rare)
       const unsigned k = atomicAdd(b.counts + sh, 1u);
       if (k < b.cap) shard[k] = e;
+      else band_spill(b, e.x, e.y);
     }
   });
 }
@@ -1316,11 +1325,13 @@ __device__ __forceinline__ void band_add(const MaskBand& b, int tile, char* smem
   uint2* shard = b.list + (size_t)sh * b.cap;
   if (!b.tslots) {
     if (i < b.cap) shard[i] = e;
+    else band_spill(b, e.x, e.y);
   } else if (i < (unsigned)b.tslots) {
     b.tlist[(size_t)tile * b.tslots + i] = e;
   } else if (!b.drop_overflow) {
     const unsigned k = atomicAdd(b.counts + sh, 1u);
     if (k < b.cap) shard[k] = e;
+    else band_spill(b, e.x, e.y);
   }
 }
 
@@ -1999,6 +2010,8 @@ void launch_gemm_mask_tiered(const GemmArgs<bf16_t>& g1, const GemmArgs<bf16_t>&
     throw Gm2Error("mask bits: row pitch %lld must be a multiple of 16 bytes covering the padded genes", (long long)ldb);
   if (!band1.rn || !band3.rn || !band1.tslots || !band3.tslots || !band1.drop_overflow || !gate3.run)
     throw Gm2Error("tiered mask: both bands with tile slots (the single tier's dropping its overflow) and the gate");
+  if (!band3.oflag || !band3.olist || !band3.ocount || band3.obn < g3.Np / 256)
+    throw Gm2Error("tiered mask: the overflow block flags, list and counter required");
   const MaskOut o1{mask, ldm, bits, ldb, nullptr, 0, nullptr, nullptr, 0, 0.5f, gate1, band1};
   const MaskOut o3{mask, ldm, bits, ldb, nullptr, 0, nullptr, nullptr, 0, 0.5f, gate3, band3};
   constexpr int lds = Big::LDS + band_lds_bytes<Big>();
@@ -2025,6 +2038,8 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
   MaskOut o{mask, ldm, bits, ldb, probs, ldpr, counts, xbits, ldxb, thr, gate, band};
   if (band.rn && (!band.cn || !band.counts || !band.list || !band.cap || thr != 0.5f))
     throw Gm2Error("mask band: norms, counter and list required (threshold 0.5 only)");
+  if (band.rn && (!band.oflag || !band.olist || !band.ocount || band.obn < (g.Np + 255) / 256))
+    throw Gm2Error("mask band: the overflow block flags, list and counter required");
   if (band.tslots && (!band.tlist || !band.tcount || !band.tfound || !big))
     throw Gm2Error("mask band: tile slots need their list, counters and the 256 x 256 kernel");
   const int band_lds = band.rn ? (big ? band_lds_bytes<Big>() : band_lds_bytes<Small>()) : 0;  // (norms + slot counter)

@@ -93,6 +93,9 @@ struct Options {
   int grad_buckets = 1;  // GM2_OPT_GRAD_BUCKETS  record the gradient-bucket events (gm2_wait_grad_bucket)
   int sample_split = 1;  // GM2_OPT_SAMPLE_SPLIT  bf16x3 output layer of the sampling decode (bound permitting)
   int sample_single = 1; // GM2_OPT_SAMPLE_SINGLE the single-product bf16 tier of that gate (bound permitting)
+  int band_cap = 65536;  // GM2_OPT_SAMPLE_BAND_CAP entries per band-list shard per decode (<= kBandShardCap;
+                         //   smaller values exercise the overflow recompute)
+  int single_bound_milli = 250;  // GM2_OPT_SAMPLE_SINGLE_BOUND the single tier's gate x 1000 (kSingleBound)
 };
 // validated edit of one option (throws on an unknown key or a bad value)
 void option_set(Options& o, int key, int value);
@@ -236,8 +239,10 @@ __device__ __forceinline__ int tile_level(const MaskGate& g, int m0, int n0) {
 // from a counter in LDS, the tile's count stored once at the end of the tile; no global atomic on
 // the common path), else (and for a tile's elements past its slots) to the list's kBandShards
 // shards of `cap` entries (shard = blockIdx % kBandShards, each with its own counter: one atomic per
-// wave per fragment position that holds band elements); entries past a shard's capacity are only
-// counted (left as the kernel decided them).
+// wave per fragment position that holds band elements). An entry past a shard's capacity is not
+// lost: its 256 x 256 block (genome rows r >> 8, genes g >> 8) is flagged once (oflag) and listed
+// (olist), and k_band_tile_fix recomputes EVERY logit of each listed block in fp64 after the band
+// fix, so a mask bit never stays as a bf16 tier decided it inside the band (round 6).
 constexpr int kBandShards = 64;
 constexpr unsigned kBandShardCap = 1u << 16;  // entries per shard per decode call (64 x 64 K x 8 B = 32 MB)
 constexpr int kBandTileSlots = 256;           // per 256 x 256 tile (a trained model: ~2 per split, ~80 per single tile)
@@ -248,6 +253,12 @@ struct MaskBand {
   unsigned* counts = nullptr; // [kBandShards]
   uint2* list = nullptr;      // [kBandShards][cap] (row, gene)
   unsigned cap = 0;
+  // overflow: per 256 x 256 block a flag word (zeroed by the caller), the flagged blocks' ids
+  // (row block * obn + gene block; capacity = the block count, so it cannot overflow) and their count
+  unsigned* oflag = nullptr;
+  unsigned* olist = nullptr;
+  unsigned* ocount = nullptr;
+  int obn = 0;                // gene blocks per row block
   uint2* tlist = nullptr;     // [tiles][tslots] (row, gene), tile = TileXY::t of the launch's grid
   unsigned* tcount = nullptr; // [tiles] the tile's band count, of which min(count, tslots) in its slots
                               // (zeroed by the caller; a tile's kernel writes its own)
@@ -271,10 +282,18 @@ void launch_gemm_mask_tiered(const GemmArgs<bf16_t>& g1, const GemmArgs<bf16_t>&
 void launch_band_fix(const MaskBand& band, int ntiles, const float* A, int64_t lda, const float* W, int64_t ldw,
                      const float* bias, int H, uint8_t* bits, int64_t ldb, uint8_t* mask, int64_t ldm, unsigned* flips,
                      hipStream_t s);
-// one workgroup: the decode call's per-call counters -> the workspace's cumulative ones (DecodeCtl)
+// k_band_tile_fix over the blocks band.olist lists (band.ocount of them, read on the device): every
+// logit of rows [256 rb, min(256 rb + 256, n)) x genes [256 gb, min(.., G)) recomputed in fp64 as
+// k_band_fix does, the block's mask bits rewritten (packed: whole 32-bit words; pad genes 0), flips
+// counted. Launched after launch_band_fix on a fixed grid (nothing to do = one load per workgroup).
+void launch_band_tile_fix(const MaskBand& band, const float* A, int64_t lda, const float* W, int64_t ldw,
+                          const float* bias, int H, int n, int G, uint8_t* bits, int64_t ldb, uint8_t* mask,
+                          int64_t ldm, unsigned* flips, hipStream_t s);
+// one workgroup: the decode call's per-call counters -> the workspace's cumulative ones (DecodeCtl);
+// ocount / ocum: the blocks k_band_tile_fix recomputed this call -> their cumulative count
 void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* tiles_single,
                          const unsigned* counts, const unsigned* tfound, const unsigned* flips, unsigned cap,
-                         unsigned long long* cum, hipStream_t s);
+                         unsigned long long* cum, const unsigned* ocount, unsigned long long* ocum, hipStream_t s);
 
 // output layer + threshold (sampling / metrics): u8 mask, packed bits, probs, per-row (TP, FP, FN).
 // big (bf16 only): the bf16x3 split decode -- 256x256 ping-pong tiles over operands in

@@ -1271,6 +1271,79 @@ __global__ __launch_bounds__(256) void k_band_fix(MaskBand band, int ntiles, con
   }
 }
 
+// Whole-block recompute of the blocks whose band entries overflowed the shard list (MaskBand.olist):
+// a work item is 16 rows (fewer for H > 1024: the rows' fp32 activations fill at most 64 KB of LDS) x
+// the block's 256 genes, one gene per thread; each logit sum_k A[row][k] W[gene][k] in fp64 in k
+// order + bias[gene], the bit (float)logit > T as in k_band_fix. Packed bits leave as whole 32-bit
+// words (one wave ballot per row: 64 genes = 2 words), so no atomics: the block's words belong to
+// this item alone, and k_band_fix is done with them (stream order). Rows >= n are not written;
+// genes >= G are 0 (the packed rows' pad bits), words past the row pitch are not written.
+constexpr int kTileFixRows = 16;
+__global__ __launch_bounds__(256) void k_band_tile_fix(const unsigned* __restrict__ olist,
+                                                     const unsigned* __restrict__ ocount, int obn,
+                                                     const float* __restrict__ A, int64_t lda,
+                                                     const float* __restrict__ W, int64_t ldw,
+                                                     const float* __restrict__ bias, int H, int rows_per, int n, int G,
+                                                     uint8_t* bits, int64_t ldb, uint8_t* mask, int64_t ldm,
+                                                     unsigned* flips) {
+  extern __shared__ __attribute__((aligned(16))) float sa[];  // [rows_per][H]
+  const int subs = 256 / rows_per, lane = threadIdx.x & 63;
+  const unsigned items = *ocount * (unsigned)subs;
+  unsigned nflip = 0;
+  for (unsigned it = blockIdx.x; it < items; it += gridDim.x) {
+    const unsigned blk = olist[it / subs];
+    const int m0 = (int)(blk / (unsigned)obn) * 256 + (int)(it % subs) * rows_per;
+    const int g = (int)(blk % (unsigned)obn) * 256 + (int)threadIdx.x;
+    __syncthreads();  // (the previous item's rows are read)
+    for (int i = threadIdx.x; i < rows_per * H; i += 256) {
+      const int r = i / H;
+      sa[i] = m0 + r < n ? A[(int64_t)(m0 + r) * lda + (i - r * H)] : 0.f;
+    }
+    __syncthreads();
+    double acc[kTileFixRows];
+#pragma unroll
+    for (int r = 0; r < kTileFixRows; ++r) acc[r] = 0.0;
+    if (g < G) {
+      const float4* w = (const float4*)(W + (int64_t)g * ldw);
+      for (int k4 = 0; k4 < H / 4; ++k4) {
+        const float4 y = w[k4];
+#pragma unroll
+        for (int r = 0; r < kTileFixRows; ++r) {
+          if (r < rows_per) {
+            const float4 x = *(const float4*)(sa + r * H + 4 * k4);
+            acc[r] = fma((double)x.x, (double)y.x, acc[r]);
+            acc[r] = fma((double)x.y, (double)y.y, acc[r]);
+            acc[r] = fma((double)x.z, (double)y.z, acc[r]);
+            acc[r] = fma((double)x.w, (double)y.w, acc[r]);
+          }
+        }
+      }
+    }
+    const double b = g < G ? (double)bias[g] : 0.0;
+#pragma unroll
+    for (int r = 0; r < kTileFixRows; ++r) {
+      const int row = m0 + r;
+      if (r >= rows_per || row >= n) continue;  // (uniform)
+      const bool pred = g < G && (float)(acc[r] + b) > kMaskLogitThreshold;
+      if (bits) {
+        const uint64_t bal = __ballot(pred);
+        const int64_t byte = (int64_t)(g - lane) / 8 + 4 * (lane & 1);  // word (lane & 1) of the wave's 64 genes
+        if (lane < 2 && byte + 4 <= ldb) {
+          unsigned* word = (unsigned*)(bits + (int64_t)row * ldb + byte);
+          const unsigned v = (unsigned)(bal >> (32 * lane));
+          nflip += __popc(*word ^ v);
+          *word = v;
+        }
+      } else if (g < G) {
+        uint8_t* p = mask + (int64_t)row * ldm + g;
+        nflip += (*p != 0) != pred;
+        *p = pred ? 1 : 0;
+      }
+    }
+  }
+  if (nflip) atomicAdd(flips, nflip);
+}
+
 // the decode call's counters -> the workspace's cumulative ones: cum[0] split tiles, [1] exact
 // tiles, [2] band elements found, [3] bits the recompute flipped, [4] band elements beyond the
 // list's capacity (left as the kernels decided them), [5] decodes with split or single tiles, [6]
@@ -1281,7 +1354,8 @@ __global__ __launch_bounds__(64) void k_decode_stats(const unsigned* __restrict_
                                                      const unsigned* __restrict__ counts,
                                                      const unsigned* __restrict__ tfound,
                                                      const unsigned* __restrict__ flips, unsigned cap,
-                                                     unsigned long long* cum) {
+                                                     unsigned long long* cum, const unsigned* __restrict__ ocount,
+                                                     unsigned long long* ocum) {
   const int t = threadIdx.x;
   unsigned long long a = t < kSplitShards ? tiles_split[t] : 0ull, b = t < kSplitShards ? tiles_exact[t] : 0ull;
   unsigned long long g = t < kSplitShards ? tiles_single[t] : 0ull;
@@ -1303,6 +1377,7 @@ __global__ __launch_bounds__(64) void k_decode_stats(const unsigned* __restrict_
     cum[4] += over;
     cum[a || g ? 5 : 6] += 1;
     cum[7] += g;
+    *ocum += *ocount;
   }
 }
 
@@ -1531,10 +1606,28 @@ void launch_band_fix(const MaskBand& band, int ntiles, const float* A, int64_t l
 
 void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* tiles_single,
                          const unsigned* counts, const unsigned* tfound, const unsigned* flips, unsigned cap,
-                         unsigned long long* cum, hipStream_t s) {
+                         unsigned long long* cum, const unsigned* ocount, unsigned long long* ocum, hipStream_t s) {
   static_assert(kSplitShards <= 64 && kBandShards <= 64, "one wave");
   hipLaunchKernelGGL(k_decode_stats, dim3(1), dim3(64), 0, s, tiles_split, tiles_exact, tiles_single, counts, tfound, flips, cap,
-                     cum);
+                     cum, ocount, ocum);
+  GM2_CHECK_LAUNCH();
+}
+
+void launch_band_tile_fix(const MaskBand& band, const float* A, int64_t lda, const float* W, int64_t ldw,
+                          const float* bias, int H, int n, int G, uint8_t* bits, int64_t ldb, uint8_t* mask,
+                          int64_t ldm, unsigned* flips, hipStream_t s) {
+  if ((!bits && !mask) || (bits && (ldb & 3)) || H < 4 || H % 4 || (((uintptr_t)W | (uintptr_t)(ldw * 4)) & 15))
+    throw Gm2Error("band tile fix: packed bits with 4-B aligned rows or a u8 mask, H %% 4 == 0, 16-B aligned weight rows");
+  if (!band.olist || !band.ocount || band.obn <= 0 || n < 0 || G < 0)
+    throw Gm2Error("band tile fix: the overflow block list and counter required");
+  // rows per work item: a power of two <= 16 whose fp32 rows fit 64 KB of LDS
+  int rows_per = kTileFixRows;
+  while (rows_per > 1 && (int64_t)rows_per * H * 4 > 65536) rows_per /= 2;
+  const size_t lds = (size_t)rows_per * H * 4;
+  if (lds > 65536) throw Gm2Error("band tile fix: hidden width %d too large", H);
+  // (<= 64 KB: within the default dynamic-LDS limit, no attribute needed)
+  hipLaunchKernelGGL(k_band_tile_fix, dim3(512), dim3(256), lds, s, band.olist, band.ocount, band.obn, A, lda, W, ldw,
+                     bias, H, rows_per, n, G, bits, ldb, mask, ldm, flips);
   GM2_CHECK_LAUNCH();
 }
 

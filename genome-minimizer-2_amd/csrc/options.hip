@@ -76,6 +76,14 @@ void option_set(Options& o, int key, int value) {
     case GM2_OPT_GRAD_BUCKETS: o.grad_buckets = value ? 1 : 0; break;
     case GM2_OPT_SAMPLE_SPLIT: o.sample_split = value ? 1 : 0; break;
     case GM2_OPT_SAMPLE_SINGLE: o.sample_single = value ? 1 : 0; break;
+    case GM2_OPT_SAMPLE_BAND_CAP:
+      if (value < 1 || value > (int)kBandShardCap) throw Gm2Error("band list cap %d: 1..%u", value, kBandShardCap);
+      o.band_cap = value;
+      break;
+    case GM2_OPT_SAMPLE_SINGLE_BOUND:
+      if (value < 1 || value > 1000000) throw Gm2Error("single-tier bound %d (x 1e-3): 1..1000000", value);
+      o.single_bound_milli = value;
+      break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -95,6 +103,8 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_GRAD_BUCKETS: return o.grad_buckets;
     case GM2_OPT_SAMPLE_SPLIT: return o.sample_split;
     case GM2_OPT_SAMPLE_SINGLE: return o.sample_single;
+    case GM2_OPT_SAMPLE_BAND_CAP: return o.band_cap;
+    case GM2_OPT_SAMPLE_SINGLE_BOUND: return o.single_bound_milli;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

@@ -112,7 +112,7 @@ def bf16_exchange_sum(dist, x, scratch=None):
     parts = recv.view(world, c)
     if dev:
         mine = sc.setdefault("mine", torch.empty(0, dtype=torch.bfloat16, device=x.device))
-        if mine.numel() < c:
+        if mine.numel() < c or mine.device != x.device:  # (a scratch dict reused across devices)
             mine = sc["mine"] = torch.empty(c, dtype=torch.bfloat16, device=x.device)
         mine = mine[:c]
         native.exchange_ranksum(recv, world, mine)

@@ -106,6 +106,8 @@ class VAE:
             self.params = self.params.to(device)
             self.bn = self.bn.to(device)
         self.device = device
+        for prec, ws in self._workspaces.items():
+            self._retire_workspace(ws, prec)
         self._workspaces.clear()
         self.touch()
         return self
@@ -171,21 +173,20 @@ class VAE:
         return self
 
     # ------------------------------------------------------------------ native workspaces
-    def _carry_decode_stats(self, ws):
-        """(a larger fp32 workspace replaced the previous one: its counters start at zero, so the
-        previous workspace's totals are kept on the host and added back by decode_stats)"""
-        if getattr(self, "_stats_ws", None) is not ws:
-            old = getattr(self, "_stats_ws", None)
-            if old is not None:
-                base = getattr(self, "_stats_base", {})
-                self._stats_base = {k: base.get(k, 0) + old.stat(v) for k, v in native.DECODE_STATS.items()}
-            self._stats_ws = ws
+    def _retire_workspace(self, ws, prec):
+        """An fp32 (sampling) workspace is about to be replaced or dropped: its decode counters
+        start at zero in the next one, so its totals are kept on the host and decode_stats adds
+        them back (whichever caller swapped it: a decode, an fp32 train/eval call, or `to`)."""
+        if ws is not None and prec == native.GM2_F32:
+            base = getattr(self, "_stats_base", {})
+            self._stats_base = {k: base.get(k, 0) + ws.stat(v) for k, v in native.DECODE_STATS.items()}
 
     def workspace(self, prec, batch_max):
         """Workspace for (precision, capacity); reused while large enough."""
         key = prec
         ws = self._workspaces.get(key)
         if ws is None or ws.d.batch_max < batch_max:
+            self._retire_workspace(ws, key)
             cap = max(int(batch_max), ws.d.batch_max if ws else 0)
             ws = native.Workspace(native.dims(self.input_dim, self.hidden_dim, self.latent_dim, cap), prec,
                                   self.device)
@@ -265,7 +266,6 @@ class VAE:
         for s in range(0, N, chunk):
             n = min(chunk, N - s)
             ws = self.workspace(native.GM2_F32, min(chunk, N))
-            self._carry_decode_stats(ws)
             native.decode_mask(ws, self.params, self.bn, z[s:s + n], n, mask[s:], G,
                                None if probs is None else probs[s:], G)
         return mask, probs
@@ -281,7 +281,6 @@ class VAE:
         for s in range(0, N, chunk):
             n = min(chunk, N - s)
             ws = self.workspace(native.GM2_F32, min(chunk, N))
-            self._carry_decode_stats(ws)
             native.decode_bits(ws, self.params, self.bn, z[s:s + n], n, pm.bits[s:], pm.ld,
                                None if probs is None else probs[s:], G)
         return pm, probs
@@ -289,9 +288,10 @@ class VAE:
     def decode_stats(self):
         """The sampling decodes' counters on this model's fp32 (sampling) workspace, cumulative
         (gm2.h GM2_STAT_*): decodes and output-layer tiles per path (bf16x3 split / exact fp32),
-        logits of the certified band recomputed in fp64, the mask bits that recompute flipped, and
-        band elements beyond a call's list capacity. Zeros before the first decode. Waits for the
-        device."""
+        logits of the certified band recomputed in fp64, the mask bits that recompute flipped,
+        band elements beyond a call's list capacity and the 256 x 256 blocks recomputed whole in fp64
+        for them. Zeros before the first decode; monotone across workspace replacements. Waits for
+        the device."""
         ws = self._workspaces.get(native.GM2_F32)
         base = getattr(self, "_stats_base", {})
         return {k: base.get(k, 0) + (ws.stat(v) if ws is not None else 0) for k, v in native.DECODE_STATS.items()}

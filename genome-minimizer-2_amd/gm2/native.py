@@ -36,20 +36,23 @@ EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_of
            "gm2_resident_layout", "gm2_resident_build",
            "gm2_timing_begin", "gm2_timing_end", "gm2_workspace_stat",
            "gm2_exchange_pack", "gm2_exchange_ranksum", "gm2_exchange_unpack"]
-ABI_VERSION = 5
+ABI_VERSION = 6
 KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
 OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE, OPT_SMALL_SPLIT, OPT_BN_EPILOGUE, OPT_SMALL_WAVES = 1, 2, 3, 4, 5, 6
 OPT_INPUT_CHUNKS, OPT_GRID_CAP, OPT_SYNC_BN, OPT_DEFER_OUTPUT_ADAM = 7, 9, 10, 11
 OPT_GRAD_BUCKETS = 15
 OPT_SAMPLE_SPLIT = 18
 OPT_SAMPLE_SINGLE = 20
+OPT_SAMPLE_BAND_CAP, OPT_SAMPLE_SINGLE_BOUND = 21, 22
 STAT_SPLIT_DECODES, STAT_EXACT_DECODES, STAT_SPLIT_TILES, STAT_EXACT_TILES = 1, 2, 3, 4
 STAT_BAND_ELEMENTS, STAT_BAND_FLIPS, STAT_BAND_OVERFLOW, STAT_SINGLE_TILES = 5, 6, 7, 8
+STAT_OVERFLOW_TILES = 9
 # the sampling decode's counters by name (gm2.h GM2_STAT_*)
 DECODE_STATS = {"split_decodes": STAT_SPLIT_DECODES, "exact_decodes": STAT_EXACT_DECODES,
                 "split_tiles": STAT_SPLIT_TILES, "exact_tiles": STAT_EXACT_TILES,
                 "band_elements": STAT_BAND_ELEMENTS, "band_flips": STAT_BAND_FLIPS,
-                "band_overflow": STAT_BAND_OVERFLOW, "single_tiles": STAT_SINGLE_TILES}
+                "band_overflow": STAT_BAND_OVERFLOW, "single_tiles": STAT_SINGLE_TILES,
+                "overflow_tiles": STAT_OVERFLOW_TILES}
 # gm2_allreduce_fn (gm2.h): int (double* buf, int64_t count, void* stream, void* user)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
 

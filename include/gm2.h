@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GM2_ABI_VERSION 5
+#define GM2_ABI_VERSION 6
 #define GM2_NUM_PARAMS 30 /* tensors in model.parameters() */
 #define GM2_NUM_SCALARS 16
 
@@ -119,7 +119,11 @@ int gm2_workspace_size(const gm2_dims* d, int precision, size_t* bytes);
  * options (copied from the process defaults here), its side stream, its gradient-bucket events and
  * its staged input slot. Nothing is shared between workspaces, so two models (or a training and a
  * sampling workspace) can be used in one process; one workspace is used from one host thread at a
- * time. gm2_workspace_release drops that state (call it before freeing the device memory). */
+ * time. gm2_workspace_release drops that state (call it before freeing the device memory). A
+ * still-QUEUED output-layer Adam update (GM2_OPT_DEFER_OUTPUT_ADAM) is discarded, not launched
+ * (release may run after the parameter buffers it would write were freed): call gm2_workspace_join
+ * first to keep it. Returns 1 (with gm2_last_error saying so) when an update was discarded, 0 when
+ * nothing was pending; the state is released either way. */
 int gm2_workspace_init(const gm2_dims* d, int precision, void* ws, size_t ws_bytes, void* stream);
 int gm2_workspace_release(void* ws);
 
@@ -333,7 +337,15 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       largest ||a_r||_2 x its largest ||w_g||_2 is at most 0.25 run ONE bf16 GEMM
  *                       over the rounded operands (a third of the split's MFMA work) with a
  *                       correspondingly wider certified band, recomputed in fp64 the same way;
- *                       0 = split or exact only. */
+ *                       0 = split or exact only.
+ *   GM2_OPT_SAMPLE_BAND_CAP (ABI 6) entries per shard of the certified band's list per decode call
+ *                       (1..65536, default 65536; 64 shards). Entries past a shard's capacity are
+ *                       not dropped: their 256 x 256 output block (genome rows x genes) is recomputed
+ *                       whole in fp64 after the band recompute (GM2_STAT_OVERFLOW_TILES), so the
+ *                       masks do not depend on this value; smaller values exercise that path.
+ *   GM2_OPT_SAMPLE_SINGLE_BOUND (ABI 6) the single tier's gate x 1000 (default 250 = 0.25, 1..1e6):
+ *                       larger values send more tiles to the single tier (a wider band; a tile
+ *                       whose band overflows its slots re-runs as bf16x3). Cost only, never the masks. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -347,7 +359,9 @@ enum {
   GM2_OPT_DEFER_OUTPUT_ADAM = 11,
   GM2_OPT_GRAD_BUCKETS = 15,
   GM2_OPT_SAMPLE_SPLIT = 18,
-  GM2_OPT_SAMPLE_SINGLE = 20
+  GM2_OPT_SAMPLE_SINGLE = 20,
+  GM2_OPT_SAMPLE_BAND_CAP = 21,
+  GM2_OPT_SAMPLE_SINGLE_BOUND = 22
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);
@@ -368,9 +382,11 @@ int gm2_workspace_join(void* ws, void* stream);
  *                           coef * ||a_r||_2 ||w_g||_2 (evaluated with the largest
  *                           of 4 neighbouring rows' norms, so a small superset) and recomputed in fp64
  *   GM2_STAT_BAND_FLIPS     mask bits that recompute changed
- *   GM2_STAT_BAND_OVERFLOW  band elements beyond a call's list capacity (256 slots per split or
- *                           single tile, then 64 shards x 65,536), left as computed
- *   GM2_STAT_SINGLE_TILES   output-layer tiles (256 x 256) the single-product kernel ran */
+ *   GM2_STAT_BAND_OVERFLOW  band elements beyond a call's list capacity (256 slots per split
+ *                           tile, then 64 shards x GM2_OPT_SAMPLE_BAND_CAP); each one's 256 x 256
+ *                           block is recomputed whole in fp64 (ABI 6: no bit is left as computed)
+ *   GM2_STAT_SINGLE_TILES   output-layer tiles (256 x 256) the single-product kernel ran
+ *   GM2_STAT_OVERFLOW_TILES 256 x 256 blocks recomputed whole in fp64 after a list overflow */
 enum {
   GM2_STAT_SPLIT_DECODES = 1,
   GM2_STAT_EXACT_DECODES = 2,
@@ -379,7 +395,8 @@ enum {
   GM2_STAT_BAND_ELEMENTS = 5,
   GM2_STAT_BAND_FLIPS = 6,
   GM2_STAT_BAND_OVERFLOW = 7,
-  GM2_STAT_SINGLE_TILES = 8
+  GM2_STAT_SINGLE_TILES = 8,
+  GM2_STAT_OVERFLOW_TILES = 9
 };
 int gm2_workspace_stat(void* ws, int key, int64_t* value);
 

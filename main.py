@@ -213,7 +213,8 @@ def run_sampling(args):
     print(f"- Decode (rank {rank}): {st['single_tiles']} bf16 / {st['split_tiles']} bf16x3 / {st['exact_tiles']} fp32 "
           f"output tiles; "
           f"{st['band_elements']} band logits recomputed in fp64, {st['band_flips']} bits changed"
-          + (f", {st['band_overflow']} past the list" if st["band_overflow"] else ""))
+          + (f"; {st['band_overflow']} past the list, their {st['overflow_tiles']} blocks recomputed whole in fp64"
+             if st["band_overflow"] else ""))
     if dist is not None:
         # the ranks' packed slices -> the full set (rank 0 writes the reference's files)
         from gm2.masks import PackedMasks

@@ -4,7 +4,9 @@
     G = 55,039;
   * C5's per-GPU step (configs[4]): v0 on the 20,000-gene synthetic matrix (G padded to 20,224 =
     79 x 256 in the bf16 workspace, so every G-wide GEMM takes the 256x256 tiles);
-each on a batch of 4096 strain rows of a synthetic pan-genome matrix. One full libgm2 step
+each on a batch of 4096 strain rows of a synthetic pan-genome matrix; and the drop-in's own small
+batches at F4 width (C1's batch 64 for v0, the reference's default batch 32 for v0 and v1). One
+full libgm2 step
 (gm2_train_fwd_bwd + gm2_grad_norm + gm2_adam_step) against the oracle's explicit gradients
 (oracle.manual_grads_emulated: the math of the CPU oracle pinned to the reference's goldens)
 evaluated on the device:
@@ -43,8 +45,15 @@ pytestmark = pytest.mark.gpu
 
 B = 4096
 BETA = 0.1
-# (name, G, H, L, w*gamma, lambda): v0 / v1 hyper-parameters at epoch 0 (experiments.py:42-73)
-CONFIGS = {"C2": (55039, 1024, 64, 0.0, 0.0), "C3": (55039, 512, 32, 1.0, 0.01), "C5": (20000, 1024, 64, 0.0, 0.0)}
+# (name, G, H, L, w*gamma, lambda, batch): v0 / v1 hyper-parameters at epoch 0 (experiments.py:42-73).
+# C1_b64 / C1_b32 / v1_b32 (verdict r5): the drop-in's own batch sizes at F4 width -- C1's batch 64
+# (BASELINE configs[0]) and the reference's default batch 32 (utils/custom_config.py:25,
+# utils/experiments.py:247) for v0 and v1 -- which take the small-M GEMM plans (split-K over the
+# 55,040-long K of the input layer's weight gradient, 128-row tiles) instead of the 256x256 ones.
+CONFIGS = {"C2": (55039, 1024, 64, 0.0, 0.0, B), "C3": (55039, 512, 32, 1.0, 0.01, B),
+           "C5": (20000, 1024, 64, 0.0, 0.0, B),
+           "C1_b64": (55039, 1024, 64, 0.0, 0.0, 64), "C1_b32": (55039, 1024, 64, 0.0, 0.0, 32),
+           "v1_b32": (55039, 512, 32, 1.0, 0.01, 32)}
 
 
 def _prebn_bias(name):
@@ -58,26 +67,26 @@ _STATES = {}
 def _state(cfg):
     if cfg not in _STATES:
         from gm2.data import synthetic_pangenome
-        G, H, L, _, _ = CONFIGS[cfg]
+        G, H, L, _, _, Bc = CONFIGS[cfg]
         torch.manual_seed(2024)
         P = O.init_params(G, H, L)
         S = O.init_bn_state(H)
         P, S = perturb_bn(P, S, 99)
-        X = synthetic_pangenome(B, G, seed=12345)
+        X = synthetic_pangenome(Bc, G, seed=12345)
         torch.manual_seed(5)
-        eps = torch.randn(B, L)
+        eps = torch.randn(Bc, L)
         _STATES.clear()  # one configuration's host state at a time
         _STATES[cfg] = (P, S, X, eps)
     return _STATES[cfg]
 
 
 @pytest.mark.parametrize("prec", ["f32", "bf16"])
-@pytest.mark.parametrize("cfg", ["C2", "C3", "C5"])
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C5", "C1_b64", "C1_b32", "v1_b32"])
 def test_train_step_real_dims(cfg, prec):
     from gm2 import native
     from gm2.data import ResidentMatrix
     from gpu_helpers import scalars, to_model
-    G, H, L, WG, LAM = CONFIGS[cfg]
+    G, H, L, WG, LAM, B = CONFIGS[cfg]
     P, S, X, eps = _state(cfg)
     pr = native.GM2_F32 if prec == "f32" else native.GM2_BF16
     m = to_model(P, S, G, H, L, pr)

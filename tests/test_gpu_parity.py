@@ -157,6 +157,8 @@ def test_decode_masks_golden_bit_exact():
     assert st1["exact_decodes"] - st0["exact_decodes"] == 1 and st1["split_tiles"] == st0["split_tiles"]
     bad, band = _band_ok(mask.cpu().numpy(), g[f"{tag}_mask"], g[f"{tag}_logit64"])
     assert bad == 0, (bad, band)
+    # (verdict r5: every bit of the reference's own mask, inside the band too)
+    np.testing.assert_array_equal(mask.cpu().numpy(), g[f"{tag}_mask"])
     np.testing.assert_allclose(p.cpu().numpy(), g[f"{tag}_p"], rtol=1e-5, atol=1e-6)
     # the default path (no probs): gated per 256 x 256 tile. The focused z (one latent point plus
     # 0.1 noise, main.py:351-370) keeps the activations small enough that both tiles (64 genomes x
@@ -188,6 +190,7 @@ def test_decode_masks_golden_bit_exact():
     assert d["split_decodes"] + d["exact_decodes"] == 1 and d["single_tiles"] + d["split_tiles"] + d["exact_tiles"] > 0, d
     bad, band = _band_ok(gm.cpu().numpy(), g[f"{tag}_mask"], g[f"{tag}_logit64"])
     assert bad == 0, (bad, band)
+    np.testing.assert_array_equal(gm.cpu().numpy(), g[f"{tag}_mask"])
 
 
 @pytest.mark.parametrize("G,H,L,N", [(1000, 128, 16, 300), (3000, 512, 32, 2000), (2500, 1024, 64, 700)])
@@ -695,4 +698,34 @@ def test_deferred_output_adam_bit_identical(prec):
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert torch.equal(a, b)
+
+
+def test_release_reports_a_discarded_queued_update():
+    """ADVICE r5 (api.hip ws_release): gm2_workspace_release with an output-layer Adam update still
+    QUEUED (GM2_OPT_DEFER_OUTPUT_ADAM, no join) discards it and says so -- return 1 and a
+    gm2_last_error message -- while a joined workspace releases with 0."""
+    G, H, L, B = 1000, 128, 16, 256
+    P, S = perturb_bn(*oracle_state(G, H, L, 75), seed=76)
+    X = synth_x(B, G, 77)
+    for join in (True, False):
+        m = to_model(P, S, G, H, L, native.GM2_BF16)
+        mat = ResidentMatrix(X)
+        ws = m.workspace(native.GM2_BF16, B)
+        ws.set_option(native.OPT_DEFER_OUTPUT_ADAM, 1)
+        grads, mom, vel = torch.zeros_like(m.params), torch.zeros_like(m.params), torch.zeros_like(m.params)
+        sc = scalars(beta=0.5, wgamma=0.0, lam=0.0, step=1)
+        loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+        eps = torch.randn(B, L, generator=torch.Generator().manual_seed(78)).cuda()
+        native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, B, eps), m.params, grads, m.bn, sc, loss)
+        native.grad_norm(ws, m.params, grads, sc, loss)
+        native.adam_step(ws, m.params, grads, mom, vel, sc)
+        if join:
+            ws.join()
+        torch.cuda.synchronize()
+        rc = native.lib().gm2_workspace_release(ws.ptr)
+        if join:
+            assert rc == 0
+        else:
+            assert rc == 1 and "discarded" in native.lib().gm2_last_error().decode()
+        assert native.lib().gm2_workspace_release(ws.ptr) == 0  # (released: unknown state is a no-op)
 

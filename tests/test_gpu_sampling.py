@@ -12,7 +12,9 @@
     with the certified-band fp64 recompute, and the exact path on the same fixture; every test that
     decodes asserts which path ran from the workspace counters (gm2.h GM2_STAT_*).
 Bar: masks bit-exact to the oracle's fp32 decode outside the fp64 rounding band of each logit
-(|logit64| <= 1e-3: counted, reported, not asserted), probabilities rel 2e-5.
+(|logit64| <= 1e-3: counted, reported), probabilities rel 2e-5; on the reference-produced fixture
+every bit (the band included) equals the reference's; with the band list forced to overflow every
+bit equals the correctly rounded fp64 logit's decision.
 """
 import numpy as np
 import pytest
@@ -241,6 +243,18 @@ def test_split3_decode_falls_back_when_the_bound_is_too_large():
     diff = int((res[0][0] != res[1][0]).sum())
     assert diff <= res[0][1]["band_flips"], (diff, res[0][1])
     assert _masks_ok(res[0][0], P, S, z) == 0 and _masks_ok(res[1][0], P, S, z) == 0
+    # the exact tiles' band entries go straight to the shard lists: with one entry per shard, a tile
+    # holding two or more overflows and is recomputed whole in fp64 -- the same masks
+    ws = m.workspace(native.GM2_F32, N)
+    ws.set_option(native.OPT_SAMPLE_SPLIT, 1)
+    ws.set_option(native.OPT_SAMPLE_BAND_CAP, 1)
+    before = m.decode_stats()
+    mask, _ = m.decode_mask(z)
+    d = _delta(before, m.decode_stats())
+    ws.set_option(native.OPT_SAMPLE_BAND_CAP, 65536)
+    print(f"band list capacity 1: {d}")
+    assert (d["overflow_tiles"] > 0) == (d["band_overflow"] > 0), d
+    np.testing.assert_array_equal(mask.cpu().numpy().astype(bool), res[0][0])
 
 
 def _split_fixture():
@@ -300,7 +314,8 @@ def test_split_fixture_gated_decode_matches_reference(single):
         band = np.abs(l64) <= 1e-3
         bad = (got != ref) & ~band
         print(f"{int(((got != ref) & band).sum())} reference mismatches inside the 1e-3 band, {int(bad.sum())} outside")
-        assert int(bad.sum()) == 0
+        # (verdict r5: the reference's own masks, every bit -- inside the band too)
+        np.testing.assert_array_equal(got, ref)
         # the fp64 decision: (float)logit64 > T
         dec64 = l64.astype(np.float32) > np.float32(8.940696716308594e-08)
         known = np.isfinite(l64) & (np.abs(l64) > 2e-5)
@@ -323,6 +338,78 @@ def test_split_fixture_exact_path_matches_reference():
     band = np.abs(l64) <= 1e-3
     print(f"{int(((got != ref) & band).sum())} mismatches inside the 1e-3 band")
     assert int(((got != ref) & ~band).sum()) == 0
+    np.testing.assert_array_equal(got, ref)  # (every bit, the band included)
+
+
+def _hidden32(P, S, z):
+    """the decoder's last hidden activations in fp32 (the oracle's eval-mode blocks)"""
+    with torch.no_grad():
+        h = z.float()
+        for i in range(3):
+            h = O._block(P, S, f"decoder.{3*i}", f"decoder.{3*i+1}", h, False)
+    return h
+
+
+@pytest.mark.parametrize("single", [1, 0])
+def test_band_overflow_recomputed_whole_blocks(single):
+    """Verdict r5 "next" 1 / ADVICE r5: every logit sits inside the certified band, so the band list
+    overflows, and no bit may be left as a bf16 tier decided it. The output weights are scaled to
+    ~1e-14 and every gene's bias is the threshold T itself (0x33C00000): each logit is T + delta with
+    |delta| of a few fp32 ulps of T (ulp 2^-47), far inside every tier's band (its 2^-20 T floor).
+      * single tier on: every tile's band overflows its 256 slots, so each re-runs as bf16x3 in place
+        (counted as split, ADVICE r5 gemm.hip:1408), whose band spills to the shard lists;
+      * with the default shard capacity (64 x 65,536) k_band_fix recomputes every element; with
+        GM2_OPT_SAMPLE_BAND_CAP = 64 the shards overflow and EVERY tile is recomputed whole in fp64
+        by k_band_tile_fix (GM2_STAT_OVERFLOW_TILES);
+    packed and u8 outputs, both capacities and both tier settings give the same bits, and those equal
+    the correctly rounded fp64 logit's decision (float)(a . w + b) > T from the fp32 activations,
+    except where the fp64 logit lies within 1e-20 of an fp32 rounding midpoint (the host's fp32
+    hidden layers differ from the device's by ~1e-7 relative, i.e. ~1e-21 in these logits)."""
+    G, H, L, N = 1000, 128, 16, 600
+    P, S = perturb_bn(*oracle_state(G, H, L, 70), seed=71)
+    T = np.float32(8.940696716308594e-08)
+    assert T.view(np.uint32) == 0x33C00000
+    P["decoder.9.weight"] = P["decoder.9.weight"] * 1e-14
+    P["decoder.9.bias"] = torch.full((G,), float(T))
+    m = to_model(P, S, G, H, L, native.GM2_F32)
+    m.eval()
+    z = torch.randn(N, L, generator=torch.Generator().manual_seed(72))
+    tiles = ((N + 255) // 256) * ((G + 255) // 256)
+    ws = m.workspace(native.GM2_F32, N)
+    ws.set_option(native.OPT_SAMPLE_SINGLE, single)
+    outs = []
+    for cap in (65536, 64):
+        ws.set_option(native.OPT_SAMPLE_BAND_CAP, cap)
+        st0 = m.decode_stats()
+        pm, _ = m.decode_bits(z)
+        mask, _ = m.decode_mask(z)
+        d = _delta(st0, m.decode_stats())
+        print(f"single {single} cap {cap}: {d}")
+        # both calls gated; every tile ran bf16x3 (single-tier tiles re-run as split after their slots overflowed)
+        assert d["split_decodes"] == 2 and d["exact_decodes"] == 0, d
+        assert d["split_tiles"] == 2 * tiles and d["single_tiles"] == 0 and d["exact_tiles"] == 0, d
+        assert d["band_elements"] >= 2 * N * G, d  # (pad genes are never in the band; every real logit is)
+        if cap == 65536:
+            assert d["band_overflow"] == 0 and d["overflow_tiles"] == 0, d
+        else:
+            assert d["band_overflow"] > 0 and d["overflow_tiles"] == 2 * tiles, d
+        bits = np.unpackbits(pm.bits.cpu().numpy(), axis=1, bitorder="little")
+        assert not bits[:, G:].any(), "pad bits beyond G must stay zero"
+        np.testing.assert_array_equal(bits[:, :G], mask.cpu().numpy())
+        outs.append(bits[:, :G].astype(bool))
+    ws.set_option(native.OPT_SAMPLE_BAND_CAP, 65536)
+    ws.set_option(native.OPT_SAMPLE_SINGLE, 1)
+    np.testing.assert_array_equal(outs[0], outs[1])
+    a = _hidden32(P, S, z).double().numpy()
+    l64 = a @ P["decoder.9.weight"].double().numpy().T + np.float64(T)
+    dec = l64.astype(np.float32) > T
+    # distance to the nearest fp32 rounding midpoint around T (ulp(T) = 2^-47 on both sides here)
+    ulp = 2.0 ** -47
+    frac = (l64 - float(T)) / ulp
+    ambiguous = np.abs(frac - np.round(frac - 0.5) - 0.5) * ulp < 1e-20
+    print(f"{int(dec.sum())} of {dec.size} bits set; {int(ambiguous.sum())} ambiguous")
+    assert dec.any() and not dec.all()
+    assert int(((outs[0] != dec) & ~ambiguous).sum()) == 0
 
 
 def test_odd_latent_width_decodes_on_the_exact_path():

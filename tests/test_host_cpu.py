@@ -34,12 +34,14 @@ def test_header_constants_match_binding():
     and reject values without a GPU, and the bucket bounds tile the gradient buffer in order. ABI 3:
     options and bucket events are per workspace; a workspace libgm2 never initialised is refused.
     ABI 4: gm2_batch gains the resident-operand fields; gm2_resident_layout sizes them. ABI 5: seven
-    tuning options pruned (their keys now refused), the sampling decode's GM2_STAT_* counters."""
+    tuning options pruned (their keys now refused), the sampling decode's GM2_STAT_* counters. ABI 6:
+    band-list overflow recomputed whole per block (GM2_STAT_OVERFLOW_TILES), the list capacity and the
+    single tier's gate as workspace options."""
     import ctypes
     from gm2 import native
     txt = open(os.path.join(ROOT, "include", "gm2.h")).read()
     assert int(re.search(r"#define GM2_ABI_VERSION (\d+)", txt).group(1)) == native.lib().gm2_abi_version() \
-        == native.ABI_VERSION == 5
+        == native.ABI_VERSION == 6
     bogus = ctypes.c_void_p(0x1000)
     v = ctypes.c_int()
     assert native.lib().gm2_workspace_set_option(bogus, native.OPT_GRID_CAP, 1) != 0
@@ -52,7 +54,7 @@ def test_header_constants_match_binding():
     for k, v in opts.items():
         assert getattr(native, "OPT_" + k) == v, k
     stats = dict((k, int(v)) for k, v in re.findall(r"GM2_STAT_([A-Z_]+) = (\d+)", txt))
-    assert len(stats) == 8 and set(native.DECODE_STATS.values()) == set(stats.values())
+    assert len(stats) == 9 and set(native.DECODE_STATS.values()) == set(stats.values())
     for k, v in stats.items():
         assert getattr(native, "STAT_" + k) == v, k
     assert [f[0] for f in native.Batch._fields_] == ["data", "ld_data", "rows", "n", "eps", "next", "resident",
@@ -78,6 +80,14 @@ def test_header_constants_match_binding():
         native.set_option(native.OPT_INPUT_CHUNKS, 2)
     with pytest.raises(RuntimeError, match="4 or 8"):
         native.set_option(native.OPT_SMALL_WAVES, 5)
+    native.set_option(native.OPT_SAMPLE_BAND_CAP, 7)
+    assert native.get_option(native.OPT_SAMPLE_BAND_CAP) == 7
+    native.set_option(native.OPT_SAMPLE_BAND_CAP, 65536)
+    with pytest.raises(RuntimeError, match="band list cap"):
+        native.set_option(native.OPT_SAMPLE_BAND_CAP, 65537)
+    with pytest.raises(RuntimeError, match="single-tier bound"):
+        native.set_option(native.OPT_SAMPLE_SINGLE_BOUND, 0)
+    assert native.get_option(native.OPT_SAMPLE_SINGLE_BOUND) == 250
     # the options pruned in ABI 5 (measured slower or neutral; evidence kept in profiles/) are gone
     for key in (8, 12, 13, 14, 16, 17, 19):
         with pytest.raises(RuntimeError, match="unknown option"):
