@@ -13,9 +13,13 @@ SUM-all-reduced over RCCL every step (weak scaling: value = all ranks' rows / ma
 
 Also reported (extra fields, not `value`): sampling throughput of `--mode sample` for the v1 preset
 (C3: 1e6 genomes from a v1 checkpoint trained on the synthetic matrix, decoded with the output layer
-gated per tile between bf16x3 and exact fp32 and the certified band recomputed in fp64, thresholded
-into packed masks, essential genes counted on the device, masks + counts copied to pinned host
-memory; the split fraction and band counts are reported), the same training step in the other GEMM
+gated per 256 x 256 tile between one bf16 product over the rounded operands (the single tier), the
+bf16x3 split and exact fp32, the certified band recomputed in fp64 (a list overflow recomputes its
+blocks whole), thresholded into packed masks, essential genes counted on the device, masks + counts
+copied to pinned host memory; the tier fractions and band counts are reported), the v1 / v2 / v3
+training steps at C3 / C4's per-GPU dims (hidden 512, latent 32, gene abundance + L1, cosine KL for
+v2 / v3), the C1 workload on the GPU (v0 at batch 64 and at the CLI default 32, F4 width), the same
+training step in the other GEMM
 precision (f32 next to the bf16 headline), the live-timed dominant kernel against the MFMA roofline,
 and the CPU baseline (the oracle = the reference's algorithm on torch-CPU, fp32, all host threads,
 the same v0 step at batch 4096 on the same matrix; plus the C1 batch-64 point), and the C5-shaped
@@ -523,8 +527,9 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
     """C3: v1 preset (hidden 512, latent 32) `--mode sample` of a.sample_genomes genomes (1e6 by
     default) in 65,536-genome chunks from a trained v1 checkpoint (train_v1_checkpoint): z ~ N(0, I)
     drawn on the device (extras.py:197), the decode (fp32 hidden layers; the output layer gated per
-    tile between bf16x3 and exact fp32, certified band recomputed in fp64) + threshold into packed
-    masks in HBM (gm2_decode_bits), the essential-gene counts of
+    256 x 256 tile between the single bf16 product, the bf16x3 split and exact fp32, certified band
+    recomputed in fp64) + threshold into packed masks in HBM (gm2_decode_bits), the essential-gene
+    counts of
     every genome on the device (gm2_mask_count_groups, a synthetic 300-gene essential table), and
     the packed masks + counts copied to pinned host memory on a second stream (overlapping the next
     chunk's decode). genomes/s = all of that, end to end; the .npy write to disk is excluded.
@@ -631,6 +636,7 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
             "single_fraction": round(single_frac, 4), "split_fraction": round(split_frac, 4),
             "single_tiles": st["single_tiles"], "split_tiles": st["split_tiles"], "exact_tiles": st["exact_tiles"],
             "band_elements": st["band_elements"], "band_flips": st["band_flips"], "band_overflow": st["band_overflow"],
+            "overflow_tiles": st["overflow_tiles"],
             "dtype": ("bf16 (output layer, rounded operands; fp64 band recompute) + f32 (hidden layers)" if bf16 and prod == 1
                       else "bf16x3 (fp32 split hi/lo, output layer) + f32 (hidden layers)" if bf16 else "f32"),
             "mask_format": "packed bits (numpy packbits, little)", "includes": "z draw, decode, threshold, pack, "

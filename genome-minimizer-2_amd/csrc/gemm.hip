@@ -68,6 +68,11 @@ using SmallDeep = Cfg<128, 128, 2, 2, 4>;
 // The same tile with 8 waves (2x4, 64x32 each): two waves per SIMD, so one's LDS reads and waits
 // hide behind the other's MFMAs (GM2_OPT_SMALL_WAVES = 8)
 using SmallDeep8 = Cfg<128, 128, 2, 4, 4>;
+// The 4-wave tile with a 2-stage (64 KB) ring, <= 256 VGPRs (182-196, no spills; the 8-wave form
+// capped at 128 spilled 9-20): two workgroups share a CU (GM2_OPT_SMALL_PAIR, bf16), so the
+// latency-bound hidden-layer GEMMs that run beside the 256x256 weight-gradient GEMMs on the few CUs
+// those leave hide one workgroup's waits behind the other's MFMAs (verdict r5 item 5)
+using SmallPair = Cfg<128, 128, 2, 2, 2, 2>;
 
 struct TileXY {
   int m0, n0, split, t;
@@ -1707,8 +1712,11 @@ static bool pp_enabled() { return opts().gemm_pp != 0; }
 // and LDS ring depth (GM2_OPT_SMALL_STAGES: 4 or 5) of the 128x128 fp32-store GEMM tiles
 
 // call f(Cfg{}) with the 128x128 fp32-store tile configuration the options select
-template <class F>
+template <typename T, class F>
 static auto small_cfg(F&& f) {
+  if constexpr (sizeof(T) == 2) {
+    if (opts().small_pair) return f(SmallPair{});
+  }
   return opts().small_waves == 8 ? f(SmallDeep8{}) : f(SmallDeep{});
 }
 
@@ -1845,7 +1853,7 @@ int launch_gemm_store(const GemmArgs<T>& g, int splits, float* C0, float* C1, in
     }
   }
   check_gemm(g, 128);
-  return small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s); });
+  return small_cfg<T>([&](auto cfg) { return store_impl<decltype(cfg), T>(g, splits, C0, C1, msplit, ldc, slab, bias, none, s); });
 }
 
 template <typename T>
@@ -1871,7 +1879,7 @@ bool launch_gemm_sq(const GemmArgs<T>& g, float* C, int64_t ldc, double* sq, hip
     }
   }
   check_gemm(g, 128);
-  small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s); });
+  small_cfg<T>([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s); });
   return true;
 }
 
@@ -1891,7 +1899,7 @@ bool launch_gemm_trans(const GemmArgs<T>& g, float* C, int64_t ldc, hipStream_t 
     }
   }
   check_gemm(g, 128);
-  small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s); });
+  small_cfg<T>([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, nullptr, ep, s); });
   return true;
 }
 
@@ -1906,7 +1914,7 @@ bool launch_gemm_bn(const GemmArgs<T>& g, float* C, int64_t ldc, const float* bi
   const GemmPlan p = plan_gemm(g);
   if (p.tile != 128 || p.splits != 1 || (bn.mode && (g.N % 4 || bn.ldy % 4))) return false;
   check_gemm(g, 128);
-  small_cfg([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s); });
+  small_cfg<T>([&](auto cfg) { return store_impl<decltype(cfg), T>(g, 1, C, nullptr, 0, ldc, 0, bias, bn, s); });
   return true;
 }
 

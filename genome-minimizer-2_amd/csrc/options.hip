@@ -84,6 +84,7 @@ void option_set(Options& o, int key, int value) {
       if (value < 1 || value > 1000000) throw Gm2Error("single-tier bound %d (x 1e-3): 1..1000000", value);
       o.single_bound_milli = value;
       break;
+    case GM2_OPT_SMALL_PAIR: o.small_pair = value ? 1 : 0; break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -105,6 +106,7 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_SAMPLE_SINGLE: return o.sample_single;
     case GM2_OPT_SAMPLE_BAND_CAP: return o.band_cap;
     case GM2_OPT_SAMPLE_SINGLE_BOUND: return o.single_bound_milli;
+    case GM2_OPT_SMALL_PAIR: return o.small_pair;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

@@ -473,6 +473,34 @@ def test_capped_grid_bit_identical(G):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("B", [1024, 300])
+def test_small_pair_tiles_bit_identical(B):
+    """GM2_OPT_SMALL_PAIR: the bf16 128x128 fp32-store tiles (hidden layers, heads, decoder input
+    layer; their BatchNorm statistics epilogues) as 4-wave workgroups on a 2-stage ring, two per CU,
+    instead of 8 waves on a 4-stage ring: every output element sums the same MFMA products in the
+    same K order, so one training step's gradient, loss record, clip statistics and BatchNorm running
+    statistics are bit-identical (B = 300: ragged row tiles)."""
+    G, H, L = 3000, 512, 32
+    P, S = perturb_bn(*oracle_state(G, H, L, 41), seed=42)
+    X = synth_x(B, G, 43)
+    eps = torch.randn(B, L, generator=torch.Generator().manual_seed(44)).cuda()
+    sc = scalars(beta=0.37, wgamma=0.55, lam=0.01)
+    outs = []
+    for pair in (0, 1):
+        m = to_model(P, S, G, H, L, native.GM2_BF16)
+        mat = ResidentMatrix(X)
+        ws = m.workspace(native.GM2_BF16, B)
+        ws.set_option(native.OPT_SMALL_PAIR, pair)
+        grads = torch.zeros_like(m.params)
+        loss = torch.zeros(native.LOSS_SLOTS, dtype=torch.float64, device="cuda")
+        native.train_fwd_bwd(ws, native.make_batch(mat.data, mat.ld, None, B, eps), m.params, grads, m.bn, sc, loss)
+        native.grad_norm(ws, m.params, grads, sc, loss)
+        torch.cuda.synchronize()
+        outs.append((grads.cpu(), loss.cpu(), m.bn.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("G", [20480, 16500])
 def test_backward_schedule_options_bit_identical(G):
     """GM2_OPT_INPUT_CHUNKS (the input-layer weight gradient as four row-quarter launches) and

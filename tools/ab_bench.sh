@@ -11,7 +11,7 @@ for r in $(seq 1 $R); do
   i=0
   for v in "$@"; do
     if [[ "$v" == *"|"* ]]; then ev=${v%%|*}; args=${v#*|}; else ev=""; args=$v; fi
-    res=$(env $ev timeout -k 10 300 python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-f32-line --no-sample --no-c5 $args 2>/dev/null | tail -1)
+    res=$(env $ev timeout -k 10 300 python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-f32-line --no-sample --no-c5 --no-presets --no-c1 $args 2>/dev/null | tail -1)
     rc=$?
     [ $rc -ne 0 ] && { echo "variant $i rc=$rc" >> $out; exit $rc; }
     echo "variant $i [$v] $(echo "$res" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["roofline"]["launch_ms"])')" >> $out
