@@ -1715,7 +1715,7 @@ static bool pp_enabled() { return opts().gemm_pp != 0; }
 template <typename T, class F>
 static auto small_cfg(F&& f) {
   if constexpr (sizeof(T) == 2) {
-    if (opts().small_pair) return f(SmallPair{});
+    if (opts().small_pair == 1) return f(SmallPair{});  // (2, 3: api.hip backward() scopes it to 1)
   }
   return opts().small_waves == 8 ? f(SmallDeep8{}) : f(SmallDeep{});
 }

@@ -84,7 +84,10 @@ void option_set(Options& o, int key, int value) {
       if (value < 1 || value > 1000000) throw Gm2Error("single-tier bound %d (x 1e-3): 1..1000000", value);
       o.single_bound_milli = value;
       break;
-    case GM2_OPT_SMALL_PAIR: o.small_pair = value ? 1 : 0; break;
+    case GM2_OPT_SMALL_PAIR:
+      if (value < 0 || value > 3) throw Gm2Error("small pair %d: 0..3", value);
+      o.small_pair = value;
+      break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

@@ -346,9 +346,12 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *   GM2_OPT_SAMPLE_SINGLE_BOUND (ABI 6) the single tier's gate x 1000 (default 250 = 0.25, 1..1e6):
  *                       larger values send more tiles to the single tier (a wider band; a tile
  *                       whose band overflows its slots re-runs as bf16x3). Cost only, never the masks.
- *   GM2_OPT_SMALL_PAIR  (ABI 6) 1 = the bf16 128x128 fp32-store GEMM tiles (hidden layers) run with a
- *                       2-stage LDS ring and at most 128 VGPRs, so two workgroups share a CU; 0 = the
- *                       4-stage, one-per-CU form (default). Same results bit for bit. */
+ *   GM2_OPT_SMALL_PAIR  (ABI 6) the bf16 128x128 fp32-store GEMM tiles (hidden layers) as 4-wave
+ *                       workgroups on a 2-stage LDS ring, two per CU, instead of 8 waves on a 4-stage
+ *                       ring: 0 = never (default), 1 = every such launch, 2 = the backward's (the
+ *                       chain's input gradients and the hidden weight gradients), 3 = the chain's
+ *                       input gradients only. GEMM elements bit for bit; the BatchNorm statistics
+ *                       epilogue sums its partials in another order (rounding-level). */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
