@@ -15,7 +15,7 @@ bash tools/ab_bench.sh $T $R "$@" || exit $?
 i=0
 for v in "$@"; do
   if [[ "$v" == *"|"* ]]; then ev=${v%%|*}; args=${v#*|}; else ev=""; args=$v; fi
-  env $ev timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${T}_$i -o run --output-format csv -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-f32-line --no-sample --no-c5 $args > gpurun_out/prof_${T}_$i.log 2>&1
+  env $ev timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${T}_$i -o run --output-format csv -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-f32-line --no-sample --no-c5 --no-presets --no-c1 $args > gpurun_out/prof_${T}_$i.log 2>&1
   rc=$?; echo "prof rc=$rc" >> gpurun_out/prof_${T}_$i.log
   [ $rc -ne 0 ] && exit $rc
   i=$((i+1))

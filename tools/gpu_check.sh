@@ -17,6 +17,6 @@ rc=$?; echo "pytest rc=$rc" >> gpurun_out/gpu_tests_$T.log
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke_$T.log 2>&1 || exit $?
 [ "$3" = "skip-bench" ] && exit 0
 timeout -k 10 400 python3 bench.py > gpurun_out/bench_$T.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$T -o run --output-format csv -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-f32-line --no-sample --no-c5 > gpurun_out/prof_$T.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$T -o run --output-format csv -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-f32-line --no-sample --no-c5 --no-presets --no-c1 > gpurun_out/prof_$T.log 2>&1
 rc=$?; echo "prof rc=$rc" >> gpurun_out/prof_$T.log
 exit $rc
