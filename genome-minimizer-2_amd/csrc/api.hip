@@ -476,9 +476,10 @@ int gemm_to_slabs(const Ctx<T>& c, const T* P, int64_t ldp, int Mp, const T* Q, 
   GemmArgs<T> g{P, ldp, Q, ldq, M, N, K, Mp, Np, 0, pk, qk};
   g.prow = prow;
   if (prow) g.idx_lim = c.res_rows;
-  const int S = plan_gemm<T>(g).splits;
   const int64_t slab = (int64_t)Mp * ldc;
-  if ((int64_t)S * slab > c.slab_cap) throw Gm2Error("slab capacity exceeded");
+  // (the plan's split count, at most what the stream's slab scratch holds)
+  const int S = (int)std::min<int64_t>(plan_gemm<T>(g).splits, c.slab_cap / std::max<int64_t>(slab, 1));
+  if (S < 1) throw Gm2Error("slab capacity exceeded");
   return launch_gemm_store<T>(g, S, c.f(c.slab_off), nullptr, 0, ldc, slab, nullptr, c.s);
 }
 

@@ -1688,7 +1688,11 @@ GemmPlan plan_gemm(const GemmArgs<T>& g) {
   // registers, which the 256x256 tile's 8 waves cannot hold)
   const int tiles_big = (sizeof(T) == 2 && g.Mp % 256 == 0 && g.Np % 256 == 0) ? (g.Mp / 256) * (g.Np / 256) : 0;
   const int tiles_small = (g.Mp / 128) * (g.Np / 128);
-  auto cap = [&](int s) { return std::max(1, std::min({s, 8, std::max(1, nk / 8)})); };
+  // (up to 32 K-slices: a launch with a few tiles -- the small-batch plans, e.g. the input layer and
+  // the output layer's input gradient at batch 32 / 64: 8 tiles of 128 x 128 over K = 55,040 --
+  // fills the chip; at most 8 had left 192 CUs idle, 117 -> ~30 us each at batch 64; the split
+  // slabs are summed in slice order by their consumers, deterministic)
+  auto cap = [&](int s) { return std::max(1, std::min({s, 32, std::max(1, nk / 8)})); };
   if (tiles_big >= 256) return {256, 1};
   if (tiles_big > 0 && g.K >= 8192) return {256, cap((256 + tiles_big - 1) / tiles_big)};
   if (tiles_small >= 192) {

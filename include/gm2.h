@@ -262,7 +262,7 @@ int gm2_reparameterize(int64_t n, const float* mu, const float* logvar, const fl
  * 0: stored [K][ld] with M (N) contiguous (P(m,k) = P[k*ld+m]). Elements of `precision` type;
  * the M (N) extent is padded to a multiple of 128 in the allocation, K % 64 == 0, pads zero.
  * (P MN-major with Q K-major is not instantiated.) splits 0/1: one pass straight into C; > 1: that
- * many split-K slices; < 0: the hot path's own tile / split plan (at most 8 slices). Split runs
+ * many split-K slices; < 0: the hot path's own tile / split plan (at most 32 slices). Split runs
  * need slab_ws (fp32, splits * M * ldc elements) and sum the slices into C. */
 int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t ldp, const void* Q,
              int64_t ldq, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, int splits,
