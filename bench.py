@@ -59,14 +59,16 @@ def decode_flops_per_genome(G, H, L):
 DEFAULTS = dict(batch=4096, genes=55039, hidden=1024, latent=64, precision="bf16")
 
 
-def pmc_traffic(a, kernel_prefix, grid=None):
-    """HBM bytes per launch of `kernel_prefix` from the newest committed PMC summary
-    (profiles/rNN_pmc_traffic.json, written by tools/pmc.py from separate FETCH_SIZE / WRITE_SIZE
-    rocprofv3 passes of this same command). Only valid for the default workload; else None."""
+def pmc_traffic(a, kernel_prefix, grid=None, pattern="r*_pmc_traffic.json"):
+    """HBM bytes per launch of `kernel_prefix` from the newest committed PMC summary matching
+    `pattern` (profiles/rNN_pmc_traffic.json, written by tools/pmc.py from separate FETCH_SIZE /
+    WRITE_SIZE rocprofv3 passes of this same command; the sample leg's kernels from
+    rNN_pmc_sample_trained.json, the passes over the trained checkpoint it decodes from,
+    tools/pmc_sample.sh). Only valid for the default workload; else None."""
     import glob
     if any(getattr(a, k) != v for k, v in DEFAULTS.items()):
         return None, None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
     if not files:
         return None, None
     rows = [r for r in json.load(open(files[-1]))["kernels"] if r["kernel"].startswith(kernel_prefix)
@@ -629,7 +631,9 @@ def sample_bench(a, dev, dist=None, rank=0, world=1):
     # the PMC passes decode from an untrained model, tools/prof.sh)
     tiered = ws.get_option(native.OPT_SAMPLE_SINGLE) != 0
     traffic, traffic_src = pmc_traffic(a, ("k_gemm_mask_tiered<Cfg<256" if tiered else "k_gemm_mask<Cfg<256") if bf16
-                                       else "k_gemm_mask<Cfg<128")
+                                       else "k_gemm_mask<Cfg<128",
+                                       pattern="r*_pmc_sample_trained.json" if trained is not None else
+                                       "r*_pmc_traffic.json")
     return {"genomes_per_s": round(gps, 1), "preset": "v1", "genomes": n_all, "n_gpus": world, "chunk": chunk,
             "checkpoint": (f"v1 trained {a.sample_train_epochs} epochs (lr 1e-3, batch 4096, L1 0.01) on the synthetic "
                            f"{a.strains}x{G} matrix" if trained is not None else "untrained (xavier init)"),

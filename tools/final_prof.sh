@@ -6,5 +6,5 @@ cd "$GRAFT_REPO_ROOT" || exit 2
 mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
 T=${1:-f}
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof35_$T -o run --output-format csv -- python3 bench.py --steps 35 --warmup 5 --no-cpu-baseline --no-f32-line --no-c5 --sample-genomes 262144 > gpurun_out/prof35_$T.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof35_$T -o run --output-format csv -- python3 bench.py --steps 35 --warmup 5 --no-cpu-baseline --no-f32-line --no-c5 --no-presets --no-c1 --sample-genomes 262144 > gpurun_out/prof35_$T.log 2>&1 || exit $?
 bash tools/prof.sh $T
