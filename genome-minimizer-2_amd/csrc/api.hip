@@ -1047,11 +1047,13 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
   bs.olist = bs.oflag + tiles;
   bs.ocount = ovf + Layout::kOvfCount;
   bs.obn = Gq / 256;
+  bs.oblocks = (unsigned)tiles;
   be.cap = bs.cap;
   be.oflag = bs.oflag;
   be.olist = bs.olist;
   be.ocount = bs.ocount;
   be.obn = bs.obn;
+  be.oblocks = bs.oblocks;
   const int on = single ? 1 : 0;
   const double single_bound = opts().single_bound_milli * 1e-3;  // (GM2_OPT_SAMPLE_SINGLE_BOUND, for A/Bs and tests)
   GemmArgs<bf16_t> g{a3, 2 * H, w3, 2 * H, n, G, 2 * H, Bq, Gq, 0};

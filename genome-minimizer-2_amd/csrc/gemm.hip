@@ -1282,6 +1282,8 @@ struct BandCols {
 // lists it) for k_band_tile_fix's whole-block fp64 recompute
 __device__ __forceinline__ void band_spill(const MaskBand& b, unsigned r, unsigned gcol) {
   const unsigned blk = (r >> 8) * (unsigned)b.obn + (gcol >> 8);
+  GM2_DBG(blk < b.oblocks && (int)(gcol >> 8) < b.obn, kDbgBandBlock);
+  if (blk >= b.oblocks) return;  // (cannot happen: the epilogues flag rows < M, genes < N only)
   if (atomicExch(b.oflag + blk, 1u) == 0u) b.olist[atomicAdd(b.ocount, 1u)] = blk;
 }
 
@@ -2022,7 +2024,8 @@ void launch_gemm_mask_tiered(const GemmArgs<bf16_t>& g1, const GemmArgs<bf16_t>&
     throw Gm2Error("mask bits: row pitch %lld must be a multiple of 16 bytes covering the padded genes", (long long)ldb);
   if (!band1.rn || !band3.rn || !band1.tslots || !band3.tslots || !band1.drop_overflow || !gate3.run)
     throw Gm2Error("tiered mask: both bands with tile slots (the single tier's dropping its overflow) and the gate");
-  if (!band3.oflag || !band3.olist || !band3.ocount || band3.obn < g3.Np / 256)
+  if (!band3.oflag || !band3.olist || !band3.ocount || band3.obn < g3.Np / 256 ||
+      band3.oblocks < (unsigned)((g3.Mp / 256) * band3.obn))
     throw Gm2Error("tiered mask: the overflow block flags, list and counter required");
   const MaskOut o1{mask, ldm, bits, ldb, nullptr, 0, nullptr, nullptr, 0, 0.5f, gate1, band1};
   const MaskOut o3{mask, ldm, bits, ldb, nullptr, 0, nullptr, nullptr, 0, 0.5f, gate3, band3};
@@ -2050,7 +2053,8 @@ void launch_gemm_mask(const GemmArgs<T>& g, const float* bias, uint8_t* mask, in
   MaskOut o{mask, ldm, bits, ldb, probs, ldpr, counts, xbits, ldxb, thr, gate, band};
   if (band.rn && (!band.cn || !band.counts || !band.list || !band.cap || thr != 0.5f))
     throw Gm2Error("mask band: norms, counter and list required (threshold 0.5 only)");
-  if (band.rn && (!band.oflag || !band.olist || !band.ocount || band.obn < (g.Np + 255) / 256))
+  if (band.rn && (!band.oflag || !band.olist || !band.ocount || band.obn < (g.Np + 255) / 256 ||
+                  band.oblocks < (unsigned)(((g.Mp + 255) / 256) * band.obn)))
     throw Gm2Error("mask band: the overflow block flags, list and counter required");
   if (band.tslots && (!band.tlist || !band.tcount || !band.tfound || !big))
     throw Gm2Error("mask band: tile slots need their list, counters and the 256 x 256 kernel");

@@ -68,6 +68,7 @@ enum DebugBit : unsigned {
   kDbgCompact = 16u,       // k_compact: an index written outside [off[row], off[row + 1])
   kDbgReconRows = 32u,     // loss epilogue: target-bit row outside [0, idx_lim)
   kDbgTile = 64u,          // a GEMM tile origin outside the padded operand extents
+  kDbgBandBlock = 128u,    // band-list overflow: a flagged 256 x 256 block outside the block grid
 };
 #ifdef GM2_DEBUG
 namespace {

@@ -260,6 +260,7 @@ struct MaskBand {
   unsigned* olist = nullptr;
   unsigned* ocount = nullptr;
   int obn = 0;                // gene blocks per row block
+  unsigned oblocks = 0;       // blocks in the grid (the flag / list capacity)
   uint2* tlist = nullptr;     // [tiles][tslots] (row, gene), tile = TileXY::t of the launch's grid
   unsigned* tcount = nullptr; // [tiles] the tile's band count, of which min(count, tslots) in its slots
                               // (zeroed by the caller; a tile's kernel writes its own)

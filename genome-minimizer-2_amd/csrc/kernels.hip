@@ -1280,7 +1280,7 @@ __global__ __launch_bounds__(256) void k_band_fix(MaskBand band, int ntiles, con
 // genes >= G are 0 (the packed rows' pad bits), words past the row pitch are not written.
 constexpr int kTileFixRows = 16;
 __global__ __launch_bounds__(256) void k_band_tile_fix(const unsigned* __restrict__ olist,
-                                                     const unsigned* __restrict__ ocount, int obn,
+                                                     const unsigned* __restrict__ ocount, int obn, unsigned oblocks,
                                                      const float* __restrict__ A, int64_t lda,
                                                      const float* __restrict__ W, int64_t ldw,
                                                      const float* __restrict__ bias, int H, int rows_per, int n, int G,
@@ -1288,10 +1288,12 @@ __global__ __launch_bounds__(256) void k_band_tile_fix(const unsigned* __restric
                                                      unsigned* flips) {
   extern __shared__ __attribute__((aligned(16))) float sa[];  // [rows_per][H]
   const int subs = 256 / rows_per, lane = threadIdx.x & 63;
-  const unsigned items = *ocount * (unsigned)subs;
+  const unsigned nblk = min(*ocount, oblocks), items = nblk * (unsigned)subs;
+  GM2_DBG(*ocount <= oblocks, kDbgBandBlock);
   unsigned nflip = 0;
   for (unsigned it = blockIdx.x; it < items; it += gridDim.x) {
     const unsigned blk = olist[it / subs];
+    GM2_DBG(blk < oblocks, kDbgBandBlock);
     const int m0 = (int)(blk / (unsigned)obn) * 256 + (int)(it % subs) * rows_per;
     const int g = (int)(blk % (unsigned)obn) * 256 + (int)threadIdx.x;
     __syncthreads();  // (the previous item's rows are read)
@@ -1618,7 +1620,7 @@ void launch_band_tile_fix(const MaskBand& band, const float* A, int64_t lda, con
                           int64_t ldm, unsigned* flips, hipStream_t s) {
   if ((!bits && !mask) || (bits && (ldb & 3)) || H < 4 || H % 4 || (((uintptr_t)W | (uintptr_t)(ldw * 4)) & 15))
     throw Gm2Error("band tile fix: packed bits with 4-B aligned rows or a u8 mask, H %% 4 == 0, 16-B aligned weight rows");
-  if (!band.olist || !band.ocount || band.obn <= 0 || n < 0 || G < 0)
+  if (!band.olist || !band.ocount || band.obn <= 0 || !band.oblocks || n < 0 || G < 0)
     throw Gm2Error("band tile fix: the overflow block list and counter required");
   // rows per work item: a power of two <= 16 whose fp32 rows fit 64 KB of LDS
   int rows_per = kTileFixRows;
@@ -1626,7 +1628,8 @@ void launch_band_tile_fix(const MaskBand& band, const float* A, int64_t lda, con
   const size_t lds = (size_t)rows_per * H * 4;
   if (lds > 65536) throw Gm2Error("band tile fix: hidden width %d too large", H);
   // (<= 64 KB: within the default dynamic-LDS limit, no attribute needed)
-  hipLaunchKernelGGL(k_band_tile_fix, dim3(512), dim3(256), lds, s, band.olist, band.ocount, band.obn, A, lda, W, ldw,
+  hipLaunchKernelGGL(k_band_tile_fix, dim3(512), dim3(256), lds, s, band.olist, band.ocount, band.obn, band.oblocks, A,
+                     lda, W, ldw,
                      bias, H, rows_per, n, G, bits, ldb, mask, ldm, flips);
   GM2_CHECK_LAUNCH();
 }

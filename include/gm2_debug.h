@@ -23,6 +23,7 @@ extern "C" {
 #define GM2_DBG_COMPACT 16       /* gm2_mask_compact: an index written outside its row's CSR span */
 #define GM2_DBG_RECON_ROWS 32    /* loss epilogue: a target-bit row outside the resident bits */
 #define GM2_DBG_TILE 64          /* a GEMM tile or K range outside the padded operand extents */
+#define GM2_DBG_BAND_BLOCK 128   /* sampling decode: a band-overflow block (or their count) outside the block grid */
 
 /* OR of the failed checks of every kernel since the last call, then cleared (waits for the device) */
 int gm2_debug_flags(unsigned* flags);
