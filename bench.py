@@ -109,6 +109,8 @@ def parse():
                     help="input-layer weight-gradient launches (default: 4 under DDP, else 1)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5-shaped (G=20,000) step line")
     ap.add_argument("--no-presets", action="store_true", help="skip the v1 / v2 / v3 step lines (C3 / C4 per GPU)")
+    ap.add_argument("--no-adam-timing", action="store_true",
+                    help="no live event pairs around the Adam launches (roofline_hbm then null)")
     ap.add_argument("--no-c1", action="store_true", help="skip the batch-64 / batch-32 GPU lines (C1 workload)")
     ap.add_argument("--defer-adam", type=int, default=None,
                     help="output layer's Adam update launched beside the next step's hidden layers on this many "
@@ -330,7 +332,7 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    native.timing_begin(native.KC_RECON_LOSS)
+    native.timing_begin(native.KC_RECON_LOSS | (0 if a.no_adam_timing else native.KC_ADAM))
     t0 = time.perf_counter()
     host_s = 0.0
     for i in range(W, nsteps):
@@ -345,7 +347,9 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    k_ms, k_n = native.timing_end()
+    native.timing_end()
+    k_ms, k_n = native.timing_class(native.KC_RECON_LOSS)
+    a_ms, a_n = native.timing_class(native.KC_ADAM)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -362,6 +366,10 @@ def train_leg(a, dev, dist, rank, world, G, H, L, B, strains, prec, seed_base=12
             "defer_adam": ws.get_option(native.OPT_DEFER_OUTPUT_ADAM),
             "grad_buckets": ws.get_option(native.OPT_GRAD_BUCKETS),
             "zero_copy": res is not None,
+            # the fused L1 + clip + Adam passes: 30 B per parameter per step (read p, g, m, v; write
+            # p, m, v and the bf16 / fp32 GEMM shadow), two launches per step (the output layer's deferred)
+            "adam": {"ms": a_ms, "launches": a_n, "bytes": 30.0 * model.n_params * (nsteps - W)
+                     if prec == native.GM2_BF16 else 32.0 * model.n_params * (nsteps - W)},
             "x": x if (rank == 0 and world == 1) else None, "mat": mat}
     del model, opt, ws, grads, sync
     return elapsed, k_ms, k_n, info
@@ -383,6 +391,23 @@ def roofline_entry(a, prec, G, H, B, k_ms, k_n, pmc=True):
             else "k_gemm_recon_loss<f32>", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
             "launch_ms": round(k_avg_ms, 4), "launches": k_n, "flops_per_launch": k_flops}
+
+
+def adam_roofline(a, ad):
+    """k_adam_fused against the HBM roofline: algorithmic bytes (30 B per parameter per step in the
+    bf16 workspace: read p, g, m, v; write p, m, v and the bf16 GEMM shadow) over the summed live
+    duration of its launches (HIP events on each launch's stream; the output layer's update is the
+    deferred launch beside the next step's hidden layers). traffic: the committed PMC pass's
+    FETCH_SIZE + WRITE_SIZE of the same two launches."""
+    if not ad["ms"]:
+        return None
+    achieved = ad["bytes"] / (ad["ms"] * 1e-3) / 1e9
+    tr = [pmc_traffic(a, "k_adam_fused<unsigned short>", g)[0] for g in (3802112, 65536)]
+    return {"bound": "hbm", "kernel": "k_adam_fused<bf16>", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+            "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+            "traffic": (sum(tr) if all(t is not None for t in tr) else None),
+            "bytes_per_step": ad["bytes"] / max(1, ad["launches"] // 2), "launch_ms": round(ad["ms"] / max(ad["launches"], 1), 4),
+            "launches": ad["launches"]}
 
 
 def main():
@@ -434,6 +459,8 @@ def main():
         "nonfinite_steps": 0,
         # dominant kernel: decoder output layer GEMM [B,H]x[H,G] + fused BCE/abundance/dlogits epilogue
         "roofline": roofline_entry(a, prec, G, H, B, k_ms, k_n),
+        # the step's HBM-bound pass: the fused L1 + clip + Adam kernel, bytes over its live launch time
+        "roofline_hbm": adam_roofline(a, info["adam"]),
     }
     x = info.pop("x")
     del info

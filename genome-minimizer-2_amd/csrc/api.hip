@@ -1704,6 +1704,13 @@ int gm2_timing_end(double* total_ms, int64_t* launches) {
   return guarded([&] { timing_end(total_ms, launches); });
 }
 
+int gm2_timing_class(int kernel_class, double* total_ms, int64_t* launches) {
+  return guarded([&] {
+    if (!total_ms || !launches) throw Gm2Error("null output");
+    timing_class(kernel_class, total_ms, launches);
+  });
+}
+
 #ifdef GM2_DEBUG
 // ---- debug build only (include/gm2_debug.h) ----
 int gm2_debug_flags(unsigned* flags) {

@@ -1614,7 +1614,9 @@ namespace {
 struct TimingState {
   int classes = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  std::vector<int> cls;  // the class of each used event pair
   size_t used = 0;
+  std::map<int, std::pair<double, int64_t>> last;  // per-class totals of the last timed region
 };
 TimingState& tstate() {
   static TimingState t;
@@ -1631,6 +1633,7 @@ void timing_begin(int classes) {
 void timing_end(double* total_ms, int64_t* launches) {
   TimingState& t = tstate();
   double tot = 0.0;
+  t.last.clear();
   for (size_t i = 0; i < t.used; ++i) {
     hipError_t e = hipEventSynchronize(t.ev[i].second);
     if (e != hipSuccess) throw Gm2Error("timing: %s", hipGetErrorString(e));
@@ -1638,6 +1641,9 @@ void timing_end(double* total_ms, int64_t* launches) {
     e = hipEventElapsedTime(&ms, t.ev[i].first, t.ev[i].second);
     if (e != hipSuccess) throw Gm2Error("timing: %s", hipGetErrorString(e));
     tot += ms;
+    auto& l = t.last[t.cls[i]];
+    l.first += ms;
+    l.second += 1;
   }
   *total_ms = tot;
   *launches = (int64_t)t.used;
@@ -1645,7 +1651,14 @@ void timing_end(double* total_ms, int64_t* launches) {
   t.used = 0;
 }
 
-TimedLaunch::TimedLaunch(int cls, hipStream_t st) : idx(-1), s(st) {
+void timing_class(int cls, double* total_ms, int64_t* launches) {
+  const TimingState& t = tstate();
+  auto it = t.last.find(cls);
+  *total_ms = it == t.last.end() ? 0.0 : it->second.first;
+  *launches = it == t.last.end() ? 0 : it->second.second;
+}
+
+TimedLaunch::TimedLaunch(int c, hipStream_t st) : idx(-1), s(st), cls(c) {
   TimingState& t = tstate();
   if (!(t.classes & cls)) return;
   if (t.used == t.ev.size()) {
@@ -1657,6 +1670,8 @@ TimedLaunch::TimedLaunch(int cls, hipStream_t st) : idx(-1), s(st) {
     t.ev.push_back({a, b});
   }
   idx = (int)t.used++;
+  if (t.cls.size() < t.used) t.cls.resize(t.used);
+  t.cls[idx] = cls;
   if (hipEventRecord(t.ev[idx].first, s) != hipSuccess) throw Gm2Error("hipEventRecord");
 }
 

@@ -116,14 +116,17 @@ struct OptionScope {
 };
 
 // ---- live per-kernel timing (bench.py): hipEvent pairs around every launch of one class ----
-enum KernelClass { kKcReconLoss = 1, kKcGemmStore = 2, kKcMask = 4 };
+enum KernelClass { kKcReconLoss = 1, kKcGemmStore = 2, kKcMask = 4, kKcAdam = 8 };
 void timing_begin(int classes);
 void timing_end(double* total_ms, int64_t* launches);
+// the last timed region's total for one class (after timing_end)
+void timing_class(int cls, double* total_ms, int64_t* launches);
 struct TimedLaunch {  // records an event pair around a launch when its class is being timed
   TimedLaunch(int cls, hipStream_t s);
   ~TimedLaunch();
   int idx;
   hipStream_t s;
+  int cls;
 };
 
 // ---- gemm.hip ----

@@ -1668,6 +1668,7 @@ void launch_adam_fused(const TensorTable& tt, const float* grads, float* params,
   for (int i = 0; i < tt.n; ++i)
     if (tt.t[i].off % 4) throw Gm2Error("adam: tensor offset not 16-B aligned");
   const int64_t grid = max_grid > 0 ? std::min<int64_t>(blocks, max_grid) : blocks;
+  TimedLaunch tl(kKcAdam, s);
   hipLaunchKernelGGL(k_adam_fused<T>, dim3((unsigned)grid), dim3(256), 0, s, tt, grads, params, m, v, scal, clip,
                      blocks, scal_copy);
   GM2_CHECK_LAUNCH();

@@ -34,10 +34,10 @@ EXPORTS = ["gm2_last_error", "gm2_abi_version", "gm2_param_count", "gm2_param_of
            "gm2_workspace_set_option", "gm2_workspace_get_option", "gm2_workspace_release",
            "gm2_workspace_set_collective", "gm2_workspace_join",
            "gm2_resident_layout", "gm2_resident_build",
-           "gm2_timing_begin", "gm2_timing_end", "gm2_workspace_stat",
+           "gm2_timing_begin", "gm2_timing_end", "gm2_timing_class", "gm2_workspace_stat",
            "gm2_exchange_pack", "gm2_exchange_ranksum", "gm2_exchange_unpack"]
 ABI_VERSION = 6
-KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK = 1, 2, 4
+KC_RECON_LOSS, KC_GEMM_STORE, KC_MASK, KC_ADAM = 1, 2, 4, 8
 OPT_GEMM_PP, OPT_SIDE_STREAM, OPT_RECON_TILE, OPT_SMALL_SPLIT, OPT_BN_EPILOGUE, OPT_SMALL_WAVES = 1, 2, 3, 4, 5, 6
 OPT_INPUT_CHUNKS, OPT_GRID_CAP, OPT_SYNC_BN, OPT_DEFER_OUTPUT_ADAM = 7, 9, 10, 11
 OPT_GRAD_BUCKETS = 15
@@ -126,6 +126,7 @@ def lib():
         "gm2_exchange_unpack": (C.c_int, [vp, i64, vp, vp]),
         "gm2_timing_begin": (C.c_int, [i32]),
         "gm2_timing_end": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+        "gm2_timing_class": (C.c_int, [i32, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -432,4 +433,11 @@ def timing_end():
     """(total_ms, launches) of the timed kernel class since timing_begin."""
     ms, n = C.c_double(), C.c_int64()
     check(lib().gm2_timing_end(C.byref(ms), C.byref(n)), "gm2_timing_end")
+    return ms.value, n.value
+
+
+def timing_class(cls: int):
+    """(total_ms, launches) of one class of the last timed region (after timing_end)."""
+    ms, n = C.c_double(), C.c_int64()
+    check(lib().gm2_timing_class(int(cls), C.byref(ms), C.byref(n)), "gm2_timing_class")
     return ms.value, n.value

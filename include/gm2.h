@@ -416,9 +416,12 @@ int gm2_workspace_stat(void* ws, int key, int64_t* value);
 typedef int (*gm2_allreduce_fn)(double* buf, int64_t count, void* stream, void* user);
 int gm2_workspace_set_collective(void* ws, gm2_allreduce_fn fn, void* user);
 
-enum { GM2_KC_RECON_LOSS = 1, GM2_KC_GEMM_STORE = 2, GM2_KC_MASK = 4 };
+enum { GM2_KC_RECON_LOSS = 1, GM2_KC_GEMM_STORE = 2, GM2_KC_MASK = 4, GM2_KC_ADAM = 8 };
 int gm2_timing_begin(int kernel_classes);
 int gm2_timing_end(double* total_ms, int64_t* launches);
+/* (ABI 6) after gm2_timing_end: the summed duration and launch count of ONE of the classes that were
+ * timed together (GM2_KC_ADAM: the fused L1 + clip + Adam passes, the deferred one included) */
+int gm2_timing_class(int kernel_class, double* total_ms, int64_t* launches);
 
 #ifdef __cplusplus
 }
