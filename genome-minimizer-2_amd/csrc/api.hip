@@ -793,12 +793,6 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
   // GPU; first keeps gradient bucket 0 early for the data-parallel exchange.)
   const BigGrads<T> bg = big_grads<T>(c, Bp);
   double* nasq = (double*)(c.ws + l.nasq);
-  // GM2_OPT_SMALL_PAIR 2: the paired 128x128 tiles for every small GEMM of the backward (the chain's
-  // dX GEMMs beside dW9, the weight gradients beside dWe0); 3: for the chain's dX GEMMs only
-  Options pair_all = opts(), pair_dx = opts();
-  pair_all.small_pair = opts().small_pair == 1 || opts().small_pair == 2 ? 1 : 0;
-  pair_dx.small_pair = opts().small_pair >= 1 ? 1 : 0;
-  OptionScope pair_scope(pair_all);
   // the forward's deferred tail launch (loss sums, output bias gradient): behind the first fork
   auto tail_on = [&](hipStream_t s) {
     if (fwd_tail && *fwd_tail) {
@@ -859,7 +853,6 @@ void backward(const Ctx<T>& c, const gm2_batch* b, const float* prm, float* gr, 
     bn.gamma = prm + d.off[kBlk[j][2]];
     bn.beta = prm + d.off[kBlk[j][3]];
     bn.H = H;
-    OptionScope dx_scope(pair_dx);
     have_part = launch_gemm_bn<T>(g, c.f(c.slab_off), H, nullptr, bn, c.s);
     return have_part ? 1 : gemm_to_slabs<T>(c, dY, lddy, Bp, W, ldw, H, B, H, K, H, 1, 0);
   };

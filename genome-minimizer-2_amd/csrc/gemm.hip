@@ -68,11 +68,6 @@ using SmallDeep = Cfg<128, 128, 2, 2, 4>;
 // The same tile with 8 waves (2x4, 64x32 each): two waves per SIMD, so one's LDS reads and waits
 // hide behind the other's MFMAs (GM2_OPT_SMALL_WAVES = 8)
 using SmallDeep8 = Cfg<128, 128, 2, 4, 4>;
-// The 4-wave tile with a 2-stage (64 KB) ring, <= 256 VGPRs (182-196, no spills; the 8-wave form
-// capped at 128 spilled 9-20): two workgroups share a CU (GM2_OPT_SMALL_PAIR, bf16), so the
-// latency-bound hidden-layer GEMMs that run beside the 256x256 weight-gradient GEMMs on the few CUs
-// those leave hide one workgroup's waits behind the other's MFMAs (verdict r5 item 5)
-using SmallPair = Cfg<128, 128, 2, 2, 2, 2>;
 
 struct TileXY {
   int m0, n0, split, t;
@@ -1733,11 +1728,10 @@ static bool pp_enabled() { return opts().gemm_pp != 0; }
 // and LDS ring depth (GM2_OPT_SMALL_STAGES: 4 or 5) of the 128x128 fp32-store GEMM tiles
 
 // call f(Cfg{}) with the 128x128 fp32-store tile configuration the options select
+// (round 6 measured a 4-wave, 2-stage form with two workgroups per CU -- GM2_OPT_SMALL_PAIR, commits
+// a952803 / 09afbbc -- neutral to slower at step level and removed it: profiles/r06_small_pair_ab.txt)
 template <typename T, class F>
 static auto small_cfg(F&& f) {
-  if constexpr (sizeof(T) == 2) {
-    if (opts().small_pair == 1) return f(SmallPair{});  // (2, 3: api.hip backward() scopes it to 1)
-  }
   return opts().small_waves == 8 ? f(SmallDeep8{}) : f(SmallDeep{});
 }
 

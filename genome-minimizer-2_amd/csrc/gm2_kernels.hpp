@@ -96,7 +96,6 @@ struct Options {
   int band_cap = 65536;  // GM2_OPT_SAMPLE_BAND_CAP entries per band-list shard per decode (<= kBandShardCap;
                          //   smaller values exercise the overflow recompute)
   int single_bound_milli = 250;  // GM2_OPT_SAMPLE_SINGLE_BOUND the single tier's gate x 1000 (kSingleBound)
-  int small_pair = 0;    // GM2_OPT_SMALL_PAIR   bf16 128x128 store tiles: 2-stage ring, two workgroups per CU
 };
 // validated edit of one option (throws on an unknown key or a bad value)
 void option_set(Options& o, int key, int value);

@@ -84,10 +84,6 @@ void option_set(Options& o, int key, int value) {
       if (value < 1 || value > 1000000) throw Gm2Error("single-tier bound %d (x 1e-3): 1..1000000", value);
       o.single_bound_milli = value;
       break;
-    case GM2_OPT_SMALL_PAIR:
-      if (value < 0 || value > 3) throw Gm2Error("small pair %d: 0..3", value);
-      o.small_pair = value;
-      break;
     default: throw Gm2Error("unknown option %d", key);
   }
 }
@@ -109,7 +105,6 @@ int option_get(const Options& o, int key) {
     case GM2_OPT_SAMPLE_SINGLE: return o.sample_single;
     case GM2_OPT_SAMPLE_BAND_CAP: return o.band_cap;
     case GM2_OPT_SAMPLE_SINGLE_BOUND: return o.single_bound_milli;
-    case GM2_OPT_SMALL_PAIR: return o.small_pair;
     default: throw Gm2Error("unknown option %d", key);
   }
 }

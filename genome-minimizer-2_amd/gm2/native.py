@@ -43,7 +43,7 @@ OPT_INPUT_CHUNKS, OPT_GRID_CAP, OPT_SYNC_BN, OPT_DEFER_OUTPUT_ADAM = 7, 9, 10, 1
 OPT_GRAD_BUCKETS = 15
 OPT_SAMPLE_SPLIT = 18
 OPT_SAMPLE_SINGLE = 20
-OPT_SAMPLE_BAND_CAP, OPT_SAMPLE_SINGLE_BOUND, OPT_SMALL_PAIR = 21, 22, 23
+OPT_SAMPLE_BAND_CAP, OPT_SAMPLE_SINGLE_BOUND = 21, 22
 STAT_SPLIT_DECODES, STAT_EXACT_DECODES, STAT_SPLIT_TILES, STAT_EXACT_TILES = 1, 2, 3, 4
 STAT_BAND_ELEMENTS, STAT_BAND_FLIPS, STAT_BAND_OVERFLOW, STAT_SINGLE_TILES = 5, 6, 7, 8
 STAT_OVERFLOW_TILES = 9

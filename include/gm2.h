@@ -345,13 +345,7 @@ int gm2_gemm(int precision, int p_kmajor, int q_kmajor, const void* P, int64_t l
  *                       masks do not depend on this value; smaller values exercise that path.
  *   GM2_OPT_SAMPLE_SINGLE_BOUND (ABI 6) the single tier's gate x 1000 (default 250 = 0.25, 1..1e6):
  *                       larger values send more tiles to the single tier (a wider band; a tile
- *                       whose band overflows its slots re-runs as bf16x3). Cost only, never the masks.
- *   GM2_OPT_SMALL_PAIR  (ABI 6) the bf16 128x128 fp32-store GEMM tiles (hidden layers) as 4-wave
- *                       workgroups on a 2-stage LDS ring, two per CU, instead of 8 waves on a 4-stage
- *                       ring: 0 = never (default), 1 = every such launch, 2 = the backward's (the
- *                       chain's input gradients and the hidden weight gradients), 3 = the chain's
- *                       input gradients only. GEMM elements bit for bit; the BatchNorm statistics
- *                       epilogue sums its partials in another order (rounding-level). */
+ *                       whose band overflows its slots re-runs as bf16x3). Cost only, never the masks. */
 enum {
   GM2_OPT_GEMM_PP = 1,
   GM2_OPT_SIDE_STREAM = 2,
@@ -367,8 +361,7 @@ enum {
   GM2_OPT_SAMPLE_SPLIT = 18,
   GM2_OPT_SAMPLE_SINGLE = 20,
   GM2_OPT_SAMPLE_BAND_CAP = 21,
-  GM2_OPT_SAMPLE_SINGLE_BOUND = 22,
-  GM2_OPT_SMALL_PAIR = 23
+  GM2_OPT_SAMPLE_SINGLE_BOUND = 22
 };
 int gm2_set_option(int key, int value);
 int gm2_get_option(int key, int* value);

@@ -473,54 +473,6 @@ def test_capped_grid_bit_identical(G):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("mode,bn", [(1, 1), (1, 0), (3, 1)], ids=["all-bnepi", "all-bnpass", "chain-bnepi"])
-@pytest.mark.parametrize("G,H,L,B,wg,lam", [(517, 256, 32, 130, 0.55, 0.01), (8192, 256, 32, 1024, 0.55, 0.01),
-                                            (3000, 512, 32, 1024, 0.55, 0.01)])
-def test_small_pair_train_step_vs_oracle(G, H, L, B, wg, lam, mode, bn):
-    """GM2_OPT_SMALL_PAIR: the bf16 128x128 fp32-store tiles (hidden layers, heads, decoder input
-    layer, their BatchNorm statistics epilogues) as 4-wave workgroups on a 2-stage ring, two per CU.
-    Every GEMM element sums the same MFMA products in the same K order as the 8-wave kernel
-    (test_gemm_small_pair_bit_identical); the BatchNorm statistics epilogue combines its per-thread
-    column partials over 256 instead of 512 threads -- another valid fp32 summation order, which the
-    ill-conditioned train-mode BatchNorm backward turns into percent-level differences of the
-    input-layer gradient (measured 3.6 % fro between the two forms at G 3,000 / H 512 / B 1,024, the
-    size of any two fp32 evaluations' disagreement, test_gpu_c2.py). So the step is held to the same
-    bar as the default tiles: test_train_step_vs_oracle's C2 method against the fp64 oracle."""
-    old = {k: native.get_option(k) for k in (native.OPT_SMALL_PAIR, native.OPT_BN_EPILOGUE)}
-    try:
-        native.set_option(native.OPT_SMALL_PAIR, mode)  # (1: every launch, 3: the backward chain's dX GEMMs)
-        native.set_option(native.OPT_BN_EPILOGUE, bn)
-        test_train_step_vs_oracle("bf16", G, H, L, B, wg, lam, 1, bn)
-    finally:
-        for k, v in old.items():
-            native.set_option(k, v)
-
-
-@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
-def test_gemm_small_pair_bit_identical(layout):
-    """GM2_OPT_SMALL_PAIR on the plain 128x128 bf16 GEMM (gm2_gemm, one pass, no epilogue statistics):
-    the 4-wave 2-stage workgroups produce the 8-wave 4-stage kernel's C bit for bit."""
-    M, N, K = 1024, 768, 1024
-    g = torch.Generator().manual_seed(45)
-    P = torch.randn(M, K, generator=g).to(torch.bfloat16)
-    Q = torch.randn(N, K, generator=g).to(torch.bfloat16)
-    pk, qk = {"nt": (True, True), "nn": (True, False), "tn": (False, False)}[layout]
-    Ps = (P if pk else P.T.contiguous()).cuda()
-    Qs = (Q if qk else Q.T.contiguous()).cuda()
-    old = native.get_option(native.OPT_SMALL_PAIR)
-    outs = []
-    try:
-        for pair in (0, 1):
-            native.set_option(native.OPT_SMALL_PAIR, pair)
-            C = torch.empty(M, N, device="cuda")
-            native.gemm(native.GM2_BF16, Ps, M if not pk else K, Qs, N if not qk else K, C, N, M, N, K, 1, None, pk, qk)
-            torch.cuda.synchronize()
-            outs.append(C.cpu())
-    finally:
-        native.set_option(native.OPT_SMALL_PAIR, old)
-    assert torch.equal(outs[0], outs[1])
-
-
 @pytest.mark.parametrize("G", [20480, 16500])
 def test_backward_schedule_options_bit_identical(G):
     """GM2_OPT_INPUT_CHUNKS (the input-layer weight gradient as four row-quarter launches) and

@@ -89,7 +89,7 @@ def test_header_constants_match_binding():
         native.set_option(native.OPT_SAMPLE_SINGLE_BOUND, 0)
     assert native.get_option(native.OPT_SAMPLE_SINGLE_BOUND) == 250
     # the options pruned in ABI 5 (measured slower or neutral; evidence kept in profiles/) are gone
-    for key in (8, 12, 13, 14, 16, 17, 19):
+    for key in (8, 12, 13, 14, 16, 17, 19, 23):  # (23: round 6's GM2_OPT_SMALL_PAIR, measured and removed)
         with pytest.raises(RuntimeError, match="unknown option"):
             native.set_option(key, 0)
     G, H, L = 55039, 1024, 64
