@@ -54,11 +54,16 @@ __global__ __launch_bounds__(256) void k_count_groups(const uint8_t* __restrict_
 constexpr int kCountRowsPerWg = 16;
 __global__ __launch_bounds__(256) void k_count_groups_rows(const uint8_t* __restrict__ bits, int64_t n, int64_t ldb,
                                                          const int32_t* __restrict__ goff, int ngroups,
-                                                         const int32_t* __restrict__ pos, int32_t* __restrict__ counts) {
+                                                         const int32_t* __restrict__ pos, int32_t* __restrict__ counts,
+                                                         int stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lmask[];  // [ldb / 4] words, then the list
   const int nw = (int)(ldb / 4);
   int* glist = (int*)(lmask + nw);
   int* gcount = glist + ngroups;
+  // (stage: each wave keeps the row it streams in an LDS row buffer [4][ldb], and the listed groups'
+  // byte reads go there instead of back to global memory -- they were ~4x the rows' own bytes)
+  uint8_t* wrow = (uint8_t*)lmask + ((ldb + (int64_t)(ngroups + 1) * 4 + 15) & ~(int64_t)15) +
+                  (int64_t)(threadIdx.x >> 6) * ldb;
   for (int i = threadIdx.x; i < nw; i += 256) lmask[i] = 0u;
   if (threadIdx.x == 0) *gcount = 0;
   __syncthreads();
@@ -90,10 +95,16 @@ __global__ __launch_bounds__(256) void k_count_groups_rows(const uint8_t* __rest
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (i0 + u * 64 >= nw / 4) break;
+        if (stage) ((uint4*)wrow)[i0 + u * 64] = v[u];
         const uint4 k = m[i0 + u * 64];
         c += __builtin_popcount(v[u].x & k.x) + __builtin_popcount(v[u].y & k.y) +
              __builtin_popcount(v[u].z & k.z) + __builtin_popcount(v[u].w & k.w);
       }
+    }
+    const uint8_t* lb = stage ? wrow : rb;
+    if (stage) {  // (this wave's row writes, visible to its own lanes' reads below)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
     }
     for (int j = lane; j < ng; j += 64) {
       const int g = glist[j];
@@ -101,10 +112,11 @@ __global__ __launch_bounds__(256) void k_count_groups_rows(const uint8_t* __rest
       for (int k = goff[g]; k < goff[g + 1] && !any; ++k) {
         const int p = pos[k];
         GM2_DBG(p >= 0 && (int64_t)(p >> 3) < ldb, kDbgMaskPos);
-        any = (rb[p >> 3] >> (p & 7)) & 1;
+        any = (lb[p >> 3] >> (p & 7)) & 1;
       }
       c += any;
     }
+    if (stage) __builtin_amdgcn_wave_barrier();  // (the next row overwrites the buffer after these reads)
     c = wave_sum_i(c);
     if (lane == 0) counts[row] = c;
   }
@@ -195,11 +207,14 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ bit
 void launch_count_groups(const uint8_t* bits, int64_t n, int64_t ldb, const int32_t* goff, int64_t ngroups,
                          const int32_t* pos, int32_t* counts, hipStream_t s) {
   if (n <= 0) return;
-  // (whole-row form when the rows are 16-B pieces and the mask + list fit in 64 KB of LDS)
+  // (whole-row form when the rows are 16-B pieces and the mask + list fit in 64 KB of LDS; each wave's
+  // row buffer too when that still fits)
   const int64_t lds = ldb + (ngroups + 1) * 4;
+  const int64_t lds_stage = ((lds + 15) & ~(int64_t)15) + 4 * ldb;
   if ((ldb & 15) == 0 && (((uintptr_t)bits) & 15) == 0 && lds <= 64 * 1024) {
+    const int stage = lds_stage <= 64 * 1024 ? 1 : 0;
     hipLaunchKernelGGL(k_count_groups_rows, dim3((unsigned)((n + kCountRowsPerWg - 1) / kCountRowsPerWg)), dim3(256),
-                       (unsigned)lds, s, bits, n, ldb, goff, (int)ngroups, pos, counts);
+                       (unsigned)(stage ? lds_stage : lds), s, bits, n, ldb, goff, (int)ngroups, pos, counts, stage);
   } else {
     hipLaunchKernelGGL(k_count_groups, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, bits, n, ldb, goff,
                        (int)ngroups, pos, counts);
