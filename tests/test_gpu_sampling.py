@@ -161,6 +161,55 @@ def test_c3_million_genomes_properties_and_stratified_oracle():
     assert _masks_ok(mask, P, S, zs) == 0
 
 
+def test_c3_trained_checkpoint_stratified_oracle():
+    """Verdict r5 (the headline sample leg is never checked against the oracle): the bench's own
+    sample-leg workload -- a v1 checkpoint (G = 55,039, hidden 512, latent 32) trained 10 epochs at lr
+    1e-3, batch 4096, L1 0.01 on the synthetic 10,000-strain matrix (bench.py train_v1_checkpoint) --
+    decodes 131,072 genomes (two 65,536-genome chunks) into packed masks on the default tiered path.
+    Bars: the single tier carries most tiles (as in the bench line), every row's popcount equals the
+    device's genome size, and 40 stratified rows (first and last of each chunk + 36 seeded random
+    rows) decoded by the oracle from the same checkpoint are bit-exact outside |logit64| <= 1e-3 and
+    equal to the fp64 decision wherever |logit64| > 2e-5."""
+    from gm2.data import ResidentMatrix, StrainLoader, synthetic_pangenome
+    from gm2.model import VAE
+    from gm2.trainer import Adam, StepLR, create_v1_trainer
+    G, H, L, N, chunk = 55039, 512, 32, 131072, 65536
+    torch.manual_seed(11)
+    m = VAE(G, H, L, precision=native.GM2_BF16)
+    opt = Adam(m, lr=1e-3)
+    tr = create_v1_trainer(m, opt, StepLR(opt), 10, 1.0, 0.01)
+    mat = ResidentMatrix(synthetic_pangenome(10000, G, seed=4242))
+    loader = StrainLoader(mat, None, 4096, shuffle=True)
+    for ep in range(10):
+        tr.train_epoch(loader, ep)
+    del mat, loader
+    m.eval()
+    torch.manual_seed(0)
+    z = torch.randn(N, L)
+    st0 = m.decode_stats()
+    pm, _ = m.decode_bits(z.cuda(), chunk=chunk)
+    d = _delta(st0, m.decode_stats())
+    print(f"trained v1 checkpoint (bench workload), {N} genomes: {d}")
+    assert d["split_decodes"] == 2 and d["exact_decodes"] == 0, d
+    assert d["single_tiles"] > d["split_tiles"] + d["exact_tiles"] / 4, d
+    host = pm.bits.cpu().numpy()
+    np.testing.assert_array_equal(np.bitwise_count(host).sum(axis=1, dtype=np.int64), pm.row_sizes())
+    rng = np.random.Generator(np.random.PCG64(21))
+    strata = sorted({0, chunk - 1, chunk, N - 1} | set(int(r) for r in rng.integers(0, N, size=36)))
+    mask = np.unpackbits(host[strata], axis=1, count=G, bitorder="little").astype(bool)
+    P = O.unflatten(m.params.detach().cpu().numpy(), G, H, L)
+    S = {}
+    for i, b in enumerate(O.BNS):
+        S[b + ".running_mean"] = m.bn[i, 0].cpu()
+        S[b + ".running_var"] = m.bn[i, 1].cpu()
+        S[b + ".num_batches_tracked"] = torch.tensor(m.num_batches_tracked[i])
+    zs = z[strata]
+    assert _masks_ok(mask, P, S, zs) == 0
+    l64 = O.decode_logits64(P, S, zs).numpy()
+    dec64 = l64.astype(np.float32) > np.float32(8.940696716308594e-08)
+    assert int(((mask != dec64) & (np.abs(l64) > 2e-5)).sum()) == 0
+
+
 def _stats(m):
     st = m.decode_stats()
     return st["split_decodes"], st["exact_decodes"]
