@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import math
 import os
+import re
 
 import numpy as np
 import torch
@@ -124,12 +125,65 @@ def split_indices(n, test_size=0.3, val_ratio=0.3333, random_state=12345):
     return tr, va, te
 
 
+_INT_CELL = re.compile(rb"-?[0-9]+\Z")
+
+
+def read_matrix_csv(path):
+    """pd.read_csv(path, index_col=0, header=0) for the pan-genome table's own form, parsed with
+    numpy over the file's bytes (pandas' tokenizer takes ~10 s at F4 width, 55,039 x 7,512): a
+    header row of distinct non-empty strain IDs after an empty first cell, then one row per gene
+    (and the 'Lineage' row) of plain integer cells -- the gene rows' single-digit 0 / 1 cells taken
+    by one vectorised check per row. Any other form (quotes, CR line ends, blanks or NA markers,
+    numeric-looking gene names, other cell text) returns pandas' own parse of the file, so the
+    result is always what pandas gives (int64 cells, object index and columns)."""
+    import pandas as pd
+
+    def fallback():
+        return pd.read_csv(path, index_col=0, header=0)
+
+    with open(path, "rb") as f:
+        raw = f.read()
+    if b'"' in raw or b"\r" in raw:
+        return fallback()
+    lines = raw.split(b"\n")
+    if lines and lines[-1] == b"":
+        lines.pop()
+    head = lines[0].split(b",") if lines else []
+    cols = [h.decode() for h in head[1:]]
+    n = len(cols)
+    if len(lines) < 2 or head[0] != b"" or n == 0 or "" in cols or len(set(cols)) != n:
+        return fallback()
+    names, vals = [], np.empty((len(lines) - 1, n), dtype=np.int64)
+    for i, ln in enumerate(lines[1:]):
+        k = ln.find(b",")
+        name = ln[:k]
+        if k <= 0 or _INT_CELL.match(name) or name.strip() != name or name.upper() in _NA_NAMES:
+            return fallback()
+        names.append(name.decode())
+        body = np.frombuffer(ln, dtype=np.uint8)[k + 1:]
+        if body.size == 2 * n - 1 and (body[1::2] == 44).all():
+            d = body[0::2] - 48  # (uint8: any byte below '0' wraps above 1)
+            if (d <= 1).all():
+                vals[i] = d
+                continue
+        parts = ln[k + 1:].split(b",")
+        if len(parts) != n or not all(_INT_CELL.match(c) for c in parts):
+            return fallback()
+        vals[i] = [int(c) for c in parts]
+    return pd.DataFrame(vals, index=pd.Index(names, dtype=object), columns=pd.Index(cols, dtype=object))
+
+
+# pandas' default NA markers (read_csv na_values), upper-cased: an index cell equal to one is NaN there
+_NA_NAMES = {b"", b"#N/A", b"#N/A N/A", b"#NA", b"-1.#IND", b"-1.#QNAN", b"-NAN", b"1.#IND", b"1.#QNAN",
+             b"<NA>", b"N/A", b"NA", b"NULL", b"NAN", b"NONE"}
+
+
 def load_and_validate_data(dataset_csv, phylogroups_csv):
     """(large_data, merged_df, data_without_lineage) as data_exploration.py:54-107: genes x strains
     CSV (index_col=0), strain IDs upper-cased, 'Lineage' row dropped, transposed and inner-merged
     with the phylogroup table on ID."""
     import pandas as pd
-    large = pd.read_csv(dataset_csv, index_col=0, header=0)
+    large = read_matrix_csv(dataset_csv)
     large.columns = large.columns.str.upper()
     phylo = pd.read_csv(phylogroups_csv, index_col=0, header=0)
     without = large.drop(index=["Lineage"], errors="ignore")
