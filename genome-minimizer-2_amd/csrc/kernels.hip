@@ -1240,12 +1240,15 @@ __device__ __forceinline__ void band_fix_one(const uint2 rg, bool valid, int lan
 
 // workgroups [0, kBandFixShardWgs): the shards (wave w takes shard w % kBandShards, its entries
 // 4 (w / kBandShards) + group, + 4 waves / kBandShards, ...); the rest: one wave per tile's slots,
-// four entries at a time
+// four entries at a time, four consecutive tiles (row-major: one genome-row block) per workgroup.
+// xcd: consecutive workgroups of ONE XCD take consecutive tile quads (the dispatcher deals
+// workgroups round-robin over the 8 XCDs), so the activation rows of a row block's band entries --
+// each row recurs in the lists of ~1/4 of its row's 215 tiles -- are fetched into one L2, not eight
 constexpr int kBandFixShardWgs = 256;
 __global__ __launch_bounds__(256) void k_band_fix(MaskBand band, int ntiles, const float* __restrict__ A, int64_t lda,
                                                 const float* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
                                                 int H, uint8_t* bits, int64_t ldb, uint8_t* mask, int64_t ldm,
-                                                unsigned* flips) {
+                                                unsigned* flips, int xcd) {
   const int lane = threadIdx.x & 63, grp = lane >> 4;
   if (blockIdx.x < kBandFixShardWgs) {
     const unsigned wave = blockIdx.x * 4 + (threadIdx.x >> 6), waves = kBandFixShardWgs * 4;
@@ -1260,7 +1263,13 @@ __global__ __launch_bounds__(256) void k_band_fix(MaskBand band, int ntiles, con
     }
     return;
   }
-  const int t = (blockIdx.x - kBandFixShardWgs) * 4 + (threadIdx.x >> 6);
+  const int nb = (int)gridDim.x - kBandFixShardWgs, b = (int)blockIdx.x - kBandFixShardWgs;
+  int lb = b;
+  if (xcd) {  // (kBandFixShardWgs % 8 == 0: b's XCD is blockIdx's)
+    const int q = nb >> 3, r = nb & 7, x = b & 7;
+    lb = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  }
+  const int t = lb * 4 + (threadIdx.x >> 6);
   if (t >= ntiles) return;
   const unsigned n = min(band.tcount[t], (unsigned)band.tslots);
   const uint2* tl = band.tlist + (size_t)t * band.tslots;
@@ -1600,9 +1609,12 @@ void launch_band_fix(const MaskBand& band, int ntiles, const float* A, int64_t l
     throw Gm2Error("band fix: shard list and counters (and tile slots for %d tiles) required", ntiles);
   // (a fixed grid for the shards, the counts live on the device: 16 waves per shard; then one wave per tile)
   static_assert((kBandFixShardWgs * 4) % kBandShards == 0, "band fix grid");
+  static_assert(kBandFixShardWgs % 8 == 0, "band fix: XCD-aware tile order");
   const unsigned grid = kBandFixShardWgs + (unsigned)((ntiles + 3) / 4);
+  // env GM2_BANDFIX_LINEAR=1: tile quads in dispatch order (A/B of the XCD-aware order)
+  static const int xcd = std::getenv("GM2_BANDFIX_LINEAR") ? 0 : 1;
   hipLaunchKernelGGL(k_band_fix, dim3(grid), dim3(256), 0, s, band, ntiles, A, lda, W, ldw, bias, H, bits, ldb, mask,
-                     ldm, flips);
+                     ldm, flips, xcd);
   GM2_CHECK_LAUNCH();
 }
 
