@@ -1273,12 +1273,15 @@ struct BandCols {
   }
 };
 
-// a band entry past its shard's capacity: its 256 x 256 block is flagged (the first lane to flag it
-// lists it) for k_band_tile_fix's whole-block fp64 recompute
-__device__ __forceinline__ void band_spill(const MaskBand& b, unsigned r, unsigned gcol) {
-  const unsigned blk = (r >> 8) * (unsigned)b.obn + (gcol >> 8);
-  GM2_DBG(blk < b.oblocks && (int)(gcol >> 8) < b.obn, kDbgBandBlock);
-  if (blk >= b.oblocks) return;  // (cannot happen: the epilogues flag rows < M, genes < N only)
+// A band entry past its shard's capacity only sets the lane's `ovf`; after its epilogue the tile
+// flags the 256 x 256 block it lies in (the first lane to flag it lists it) for k_band_tile_fix's
+// whole-block fp64 recompute. (Flagging at each of the unrolled epilogue's 128 append sites had grown
+// the bit-packing mask kernel from 120 to 208 KB of code and its launch from 5.0 to 5.7 ms: an
+// instruction-cache cost, profiles/r06_mask_code_size_ab.txt.)
+__device__ __forceinline__ void band_spill_block(const MaskBand& b, int m0, int n0) {
+  const unsigned blk = (unsigned)(m0 >> 8) * (unsigned)b.obn + (unsigned)(n0 >> 8);
+  GM2_DBG(blk < b.oblocks && (n0 >> 8) < b.obn, kDbgBandBlock);
+  if (blk >= b.oblocks) return;  // (cannot happen: tiles lie inside the block grid)
   if (atomicExch(b.oflag + blk, 1u) == 0u) b.olist[atomicAdd(b.ocount, 1u)] = blk;
 }
 
@@ -1286,7 +1289,7 @@ __device__ __forceinline__ void band_spill(const MaskBand& b, unsigned r, unsign
 // fixed order; per position with flagged lanes, one reservation for all of them (an LDS counter
 // for the tile's slots, else the shard's counter) and each flagged lane's entry at its prefix
 template <class C, class F>
-__device__ __forceinline__ void band_walk(const MaskBand& b, int tile, char* smem, int lane, F&& walk) {
+__device__ __forceinline__ void band_walk(const MaskBand& b, int tile, char* smem, int lane, bool& ovf, F&& walk) {
   unsigned* lcount = (unsigned*)(smem + C::LDS) + C::BM + C::BN;
   const int sh = blockIdx.x % kBandShards;
   uint2* shard = b.list + (size_t)sh * b.cap;
@@ -1301,13 +1304,13 @@ __device__ __forceinline__ void band_walk(const MaskBand& b, int tile, char* sme
     const uint2 e = make_uint2((unsigned)r, (unsigned)gcol);
     if (!b.tslots) {
       if (i < b.cap) shard[i] = e;
-      else band_spill(b, e.x, e.y);
+      else ovf = true;
     } else if (i < (unsigned)b.tslots) {
       b.tlist[(size_t)tile * b.tslots + i] = e;
     } else if (!b.drop_overflow) {  // past the tile's slots: the shard (rare)
       const unsigned k = atomicAdd(b.counts + sh, 1u);
       if (k < b.cap) shard[k] = e;
-      else band_spill(b, e.x, e.y);
+      else ovf = true;
     }
   });
 }
@@ -1315,7 +1318,7 @@ __device__ __forceinline__ void band_walk(const MaskBand& b, int tile, char* sme
 // reservation for all of them, as band_walk's visitor
 template <class C>
 __device__ __forceinline__ void band_add(const MaskBand& b, int tile, char* smem, int lane, uint64_t bal, bool in,
-                                         int r, int gcol) {
+                                         int r, int gcol, bool& ovf) {
   unsigned* lcount = (unsigned*)(smem + C::LDS) + C::BM + C::BN;
   const int sh = blockIdx.x % kBandShards;
   const unsigned pre = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
@@ -1327,13 +1330,13 @@ __device__ __forceinline__ void band_add(const MaskBand& b, int tile, char* smem
   uint2* shard = b.list + (size_t)sh * b.cap;
   if (!b.tslots) {
     if (i < b.cap) shard[i] = e;
-    else band_spill(b, e.x, e.y);
+    else ovf = true;
   } else if (i < (unsigned)b.tslots) {
     b.tlist[(size_t)tile * b.tslots + i] = e;
   } else if (!b.drop_overflow) {
     const unsigned k = atomicAdd(b.counts + sh, 1u);
     if (k < b.cap) shard[k] = e;
-    else band_spill(b, e.x, e.y);
+    else ovf = true;
   }
 }
 
@@ -1451,6 +1454,7 @@ __device__ __forceinline__ void mask_tile(const TileXY tl, const GemmArgs<T>& g,
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / C::WGN, wn = wid % C::WGN;
   const BandCols<C> bc(bias, brn, o.band, bchk, tl.n0, g.N, lane, wn);
   uint64_t bandw = 0;  // this wave's band flags, OR-ed over its fragment positions
+  bool ovf = false;    // an entry of this lane's found its shard full (band_spill_block)
   if constexpr (BITS) {
     static_assert(PP, "bit-image epilogue: the split decode's kernel");
     {
@@ -1478,13 +1482,14 @@ __device__ __forceinline__ void mask_tile(const TileXY tl, const GemmArgs<T>& g,
             // the band elements of this position appended at once (a uniform branch, rarely taken)
             const bool inb = fabsf(d) <= e[ni] && rok;
             const uint64_t bb = __ballot(inb);
-            if (bb) band_add<C>(o.band, tl.t, smem, lane, bb, inb, r, tl.n0 + wn * C::WTN + ni * 16 + (lane & 15));
+            if (bb) band_add<C>(o.band, tl.t, smem, lane, bb, inb, r, tl.n0 + wn * C::WTN + ni * 16 + (lane & 15), ovf);
           }
           if (lane < 4)
             *(uint64_t*)(smem + (wm * C::WTM + mi * 16 + 4 * lane + j) * (C::BN / 8) + wn * (C::WTN / 8)) = rb;
           __builtin_amdgcn_sched_barrier(0);  // (one row quad at a time: the ballots' SGPR pairs stay few)
         }
       }
+      if (ovf) band_spill_block(o.band, tl.m0, tl.n0);
       __syncthreads();
       band_close<C>(o.band, tl.t, smem);
       constexpr int BPR = C::BN / 8;
@@ -1524,7 +1529,7 @@ __device__ __forceinline__ void mask_tile(const TileXY tl, const GemmArgs<T>& g,
     }
   }
   if (bandw) {  // append this wave's band elements (unrolled: acc stays in registers)
-    band_walk<C>(o.band, tl.t, smem, lane, [&](auto&& visit) {
+    band_walk<C>(o.band, tl.t, smem, lane, ovf, [&](auto&& visit) {
 #pragma unroll
       for (int mi = 0; mi < C::FM; ++mi) {
         float e[C::FN];
@@ -1540,6 +1545,7 @@ __device__ __forceinline__ void mask_tile(const TileXY tl, const GemmArgs<T>& g,
       }
     });
   }
+  if (ovf) band_spill_block(o.band, tl.m0, tl.n0);
   __syncthreads();
   band_close<C>(o.band, tl.t, smem);
   const int rows = min(C::BM, g.M - tl.m0);
