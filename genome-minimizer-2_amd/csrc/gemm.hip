@@ -1494,10 +1494,44 @@ __device__ __forceinline__ void mask_tile(const TileXY tl, const GemmArgs<T>& g,
       band_close<C>(o.band, tl.t, smem);
       constexpr int BPR = C::BN / 8;
       const int rows = min(C::BM, g.M - tl.m0);
-      for (int i = threadIdx.x; i < rows * (BPR / 16); i += C::NT) {
-        const int r = i / (BPR / 16), cc = i % (BPR / 16);
-        if (tl.n0 / 8 + cc * 16 >= o.ldb) continue;  // (pad genes past the row pitch: all zero)
-        *(uint4*)(o.bits + (int64_t)(tl.m0 + r) * o.ldb + tl.n0 / 8 + cc * 16) = *(const uint4*)(smem + r * BPR + cc * 16);
+      if (o.bits) {
+        for (int i = threadIdx.x; i < rows * (BPR / 16); i += C::NT) {
+          const int r = i / (BPR / 16), cc = i % (BPR / 16);
+          if (tl.n0 / 8 + cc * 16 >= o.ldb) continue;  // (pad genes past the row pitch: all zero)
+          *(uint4*)(o.bits + (int64_t)(tl.m0 + r) * o.ldb + tl.n0 / 8 + cc * 16) = *(const uint4*)(smem + r * BPR + cc * 16);
+        }
+      }
+      if (o.mask) {
+        // u8 masks expanded from the bit image (gm2_decode_mask): one lane per 4-B aligned dword of a
+        // row's 256-byte segment, so a wave instruction writes one row's bytes contiguously at any row
+        // alignment (the rows of a [n][G] mask are not 16-B aligned at odd G; the byte image's write-out
+        // took one byte store per element there); the partial dwords at the segment's two ends and at
+        // the gene edge by bytes (the neighbouring tiles own the rest of those dwords)
+        static_assert(BPR == 32, "eight bit words per tile row");
+        const int cols = min(C::BN, g.N - tl.n0);
+        for (int r = wid; r < rows; r += C::NT / 64) {
+          uint8_t* row = o.mask + (int64_t)(tl.m0 + r) * o.ldm + tl.n0;
+          const int a = (int)((uintptr_t)row & 3);
+          const uint32_t* bw = (const uint32_t*)(smem + r * BPR);
+          for (int k = lane; k < 64 + (a != 0); k += 64) {
+            const int c0 = 4 * k - a;  // tile column of the dword's first byte (-a at k = 0)
+            uint32_t x;                // its four mask bits
+            if (c0 < 0) {
+              x = (bw[0] << a) & 0xFu;
+            } else {
+              const int q = c0 >> 5;
+              const uint64_t w = (uint64_t)bw[q] | ((uint64_t)(q + 1 < 8 ? bw[q + 1] : 0u) << 32);
+              x = (uint32_t)(w >> (c0 & 31)) & 0xFu;
+            }
+            if (c0 >= 0 && c0 + 3 < cols) {
+              *(uint32_t*)(row + c0) = (x * 0x00204081u) & 0x01010101u;  // (row - a + 4k: aligned)
+            } else {
+#pragma unroll
+              for (int t = 0; t < 4; ++t)
+                if (c0 + t >= 0 && c0 + t < cols) row[c0 + t] = (uint8_t)((x >> t) & 1u);
+            }
+          }
+        }
       }
       return;
     }
@@ -2051,8 +2085,10 @@ void launch_gemm_mask_tiered(const GemmArgs<bf16_t>& g1, const GemmArgs<bf16_t>&
     ensure_lds_attr((const void*)kern, lds);
     hipLaunchKernelGGL(kern, grid, dim3(Big::NT), lds, s, g1, g3, bias, o1, o3);
   };
-  if (bits && !mask) go(k_gemm_mask_tiered<Big, bf16_t, true>);
-  else go(k_gemm_mask_tiered<Big, bf16_t, false>);
+  // (packed bits and u8 masks both leave the bit-image epilogue: its ballots replace the byte image's
+  // per-element LDS stores; the u8 form through k_gemm_mask_tiered<..., false> measured 11.7 vs 5.3 ms
+  // per 65,536-genome chunk, profiles/r06_decode_u8_ab.txt)
+  go(k_gemm_mask_tiered<Big, bf16_t, true>);
   GM2_CHECK_LAUNCH();
 }
 
