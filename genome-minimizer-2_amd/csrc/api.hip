@@ -126,6 +126,9 @@ struct Layout {
   // per-block flags, then [tiles] the listed block ids. Words [4, 64 + tiles) zeroed per decode.
   int64_t s3ovf;
   static constexpr int kOvfCount = 4, kOvfFlags = 64;
+  // u8 masks of the gated decode (gm2_decode_mask): its packed bits [roundup(Bm, 256)][s3ldb], expanded
+  // to the caller's rows by one streaming pass (k_expand_bits)
+  int64_t s3bits, s3ldb;
   int64_t adamscal;            // scalar block of a queued output-layer Adam update
   int64_t ridx;                // zero-copy rows: int32 [roundup(Bm, 256)] resident-matrix row per batch row
 };
@@ -214,6 +217,8 @@ Layout make_layout(const gm2_dims* gd, int prec) {
   o.s3a1 = take(split3 ? round_up(Bm, 2 * kTile) * H * 2 : 0);
   o.s3w1 = take(split3 ? round_up(d.G, 2 * kTile) * H * 2 : 0);
   o.s3ovf = take(split3 ? (Layout::kOvfFlags + 2 * s3tiles) * 4 : 0);
+  o.s3ldb = split3 ? round_up(d.G, 2 * kTile) / 8 : 0;
+  o.s3bits = take(split3 ? round_up(Bm, 2 * kTile) * o.s3ldb : 0);
   o.adamscal = take(GM2_NUM_SCALARS * 4);
   o.ridx = take(round_up(Bm, 2 * kTile) * 4);
   o.total = cur;
@@ -991,6 +996,17 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
   if ((((uintptr_t)(prm + d.off[D9W])) | ((uintptr_t)c.f(l.A[5]))) & 15) return false;
   if (bits && ((ldb & 15) || (((uintptr_t)bits) & 15) || ldb * 8 < d.Gp)) return false;
   if (mask && !bits && (ldm < G)) return false;
+  // u8 masks alone: the decode writes packed bits into the workspace and k_expand_bits writes the
+  // caller's rows from them in one streaming pass (the tile epilogue's own u8 rows, at odd G never
+  // 16-B aligned, cost 3.4 ms more per 65,536-genome chunk, profiles/r06_decode_u8_ab.txt)
+  uint8_t* mask_out = nullptr;
+  if (mask && !bits) {
+    if (!l.s3bits || l.s3ldb * 8 < d.Gp) return false;
+    mask_out = mask;
+    mask = nullptr;
+    bits = (uint8_t*)(c.ws + l.s3bits);
+    ldb = l.s3ldb;
+  }
   unsigned* ctl = (unsigned*)(c.ws + l.s3ctl);
   unsigned* ablk = ctl + DecodeCtl::kBlk;
   unsigned* wblk = ablk + Bq / 256;
@@ -1069,6 +1085,7 @@ bool decode_split3(const Ctx<float>& c, const float* prm, int n, uint8_t* mask, 
   launch_decode_stats(ctl + DecodeCtl::kTilesSplit, ctl + DecodeCtl::kTilesExact, ctl + DecodeCtl::kTilesSingle,
                       ctl + DecodeCtl::kCounts, ctl + DecodeCtl::kTileFound, ctl + DecodeCtl::kFlips, bs.cap,
                       (unsigned long long*)(ctl + DecodeCtl::kCum), bs.ocount, (unsigned long long*)ovf, c.s);
+  if (mask_out) launch_expand_bits(bits, ldb, n, G, mask_out, ldm, c.s);
   return true;
 }
 
@@ -1730,7 +1747,7 @@ int gm2_debug_check_layout(const gm2_dims* d, int precision, int64_t* n_regions,
                              o.slabs, o.side_slabs, o.DA, o.dH, o.AT5, o.dYT0, o.bnpart, o.colpart, o.losspart,
                              o.klpart, o.gradpart, o.colbwd, o.nahdr, o.nasq, o.clip, o.scal0, o.X1, o.XB1, o.syncb,
                              o.s3a, o.s3w, o.s3rn, o.s3cn, o.s3ctl, o.s3band, o.s3tlist, o.s3tcount, o.s3a1, o.s3w1,
-                             o.adamscal, o.ridx};
+                             o.s3ovf, o.s3bits, o.adamscal, o.ridx};
     auto known = [&](int64_t off) {
       for (const auto& x : r)
         if (x.first == off) return true;

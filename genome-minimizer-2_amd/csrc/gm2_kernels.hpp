@@ -295,6 +295,8 @@ void launch_band_tile_fix(const MaskBand& band, const float* A, int64_t lda, con
                           int64_t ldm, unsigned* flips, hipStream_t s);
 // one workgroup: the decode call's per-call counters -> the workspace's cumulative ones (DecodeCtl);
 // ocount / ocum: the blocks k_band_tile_fix recomputed this call -> their cumulative count
+// packed mask bits [n][ldb] (bit g % 8 of byte g / 8) -> u8 [n][ldm] (0 / 1), any row alignment
+void launch_expand_bits(const uint8_t* bits, int64_t ldb, int n, int G, uint8_t* out, int64_t ldm, hipStream_t s);
 void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* tiles_single,
                          const unsigned* counts, const unsigned* tfound, const unsigned* flips, unsigned cap,
                          unsigned long long* cum, const unsigned* ocount, unsigned long long* ocum, hipStream_t s);

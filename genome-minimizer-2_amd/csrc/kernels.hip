@@ -1618,6 +1618,52 @@ void launch_band_fix(const MaskBand& band, int ntiles, const float* A, int64_t l
   GM2_CHECK_LAUNCH();
 }
 
+// packed mask bits (bit g % 8 of byte g / 8, rows of ldb bytes) -> u8 rows of ldm bytes at any
+// alignment (gm2_decode_mask): a workgroup per row at a time -- the row's packed bytes staged in LDS
+// by 16-B loads, then one thread per 4-B aligned output dword (the first and last dwords of a row,
+// shared with its neighbours, by bytes), so every wave instruction writes 256 contiguous bytes
+__global__ __launch_bounds__(256) void k_expand_bits(const uint8_t* __restrict__ bits, int64_t ldb, int n, int G,
+                                                   uint8_t* __restrict__ out, int64_t ldm) {
+  extern __shared__ __attribute__((aligned(16))) char lrow[];
+  const int nb = (G + 7) / 8, nv = (nb + 15) / 16;  // packed bytes of a row, 16-B pieces
+  for (int r = blockIdx.x; r < n; r += gridDim.x) {
+    const uint8_t* br = bits + (int64_t)r * ldb;
+    __syncthreads();  // (the previous row's reads of lrow are done)
+    for (int v = threadIdx.x; v < nv; v += 256) *(uint4*)(lrow + 16 * v) = *(const uint4*)(br + 16 * v);
+    __syncthreads();
+    uint8_t* row = out + (int64_t)r * ldm;
+    const int a = (int)((uintptr_t)row & 3);
+    const int nd = (G + a + 3) / 4;
+    for (int k = threadIdx.x; k < nd; k += 256) {
+      const int c0 = 4 * k - a;  // the dword's first column (-a at k = 0: those bytes are the row before's)
+      uint32_t x = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int c = c0 + t;
+        if (c >= 0 && c < G) x |= ((uint32_t)((uint8_t)lrow[c >> 3] >> (c & 7)) & 1u) << t;
+      }
+      if (c0 >= 0 && c0 + 3 < G) {
+        *(uint32_t*)(row + c0) = (x * 0x00204081u) & 0x01010101u;  // (row - a + 4k: aligned)
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (c0 + t >= 0 && c0 + t < G) row[c0 + t] = (uint8_t)((x >> t) & 1u);
+      }
+    }
+  }
+}
+
+void launch_expand_bits(const uint8_t* bits, int64_t ldb, int n, int G, uint8_t* out, int64_t ldm, hipStream_t s) {
+  if (!bits || !out || n < 0 || G < 0 || ldb * 8 < G || ldm < G) throw Gm2Error("expand bits: bad rows");
+  const int64_t lds = round_up((G + 7) / 8, 16);
+  if (ldb < lds || (ldb & 15) || (((uintptr_t)bits) & 15)) throw Gm2Error("expand bits: rows must be 16-B pieces");
+  if (lds > 64 * 1024) throw Gm2Error("expand bits: %lld genes per row", (long long)G);
+  if (n == 0 || G == 0) return;
+  hipLaunchKernelGGL(k_expand_bits, dim3((unsigned)std::min(n, 4096)), dim3(256), (unsigned)lds, s, bits, ldb, n, G,
+                     out, ldm);
+  GM2_CHECK_LAUNCH();
+}
+
 void launch_decode_stats(const unsigned* tiles_split, const unsigned* tiles_exact, const unsigned* tiles_single,
                          const unsigned* counts, const unsigned* tfound, const unsigned* flips, unsigned cap,
                          unsigned long long* cum, const unsigned* ocount, unsigned long long* ocum, hipStream_t s) {
