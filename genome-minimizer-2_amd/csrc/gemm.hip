@@ -1276,8 +1276,8 @@ struct BandCols {
 // A band entry past its shard's capacity only sets the lane's `ovf`; after its epilogue the tile
 // flags the 256 x 256 block it lies in (the first lane to flag it lists it) for k_band_tile_fix's
 // whole-block fp64 recompute. (Flagging at each of the unrolled epilogue's 128 append sites had grown
-// the bit-packing mask kernel from 120 to 208 KB of code and its launch from 5.0 to 5.7 ms: an
-// instruction-cache cost, profiles/r06_mask_code_size_ab.txt.)
+// the bit-packing mask kernel from 120 to 208 KB of code and its launch from 5.0 to 5.7 ms; deferring
+// every append to one rolled loop, 49 KB, measured 5.4 ms: profiles/r06_mask_code_size_ab.txt.)
 __device__ __forceinline__ void band_spill_block(const MaskBand& b, int m0, int n0) {
   const unsigned blk = (unsigned)(m0 >> 8) * (unsigned)b.obn + (unsigned)(n0 >> 8);
   GM2_DBG(blk < b.oblocks && (n0 >> 8) < b.obn, kDbgBandBlock);
